@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""Headline bench: edges/s (fwd+bwd) of hetero message passing on MI355X (BASELINE.json).
+
+Workload (N=1): BASELINE config 2 — synthetic user<->post graph, 1M users / 100k posts / 20M
+engages (+ the 20M reverse relation), d = h = 64, 2-layer relation-weighted SAGE
+(``HeteroSAGE`` = the reference ``WeightedRGCN`` layer stacked twice).  One step = one training
+step of ``train_gnn.py:242-285``: forward, the reference link loss over all 20M positive edges
+with fresh ``torch.randint`` negatives, full backward, Adam.  Inputs resident in HBM before the
+timed region.  Metric numerator = sum over layers and relations of E_r = 80M edges/step.
+
+N>1 (``torch.distributed.run``): weak scaling — each rank owns one cfg2-sized destination shard
+(its own seeded graph), runs the same step, and the weight gradients are all-reduced over RCCL
+before the optimizer step (the only exchange this layout has).  value = all ranks' edges /
+max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with ``roofline`` for the dominant kernel (the K1 forward gather:
+algorithmic bytes per launch / HIP-event-timed duration inside the timed region) and
+``cpu_baseline`` (the plain-torch CPU oracle on a bounded sample, rank 0 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from truth_recommendation_gnn_amd import HeteroSAGE, ops, synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="cfg2")
+    p.add_argument("--scale", type=float, default=1.0, help="shrink the config (debug only)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--profile-steps", action="store_true",
+                   help="no per-kernel events (for rocprofv3 runs)")
+    return p.parse_args()
+
+
+def build(cfg, device, rank):
+    g = synth.make_graph(cfg, device=device)
+    if rank:  # a different destination shard per rank: reseed the edges
+        gen = torch.Generator(device=device).manual_seed(1000 + rank)
+        ei = g.edge_index_dict[synth.ENGAGES]
+        perm = torch.randperm(cfg.num_users, generator=gen, device=device)
+        ei = torch.stack([perm[ei[0]], ei[1]])
+        g.edge_index_dict[synth.ENGAGES] = ei
+        g.edge_index_dict[synth.REV_ENGAGES] = ei.flip(0)
+    return g
+
+
+def cpu_baseline(cfg, threads):
+    """Oracle (plain torch CPU, PyG's op pattern) on a bounded cfg sample; edges/s."""
+    from oracle import sage_ref
+    torch.set_num_threads(threads)
+    sample = synth.scaled(cfg.name, 0.05) if cfg.num_engages > 1_000_000 else cfg
+    g = synth.make_graph(sample)
+    names = []
+    for l in range(sample.layers):
+        cin = sample.dim if l == 0 else sample.hidden
+        for et, _ in RELATIONS:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (sample.hidden, cin)), (f"{p}.lin_l.bias", (sample.hidden,)),
+                      (f"{p}.lin_r.weight", (sample.hidden, cin))]
+    params = {k: v.requires_grad_() for k, v in sage_ref.init_params(names).items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    pos = g.edge_index_dict[synth.ENGAGES]
+    pw = synth.interaction_weights(sample.num_posts)[pos[1]]
+
+    def step():
+        opt.zero_grad()
+        out = sage_ref.hetero_sage(params, g.x_dict, g.edge_index_dict, RELATIONS, sample.layers)
+        neg = torch.randint(0, sample.num_posts, (pos.shape[1],))
+        loss = sage_ref.link_loss(out["user"], out["post"], pos, neg, pw)
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        step()
+        n += 1
+        if time.perf_counter() - t0 > 10.0 or n >= 5:
+            break
+    dt = (time.perf_counter() - t0) / n
+    edges = sample.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
+    return {"value": edges / dt, "unit": "edges/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{sample.name}: U={sample.num_users} P={sample.num_posts} "
+                      f"E_engage={sample.num_engages} d={sample.dim}, {sample.layers}-layer fwd+loss+"
+                      f"bwd+Adam, mean of {n} steps after 1 warmup (oracle/sage_ref.py, torch CPU)"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = synth.CONFIGS[args.config]
+    if args.scale != 1.0:
+        cfg = synth.scaled(args.config, args.scale)
+    g = build(cfg, dev, rank)
+    pos = g.edge_index_dict[synth.ENGAGES]
+    pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
+    torch.manual_seed(synth.WEIGHT_SEED)
+    model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers).to(dev)
+    with torch.no_grad():
+        model(g.x_dict, g.edge_index_dict)      # materialise lazy weights, build + cache CSR/CSC
+    if world > 1:
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED + rank)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        out = model(g.x_dict, g.edge_index_dict)
+        neg = torch.randint(0, cfg.num_posts, (pos.shape[1],), device=dev, generator=gen)
+        loss = ops.link_loss(out["user"], out["post"], pos, neg, pw)
+        loss.backward()
+        if world > 1:
+            flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+            dist.all_reduce(flat)
+            flat /= world
+            o = 0
+            for p in model.parameters():
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p))
+                o += n
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    timer = None if args.profile_steps else ops.KernelTimer()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ops.set_timer(timer)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ops.set_timer(None)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed)
+    edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
+    value = edges_step * args.steps * world / elapsed
+    kern = timer.summary() if timer else {}
+    if rank == 0:
+        roof = None
+        fwd = {k: v for k, v in kern.items() if k.startswith("gather_fwd")}
+        if fwd:
+            name, r = max(fwd.items(), key=lambda kv: kv[1]["ms"])
+            per_launch_ms = r["ms"] / r["launches"]
+            per_launch_bytes = r["bytes"] / r["launches"]
+            ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": f"k_gather ({name}: K1 mean gather, fwd)",
+                    "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "avg_launch_us": round(per_launch_ms * 1e3, 1),
+                    "algorithmic_bytes_per_launch": int(per_launch_bytes)}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(cfg, args.cpu_threads)
+        line = {
+            "metric": "edges/s (fwd+bwd) hetero message-passing",
+            "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded numpy PCG64 graph, Zipf post degrees; random-init weights)",
+            "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
+                                   f"E_engage={cfg.num_engages} (+reverse), d=h={cfg.dim}, "
+                                   f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
+                       "edges_per_step": edges_step, "global_batch": edges_step * world,
+                       "parallelism": f"dst-shard x{world}" if world > 1 else "single"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
+                            "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+                        for k, v in sorted(kern.items())},
+            "loss": float(loss),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

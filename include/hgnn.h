@@ -1,0 +1,117 @@
+/* hgnn — MI355X (gfx950) hetero message-passing hot path, C ABI.
+ *
+ * Drop-in boundary for the per-relation SAGE aggregation the reference reaches through PyG
+ * (SAGEConv((-1,-1), h) at train_gnn.py:158-160, called at train_gnn.py:177-198,
+ * inference.py:143-166, test_gnn.py:141-166).  The reference has no FFI of its own (it is
+ * pure Python over torch_geometric), so each entry point below names the PyG/ATen
+ * step it replaces; INTEGRATION.md shows the ctypes binding a maintainer adds.
+ *
+ * Conventions
+ *   - every pointer is DEVICE memory owned by the caller (PyTorch's caching allocator in the
+ *     shipped host code); the library allocates nothing persistent, scratch comes in `ws`;
+ *   - all work is stream-ordered on `stream` (a hipStream_t passed as void*); no host syncs,
+ *     no hipMalloc/hipFree inside, so every call can be captured into a hipGraph;
+ *   - row-major fp32 feature tables ([rows, d] contiguous); int32 CSR; int64 COO inputs;
+ *   - return 0 (HGNN_OK) or an HGNN_E_* code; hgnn_last_error_string() (thread-local) says why.
+ */
+#ifndef HGNN_H_
+#define HGNN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGNN_OK 0
+#define HGNN_E_ARG 1001         /* bad shape / null pointer / size out of range */
+#define HGNN_E_HIP 1002         /* a HIP runtime error (launch failure) */
+#define HGNN_E_WS 1003          /* workspace too small */
+#define HGNN_E_UNSUPPORTED 1004 /* shape outside what the kernels implement */
+
+#define HGNN_MEAN 1        /* multiply each row sum by 1/deg (deg 0 -> 0) */
+#define HGNN_ACCUMULATE 2  /* out += result instead of out = result */
+
+#define HGNN_MAX_SEG 6     /* input segments of one fused linear */
+
+typedef void* hgnn_stream_t; /* hipStream_t */
+
+int hgnn_version(void);
+const char* hgnn_last_error_string(void);
+
+/* ---- K5: COO -> CSR, stable (each row keeps the COO edge order) -------------------------------
+ * Replaces PyG's implicit scatter over unsorted COO (train_gnn.py:28,55 keep edges chronological;
+ * train_gnn.py:128-133 masks out-of-range ids, train_gnn.py:142 flips for rev_engages).
+ * Groups edges by key (dst for the forward CSR, src for the backward CSC):
+ *   rowptr[n_keys+1], col[e] = other[perm[e]], perm[e] = original edge id.
+ * Edges whose key is outside [0,n_keys) or whose other is outside [0,n_other) are dropped (sorted
+ * to the end, excluded from rowptr); their count is written to *d_invalid (device int32).
+ * E < 2^31.  Workspace: hgnn_coo_to_csr_ws_bytes(E, n_keys). */
+size_t hgnn_coo_to_csr_ws_bytes(int64_t E, int64_t n_keys);
+int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t n_keys,
+                    int64_t n_other, int32_t* rowptr, int32_t* col, int32_t* perm,
+                    int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
+/* ---- degree-skew plan ----------------------------------------------------------------------
+ * Rows with more than `chunk` edges are split into ceil(deg/chunk) chunks, each summed by its own
+ * wave into a partial slot, then reduced in chunk order (deterministic).  Two phases so the host
+ * can size the plan: count writes {n_heavy, n_chunks} to d_counts2 (device int32[2]). */
+size_t hgnn_plan_ws_bytes(int64_t n_rows);
+int hgnn_plan_count(const int32_t* rowptr, int64_t n_rows, int32_t chunk, int32_t* d_counts2,
+                    void* ws, size_t ws_bytes, hgnn_stream_t stream);
+int hgnn_plan_fill(const int32_t* rowptr, int64_t n_rows, int32_t chunk, int32_t* heavy_rows,
+                   int32_t* heavy_first, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+/* inv_deg[i] = 1/(rowptr[i+1]-rowptr[i]) or 0 for an empty row. */
+int hgnn_inv_degree(const int32_t* rowptr, int64_t n_rows, float* inv_deg, hgnn_stream_t stream);
+
+/* ---- K1/K2: segmented gather-reduce over a CSR ----------------------------------------------
+ *   out[i,:] (+)= s_i * sum_{p in [rowptr[i],rowptr[i+1])} w_p * x[col[p],:]
+ * with w_p = (edge_w ? edge_w[p] : 1) * (col_w ? col_w[col[p]] : 1), s_i = 1/deg_i under
+ * HGNN_MEAN (0 for deg 0), else 1.  Heavy rows follow the plan (slab: n_chunks*d floats).
+ * Any d >= 1 (float4 path when d % 4 == 0). */
+int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* rowptr,
+                       const int32_t* col, int64_t n_rows, const float* edge_w,
+                       const float* col_w, int32_t flags, const int32_t* heavy_rows,
+                       const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                       int32_t chunk, float* slab, float* out, hgnn_stream_t stream);
+
+/* K1 forward: aggr = mean_{(j->i)} x_src[j]  — PyG propagate(aggr='mean') inside SAGEConv:
+ * x_src.index_select(0, src) + scatter(..., dst, reduce='mean'), train_gnn.py:177-198. */
+int hgnn_gather_mean_fwd(const float* x_src, int64_t n_src, int32_t d, const int32_t* rowptr,
+                         const int32_t* col, int64_t n_dst, const int32_t* heavy_rows,
+                         const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                         int32_t chunk, float* slab, float* aggr, hgnn_stream_t stream);
+
+/* K2 backward: grad_x_src[j] (+)= sum_{(j->i)} grad_aggr[i] * inv_deg[i], walking the transposed
+ * CSR (grouped by source; t_col holds destinations) — autograd of the mean scatter. */
+int hgnn_scatter_mean_bwd(const float* grad_aggr, int64_t n_dst, const float* inv_deg,
+                          const int32_t* t_rowptr, const int32_t* t_col, int64_t n_src,
+                          int32_t d, const int32_t* heavy_rows, const int32_t* heavy_first,
+                          int64_t n_heavy, int64_t n_chunks, int32_t chunk, float* slab,
+                          float* grad_x_src, int32_t accumulate, hgnn_stream_t stream);
+
+/* ---- K3/K4: fused multi-segment linear (fp32 MFMA) -------------------------------------------
+ * Replaces SAGEConv's lin_l/lin_r addmm plus WeightedRGCN's weighted sum + ReLU
+ * (train_gnn.py:187-198):
+ *   out[n, h] = act( sum_s xs[s][n, ks[s]] @ w[:, off_s:off_s+ks[s]]^T + bias )
+ * w is [h, sum(ks)] row-major (torch Linear layout), act = ReLU when relu != 0. */
+int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                    const float* w, int32_t h, const float* bias, int32_t relu, float* out,
+                    hgnn_stream_t stream);
+
+/* Backward of hgnn_linear_fwd.  dz = dout * (out > 0) when out != NULL (ReLU), else dout.
+ *   dxs[s] = dz @ w[:, seg s]           (skipped for NULL entries)
+ *   dw     = dz^T @ [xs...]             (NULL: skipped; same for db = colsum(dz))
+ * Deterministic (per-block partials reduced in block order).  Workspace:
+ * hgnn_linear_bwd_ws_bytes(n_rows, sum(ks), h). */
+size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h);
+int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                    const float* w, int32_t h, const float* dout, const float* out,
+                    float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,
+                    hgnn_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HGNN_H_ */

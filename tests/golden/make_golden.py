@@ -1,0 +1,117 @@
+"""Generate the committed golden fixtures (run from the repo root: python tests/golden/make_golden.py).
+
+The reference cannot be imported here (permission denied) and its arithmetic
+library (torch_geometric) is absent, so the fixtures are outputs of the CPU oracle
+(``oracle/sage_ref.py``), cross-checked against the float64 dense formulation
+(``oracle/dense_ref.py``) before they are written.  Inputs come from the seeded synthetic
+generator (``truth_recommendation_gnn_amd.synth``).
+
+* ``cfg1_weighted_rgcn.npz`` — BASELINE config 1 (toy graph, 3 relations, d=h=64), the
+  reference ``WeightedRGCN`` (train_gnn.py:147-200) + loss (train_gnn.py:259-281): outputs,
+  loss, all 9 parameter gradients.
+* ``cfg2_slice_hetero_sage.npz`` — a 20k-edge slice of config 2 (U=1000, P=100, Zipf posts),
+  2-layer HeteroSAGE over engages + rev_engages: outputs, loss, all parameter gradients.
+"""
+from __future__ import annotations
+
+import pathlib
+import sys
+
+import numpy as np
+import torch
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+
+from oracle import dense_ref, sage_ref  # noqa: E402
+from truth_recommendation_gnn_amd import synth  # noqa: E402
+
+OUT = pathlib.Path(__file__).resolve().parent
+
+
+def rgcn_param_shapes(d, h, names=("msg_direct", "msg_social", "post_update")):
+    out = []
+    for n in names:
+        out += [(f"{n}.lin_l.weight", (h, d)), (f"{n}.lin_l.bias", (h,)), (f"{n}.lin_r.weight", (h, d))]
+    return out
+
+
+def hetero_param_shapes(relations, d, h, layers):
+    out = []
+    for l in range(layers):
+        cin = d if l == 0 else h
+        for et, _ in relations:
+            p = f"layers.{l}.{'__'.join(et)}"
+            out += [(f"{p}.lin_l.weight", (h, cin)), (f"{p}.lin_l.bias", (h,)),
+                    (f"{p}.lin_r.weight", (h, cin))]
+    return out
+
+
+def dense_check_rgcn(params, g, out):
+    """float64 dense recomputation of the WeightedRGCN forward."""
+    x = {k: v.numpy() for k, v in g.x_dict.items()}
+    e = {k: v.numpy() for k, v in g.edge_index_dict.items()}
+    P = {k: v.numpy() for k, v in params.items()}
+    c = lambda n, s, dd, et: dense_ref.sage_conv_dense(x[s], x[dd], e[et], P[f"{n}.lin_l.weight"],
+                                                       P[f"{n}.lin_l.bias"], P[f"{n}.lin_r.weight"])
+    u = np.maximum(1.0 * c("msg_direct", "post", "user", synth.REV_ENGAGES)
+                   + 0.75 * c("msg_social", "user", "user", synth.SOCIAL), 0)
+    p = np.maximum(c("post_update", "user", "post", synth.ENGAGES), 0)
+    for got, ref in ((out["user"], u), (out["post"], p)):
+        err = np.abs(got.numpy().astype(np.float64) - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert err < 1e-5, err
+
+
+def main():
+    # ---------------- cfg1: reference WeightedRGCN
+    g = synth.make_graph("cfg1")
+    d = h = 64
+    params = sage_ref.init_params(rgcn_param_shapes(d, h), seed=synth.WEIGHT_SEED)
+    pos = g.edge_index_dict[synth.ENGAGES]
+    neg = synth.negative_posts(g.num_posts, pos.shape[1])
+    w_post = synth.interaction_weights(g.num_posts)
+    pw = w_post[pos[1]]
+    fwd = lambda P: sage_ref.weighted_rgcn(P, g.x_dict, g.edge_index_dict)
+    out, loss, grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
+    dense_check_rgcn(params, g, out)
+    ld = dense_ref.link_loss_dense(out["user"], out["post"], pos.numpy(), neg.numpy(), pw.numpy())
+    assert abs(ld - float(loss)) < 1e-5 * max(1.0, abs(ld)), (ld, float(loss))
+    arrs = {"x_user": g.x_dict["user"].numpy(), "x_post": g.x_dict["post"].numpy(),
+            "ei_social": g.edge_index_dict[synth.SOCIAL].numpy(),
+            "ei_engages": g.edge_index_dict[synth.ENGAGES].numpy(),
+            "ei_rev_engages": g.edge_index_dict[synth.REV_ENGAGES].numpy(),
+            "neg_p": neg.numpy(), "pos_weights": pw.numpy(),
+            "out_user": out["user"].numpy(), "out_post": out["post"].numpy(),
+            "loss": np.array(float(loss), np.float32)}
+    for k, v in params.items():
+        arrs["param:" + k] = v.numpy()
+    for k, v in grads.items():
+        arrs["grad:" + k] = v.numpy()
+    np.savez_compressed(OUT / "cfg1_weighted_rgcn.npz", **arrs)
+
+    # ---------------- cfg2 slice: 2-layer HeteroSAGE over engages + rev_engages
+    cfg = synth.scaled("cfg2", 0.001)
+    g = synth.make_graph(cfg)
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+    params = sage_ref.init_params(hetero_param_shapes(rels, cfg.dim, cfg.hidden, cfg.layers),
+                                  seed=synth.WEIGHT_SEED)
+    pos = g.edge_index_dict[synth.ENGAGES]
+    neg = synth.negative_posts(g.num_posts, pos.shape[1])
+    pw = synth.interaction_weights(g.num_posts)[pos[1]]
+    fwd = lambda P: sage_ref.hetero_sage(P, g.x_dict, g.edge_index_dict, rels, cfg.layers)
+    out, loss, grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
+    arrs = {"x_user": g.x_dict["user"].numpy(), "x_post": g.x_dict["post"].numpy(),
+            "ei_engages": pos.numpy(), "neg_p": neg.numpy(), "pos_weights": pw.numpy(),
+            "out_user": out["user"].numpy(), "out_post": out["post"].numpy(),
+            "loss": np.array(float(loss), np.float32)}
+    for k, v in params.items():
+        arrs["param:" + k] = v.numpy()
+    for k, v in grads.items():
+        arrs["grad:" + k] = v.numpy()
+    np.savez_compressed(OUT / "cfg2_slice_hetero_sage.npz", **arrs)
+    for f in sorted(OUT.glob("*.npz")):
+        print(f.name, f.stat().st_size)
+
+
+if __name__ == "__main__":
+    main()

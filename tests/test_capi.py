@@ -1,0 +1,76 @@
+"""CPU: the C-ABI library loads and exports every entry point include/hgnn.h declares; the host
+side fails loudly (no CPU fallback)."""
+import pathlib
+import re
+import subprocess
+
+import pytest
+import torch
+
+from truth_recommendation_gnn_amd import _native as N
+from truth_recommendation_gnn_amd import HeteroData, SAGEConv, WeightedRGCN
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def _declared():
+    text = (ROOT / "include" / "hgnn.h").read_text()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(hgnn_\w+)\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    names = _declared()
+    assert len(names) >= 12
+    lib = N.lib()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", str(N.LIB_PATH)], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (hgnn_\w+)", out))
+    assert set(names) <= exported
+    assert lib.hgnn_version() >= 100
+
+
+def test_ctypes_signatures_cover_header():
+    assert set(_declared()) <= set(N._SIGS)
+
+
+def test_workspace_queries_run_without_gpu():
+    lib = N.lib()
+    assert lib.hgnn_coo_to_csr_ws_bytes(20_000_000, 100_000) > 4 * 4 * 20_000_000
+    assert lib.hgnn_plan_ws_bytes(1_000_000) > 4 * 1_000_000
+    assert lib.hgnn_linear_bwd_ws_bytes(1_000_000, 128, 64) > 0
+
+
+def test_cpu_tensors_are_refused_not_silently_computed():
+    conv = SAGEConv((-1, -1), 8)
+    x = torch.randn(4, 8)
+    ei = torch.tensor([[0, 1], [1, 2]])
+    with pytest.raises(ValueError, match="ROCm GPU"):
+        conv((x, x), ei)
+
+
+def test_module_surface_matches_reference_state_dict_keys():
+    m = WeightedRGCN(hidden_dim=64)
+    for conv in (m.msg_direct, m.msg_social, m.post_update):
+        conv.materialize(64, 64)
+    keys = sorted(m.state_dict())
+    want = sorted(f"{c}.{p}" for c in ("msg_direct", "msg_social", "post_update")
+                  for p in ("lin_l.weight", "lin_l.bias", "lin_r.weight"))
+    assert keys == want
+    # a fresh (lazy) model loads a state_dict without a forward, as inference.py:172 does
+    fresh = WeightedRGCN(hidden_dim=64)
+    fresh.load_state_dict(m.state_dict())
+    assert fresh.msg_direct.lin_l.weight.shape == (64, 64)
+
+
+def test_heterodata_lite():
+    g = HeteroData()
+    g["user"].x = torch.zeros(3, 4)
+    g["post"].x = torch.zeros(2, 4)
+    g["user", "engages", "post"].edge_index = torch.tensor([[0, 2], [1, 0]])
+    g["post", "rev_engages", "user"].edge_index = g["user", "engages", "post"].edge_index.flip(0)
+    assert g["user"].num_nodes == 3
+    assert set(g.edge_index_dict) == {("user", "engages", "post"), ("post", "rev_engages", "user")}
+    assert g.metadata()[0] == ["user", "post"]
+    assert g.to("cpu") is g

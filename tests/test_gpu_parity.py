@@ -1,0 +1,241 @@
+"""GPU parity: every HIP kernel through the C ABI against the CPU oracle / golden fixtures.
+
+Tolerances: integer CSR work bit-exact; fp32 paths within 1e-4 relative (north_star) — written as
+``assert_close(rtol=1e-4, atol=1e-5 * scale)``.
+"""
+import pathlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import csr_ref, sage_ref
+from truth_recommendation_gnn_amd import (HeteroSAGE, SAGEConv, WeightedRGCN, WeightedRGCNAuthor,
+                                          graph, ops, synth)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLD = pathlib.Path(__file__).resolve().parent / "golden"
+RTOL = 1e-4
+
+
+def close(got, ref, rtol=RTOL, atol_scale=1e-5):
+    got = got.detach().double().cpu()
+    ref = torch.as_tensor(ref).double().cpu()
+    scale = max(float(ref.abs().max()) if ref.numel() else 0.0, 1e-6)
+    torch.testing.assert_close(got, ref, rtol=rtol, atol=atol_scale * scale)
+
+
+def rand_coo(rng, n_src, n_dst, E, skew=False):
+    src = rng.integers(0, n_src, size=E)
+    if skew:
+        dst = synth._zipf_sample_np(rng, n_dst, E, 1.1)
+    else:
+        dst = rng.integers(0, n_dst, size=E)
+    return torch.from_numpy(np.stack([src, dst]).astype(np.int64))
+
+
+# ----------------------------------------------------------------------------- K5
+@pytest.mark.parametrize("n_keys,E,skew", [(1, 10, False), (7, 0, False), (300, 5000, True),
+                                           (70000, 200000, True), (1 << 17, 300000, False)])
+def test_coo_to_csr_bit_exact(n_keys, E, skew):
+    rng = np.random.default_rng(n_keys + E)
+    ei = rand_coo(rng, 1000, n_keys, E, skew)
+    g = graph.group_edges(ei[1].to(DEV), ei[0].to(DEV), n_keys, 1000)
+    rowptr, col, perm = csr_ref.coo_to_csr(ei[1].numpy(), ei[0].numpy(), n_keys)
+    assert np.array_equal(g.rowptr.cpu().numpy(), rowptr)
+    assert np.array_equal(g.perm.cpu().numpy(), perm)
+    assert np.array_equal(g.col.cpu().numpy(), col)
+
+
+def test_coo_to_csr_rejects_out_of_range():
+    ei = torch.tensor([[0, 5], [1, 2]], device=DEV)
+    with pytest.raises(ValueError, match="out of range"):
+        graph.group_edges(ei[1], ei[0], 3, 4)
+
+
+def test_skew_plan_matches_reference_plan():
+    rng = np.random.default_rng(3)
+    ei = rand_coo(rng, 500, 50, 20000, skew=True)
+    g = graph.group_edges(ei[1].to(DEV), ei[0].to(DEV), 50, 500, chunk=64)
+    heavy, first = csr_ref.heavy_plan(g.rowptr.cpu().numpy(), 64)
+    assert g.plan.n_heavy == heavy.size and g.plan.n_chunks == int(first[-1])
+    assert np.array_equal(g.plan.heavy_rows.cpu().numpy(), heavy)
+    assert np.array_equal(g.plan.heavy_first.cpu().numpy(), first)
+
+
+# ----------------------------------------------------------------------------- K1 / K2
+@pytest.mark.parametrize("d", [1, 3, 4, 7, 16, 64, 100, 128, 256, 300])
+@pytest.mark.parametrize("chunk", [None, 8])
+def test_gather_mean_matches_oracle(d, chunk):
+    rng = np.random.default_rng(d)
+    n_src, n_dst, E = 700, 300, 6000
+    ei = rand_coo(rng, n_src, n_dst, E, skew=True)
+    x = torch.from_numpy(rng.standard_normal((n_src, d)).astype(np.float32))
+    ref = sage_ref.mean_aggregate(x, ei, n_dst)
+    csr = graph.RelationCSR(ei.to(DEV), n_src, n_dst, chunk=chunk)
+    got = ops.gather_mean(x.to(DEV), csr)
+    close(got, ref)
+
+
+@pytest.mark.parametrize("d", [3, 64, 128])
+@pytest.mark.parametrize("chunk", [None, 16])
+def test_scatter_mean_bwd_matches_autograd(d, chunk):
+    rng = np.random.default_rng(10 + d)
+    n_src, n_dst, E = 400, 900, 8000
+    ei = rand_coo(rng, n_src, n_dst, E, skew=True)
+    x = torch.from_numpy(rng.standard_normal((n_src, d)).astype(np.float32)).requires_grad_()
+    g = torch.from_numpy(rng.standard_normal((n_dst, d)).astype(np.float32))
+    sage_ref.mean_aggregate(x, ei, n_dst).backward(g)
+    csr = graph.RelationCSR(ei.to(DEV), n_src, n_dst, chunk=chunk)
+    got = ops.scatter_mean_bwd(g.to(DEV), csr)
+    close(got, x.grad)
+    acc = torch.ones(n_src, d, device=DEV)
+    ops.scatter_mean_bwd(g.to(DEV), csr, out=acc)
+    close(acc, x.grad + 1.0)
+
+
+def test_gather_is_deterministic_bitwise():
+    rng = np.random.default_rng(5)
+    ei = rand_coo(rng, 5000, 200, 100000, skew=True).to(DEV)
+    x = torch.randn(5000, 64, device=DEV)
+    csr = graph.RelationCSR(ei, 5000, 200, chunk=64)
+    a = ops.gather_mean(x, csr)
+    b = ops.gather_mean(x, csr)
+    assert torch.equal(a, b)
+
+
+# ----------------------------------------------------------------------------- K3 / K4
+@pytest.mark.parametrize("ks,h", [([64], 64), ([64, 64], 64), ([64, 64, 64], 64),
+                                  ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100)])
+@pytest.mark.parametrize("n", [1, 37, 1000])
+def test_linear_fwd_bwd_matches_torch(ks, h, n):
+    gen = torch.Generator().manual_seed(n + h)
+    segs = [torch.randn(n, k, generator=gen) for k in ks]
+    w = torch.randn(h, sum(ks), generator=gen) * 0.2
+    b = torch.randn(h, generator=gen)
+    dout = torch.randn(n, h, generator=gen)
+    ref_in = [s.clone().requires_grad_() for s in segs]
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = torch.relu(torch.cat(ref_in, 1) @ wr.T + br)
+    ref.backward(dout)
+    dsegs = [s.to(DEV) for s in segs]
+    out = ops.linear_fwd(dsegs, w.to(DEV), b.to(DEV), relu=True)
+    close(out, ref)
+    dxs = [torch.empty_like(s) for s in dsegs]
+    dw, db = ops.linear_bwd(dsegs, w.to(DEV), dout.to(DEV), out, dxs, True, True)
+    for gx, r in zip(dxs, ref_in):
+        close(gx, r.grad)
+    close(dw, wr.grad)
+    close(db, br.grad)
+
+
+# ----------------------------------------------------------------------------- models
+def _fixture_cfg1():
+    z = np.load(GOLD / "cfg1_weighted_rgcn.npz")
+    x = {"user": torch.from_numpy(z["x_user"]).to(DEV), "post": torch.from_numpy(z["x_post"]).to(DEV)}
+    e = {synth.SOCIAL: torch.from_numpy(z["ei_social"]).to(DEV),
+         synth.ENGAGES: torch.from_numpy(z["ei_engages"]).to(DEV),
+         synth.REV_ENGAGES: torch.from_numpy(z["ei_rev_engages"]).to(DEV)}
+    params = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")}
+    return z, x, e, params
+
+
+def test_weighted_rgcn_train_step_matches_golden():
+    z, x, e, params = _fixture_cfg1()
+    model = WeightedRGCN(hidden_dim=64).to(DEV)
+    model.load_state_dict(params)
+    out = model(x, e)
+    close(out["user"], z["out_user"])
+    close(out["post"], z["out_post"])
+    pos = e[synth.ENGAGES]
+    loss = ops.link_loss(out["user"], out["post"], pos, torch.from_numpy(z["neg_p"]).to(DEV),
+                         torch.from_numpy(z["pos_weights"]).to(DEV))
+    assert abs(float(loss) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_hetero_sage_two_layer_matches_golden():
+    z = np.load(GOLD / "cfg2_slice_hetero_sage.npz")
+    ei = torch.from_numpy(z["ei_engages"]).to(DEV)
+    e = {synth.ENGAGES: ei, synth.REV_ENGAGES: ei.flip(0)}
+    x = {"user": torch.from_numpy(z["x_user"]).to(DEV), "post": torch.from_numpy(z["x_post"]).to(DEV)}
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+    model = HeteroSAGE(64, rels, num_layers=2).to(DEV)
+    params = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")}
+    model.load_state_dict(params)
+    out = model(x, e)
+    close(out["user"], z["out_user"])
+    close(out["post"], z["out_post"])
+    loss = ops.link_loss(out["user"], out["post"], ei, torch.from_numpy(z["neg_p"]).to(DEV),
+                         torch.from_numpy(z["pos_weights"]).to(DEV))
+    assert abs(float(loss) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_sage_conv_standalone_and_homogeneous_input():
+    rng = np.random.default_rng(1)
+    ei = rand_coo(rng, 50, 50, 400)
+    x = torch.from_numpy(rng.standard_normal((50, 12)).astype(np.float32))
+    conv = SAGEConv(12, 9).to(DEV)
+    xg = x.to(DEV).requires_grad_()
+    out = conv(xg, ei.to(DEV))
+    W = {k: v.detach().cpu() for k, v in conv.state_dict().items()}
+    xr = x.clone().requires_grad_()
+    ref = sage_ref.sage_conv(xr, xr, ei, W["lin_l.weight"], W["lin_l.bias"], W["lin_r.weight"])
+    close(out, ref)
+    g = torch.randn(50, 9)
+    out.backward(g.to(DEV))
+    ref.backward(g)
+    close(xg.grad, xr.grad)
+
+
+def test_inductive_single_user_zero_edges():
+    # inference.py:410-424: one user, post table [0, 64], every relation E=0
+    z, _, _, params = _fixture_cfg1()
+    model = WeightedRGCN(64).to(DEV)
+    model.load_state_dict(params)
+    empty = torch.empty(2, 0, dtype=torch.long, device=DEV)
+    xu = torch.randn(1, 64, device=DEV)
+    e = {synth.SOCIAL: empty, synth.ENGAGES: empty.clone(), synth.REV_ENGAGES: empty.clone()}
+    with torch.no_grad():
+        out = model({"user": xu, "post": torch.empty(0, 64, device=DEV)}, e)
+    P = {k: v for k, v in params.items()}
+    ref_u = torch.relu(1.0 * (P["msg_direct.lin_l.bias"] + xu.cpu() @ P["msg_direct.lin_r.weight"].T)
+                       + 0.75 * (P["msg_social.lin_l.bias"] + xu.cpu() @ P["msg_social.lin_r.weight"].T))
+    close(out["user"], ref_u)
+    assert out["post"].shape == (0, 64)
+
+
+def test_author_variant_matches_oracle():
+    g = synth.make_graph("cfg1")
+    e = dict(g.edge_index_dict)
+    e[("post", "followed_by", "user")] = torch.empty(2, 0, dtype=torch.long)  # test_gnn.py:103-106
+    model = WeightedRGCNAuthor(64).to(DEV)
+    x = {k: v.to(DEV) for k, v in g.x_dict.items()}
+    out = model(x, {k: v.to(DEV) for k, v in e.items()})
+    params = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    ref = sage_ref.weighted_rgcn(params, g.x_dict, e, layout=sage_ref.TEST_LAYOUT)
+    close(out["user"], ref["user"])
+    close(out["post"], ref["post"])
+
+
+# ----------------------------------------------------------------------------- full-size properties
+def test_cfg2_full_size_linearity_checksum():
+    """At BASELINE config 2 size (20M edges): sum_i deg_i * aggr_i == sum_e x_src[src_e]
+    (a checksum of checksums, float64), and the CSR row lengths equal the COO degree counts."""
+    g = synth.make_graph("cfg2", device=DEV)
+    ei = g.edge_index_dict[synth.ENGAGES]
+    csr = graph.RelationCSR(ei, g.num_users, g.num_posts)
+    deg = torch.bincount(ei[1], minlength=g.num_posts)
+    assert torch.equal((csr.fwd.rowptr[1:] - csr.fwd.rowptr[:-1]).long(), deg)
+    agg = ops.gather_mean(g.x_dict["user"], csr)
+    lhs = (agg.double() * deg.double()[:, None]).sum(0)
+    outdeg = torch.bincount(ei[0], minlength=g.num_users).double()
+    rhs = (g.x_dict["user"].double() * outdeg[:, None]).sum(0)
+    torch.testing.assert_close(lhs, rhs, rtol=1e-6, atol=1e-3)
+    assert csr.fwd.plan.n_heavy > 0   # the Zipf head really exercised the chunked path

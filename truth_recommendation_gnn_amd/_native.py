@@ -1,0 +1,122 @@
+"""ctypes binding of ``lib/libhgnn.so`` (the C ABI declared in ``include/hgnn.h``).
+
+Only plain pointers, sizes and a ``hipStream_t`` (as ``void*``) cross this boundary.  There is no
+CPU fallback anywhere in the package: if the library is missing, or a tensor is not on a ROCm
+device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+from typing import Optional, Sequence
+
+import torch
+
+LIB_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "libhgnn.so"
+
+HGNN_MEAN = 1
+HGNN_ACCUMULATE = 2
+MAX_SEG = 6
+
+_c_i32, _c_i64, _c_sz, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/hgnn.h
+_SIGS = {
+    "hgnn_version": (_c_i32, []),
+    "hgnn_last_error_string": (ctypes.c_char_p, []),
+    "hgnn_coo_to_csr_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_coo_to_csr": (_c_i32, [_p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_plan_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_plan_count": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_sz, _p]),
+    "hgnn_plan_fill": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _p, _c_sz, _p]),
+    "hgnn_inv_degree": (_c_i32, [_p, _c_i64, _p, _p]),
+    "hgnn_gather_reduce": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_i64, _p, _p, _c_i32, _p, _p,
+                                    _c_i64, _c_i64, _c_i32, _p, _p, _p]),
+    "hgnn_gather_mean_fwd": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_i64, _p, _p, _c_i64,
+                                      _c_i64, _c_i32, _p, _p, _p]),
+    "hgnn_scatter_mean_bwd": (_c_i32, [_p, _c_i64, _p, _p, _p, _c_i64, _c_i32, _p, _p, _c_i64,
+                                       _c_i64, _c_i32, _p, _p, _c_i32, _p]),
+    "hgnn_linear_fwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _c_i32, _p, _p]),
+    "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
+    "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
+                                 _c_sz, _p]),
+    "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _p, _p, _p, _c_i64, _p, _p, _p, _p]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load the library once.  torch is imported first so its HIP runtime (same SONAME
+    libamdhip64.so.7) is the one the library binds to — one runtime, one set of streams."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise NativeError(f"hgnn native library not found at {LIB_PATH}; build it with "
+                              "`python -m truth_recommendation_gnn_amd.build` (no CPU fallback)")
+        l = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(l, name, None)
+            if fn is None:
+                continue
+            fn.restype, fn.argtypes = res, args
+        _lib = l
+    return _lib
+
+
+def exported_symbols() -> Sequence[str]:
+    l = lib()
+    return [n for n in _SIGS if hasattr(l, n)]
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().hgnn_last_error_string().decode(errors="replace")
+        raise NativeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else _p(t.data_ptr())
+
+
+def stream_ptr(device: torch.device):
+    return _p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*tensors: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise ValueError("hgnn runs only on a ROCm GPU (MI355X / gfx950); got a tensor on "
+                             f"{t.device} — move the graph and model with .to('cuda')")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"tensors on different devices: {dev} vs {t.device}")
+    if dev is None:
+        raise ValueError("no tensor to infer the device from")
+    return dev
+
+
+def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+def ptr_array(ts: Sequence[Optional[torch.Tensor]]):
+    arr = (_p * MAX_SEG)()
+    for i, t in enumerate(ts):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+def int_array(vals: Sequence[int]):
+    arr = (_c_i32 * MAX_SEG)()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr

@@ -1,0 +1,78 @@
+"""Build the in-tree C-ABI library ``lib/libhgnn.so`` from ``csrc/*.hip`` for gfx950.
+
+``python -m truth_recommendation_gnn_amd.build`` (or ``__graft_entry__.build()``).  hipcc
+cross-compiles here without a GPU; the built ``.so`` stays in-tree (git-ignored, not
+gpurun-ignored) so it travels to the GPU box with the snapshot.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import pathlib
+import subprocess
+import sys
+
+PKG = pathlib.Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "lib"
+LIB = LIBDIR / "libhgnn.so"
+INCLUDE = PKG.parent / "include"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall",
+         "-Wno-unused-result", f"-I{INCLUDE}"]
+
+
+def _sources():
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _digest() -> str:
+    h = hashlib.sha256()
+    for p in _sources() + sorted(CSRC.glob("*.h")) + [INCLUDE / "hgnn.h"]:
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def build(force: bool = False, verbose: bool = True) -> pathlib.Path:
+    """Compile every ``csrc/*.hip`` to an object and link ``lib/libhgnn.so``.
+
+    Skips the work when the sources' digest matches the one recorded beside the library.
+    """
+    LIBDIR.mkdir(exist_ok=True)
+    stamp = LIBDIR / "libhgnn.digest"
+    dig = _digest()
+    if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
+        return LIB
+    objdir = PKG.parent / "build" / "obj"
+    objdir.mkdir(parents=True, exist_ok=True)
+
+    def compile_one(src: pathlib.Path) -> pathlib.Path:
+        obj = objdir / (src.stem + ".o")
+        cmd = [HIPCC, *FLAGS, "-c", str(src), "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stdout}\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            sys.stderr.write(r.stderr)
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(compile_one, _sources()))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    stamp.write_text(dig + "\n")
+    if verbose:
+        print(f"built {LIB} ({LIB.stat().st_size // 1024} KiB)")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,441 @@
+// K5: COO -> CSR by a stable LSD radix sort (8-bit digits), the device scan it needs, and the
+// degree-skew plan.  Integer work, HBM/latency bound; no MFMA.
+//
+// Why a sort and not an atomic counting fill: the fill would order each row's edges by atomic
+// arrival, so the fp32 sum order — and the last bits of every aggregate — would change from run
+// to run.  A stable sort keeps each row in COO order (the order PyG scatters in), which makes the
+// whole forward/backward bitwise reproducible and lets tests compare the CSR bit for bit with
+// oracle/csr_ref.py.
+#include "hgnn_common.h"
+
+#include <string.h>
+
+namespace hgnn {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+// ------------------------------------------------------------------------------------------
+// Exclusive scan (int32), three phases: tile sums -> scan of tile sums (recursive) -> tile scan.
+// ------------------------------------------------------------------------------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 16;                        // per thread
+constexpr int kScanTile = kScanThreads * kScanItems;  // 4096
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the block total in *total.
+__device__ __forceinline__ int block_excl_scan(int v, int* lds /*[kScanThreads/64]*/, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int inc = wave_incl_scan(v);
+  if (lane == 63) lds[wid] = inc;
+  __syncthreads();
+  int wpre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kScanThreads / 64; ++w) {
+    int s = lds[w];
+    wpre += (w < wid) ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return wpre + inc - v;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_tile_sums(const int32_t* in, int64_t n,
+                                                            int32_t* sums) {
+  __shared__ int lds[kScanThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile;
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    int64_t idx = base + (int64_t)i * kScanThreads + threadIdx.x;
+    s += idx < n ? in[idx] : 0;
+  }
+  int tot;
+  block_excl_scan(s, lds, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// out[i] = offs[tile] + exclusive prefix of in within the tile; out[n] = grand total when the
+// last tile writes it (total pointer).
+__global__ void __launch_bounds__(kScanThreads) k_tile_scan(const int32_t* in, int64_t n,
+                                                            const int32_t* offs, int32_t* out,
+                                                            int write_total) {
+  __shared__ int lds[kScanThreads / 64];
+  const int64_t base = (int64_t)blockIdx.x * kScanTile + (int64_t)threadIdx.x * kScanItems;
+  int v[kScanItems];
+  int s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    int64_t idx = base + i;
+    v[i] = idx < n ? in[idx] : 0;
+    s += v[i];
+  }
+  int tot;
+  int pre = block_excl_scan(s, lds, &tot) + (offs ? offs[blockIdx.x] : 0);
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    int64_t idx = base + i;
+    if (idx < n) out[idx] = pre;
+    pre += v[i];
+  }
+  if (write_total && blockIdx.x == gridDim.x - 1 && threadIdx.x == kScanThreads - 1) out[n] = pre;
+}
+
+static size_t scan_ws_bytes(int64_t n) {
+  size_t b = 0;
+  while (n > kScanTile) {
+    int64_t t = cdiv(n, kScanTile);
+    b += align_up((size_t)(t + 1) * 4, 256);
+    n = t;
+  }
+  return b + 256;
+}
+
+// Recursive: ws holds the tile-sum levels.
+int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t* ws_bytes,
+                       hipStream_t stream) {
+  if (!ws) {
+    *ws_bytes = scan_ws_bytes(n);
+    return HGNN_OK;
+  }
+  if (n <= 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(int32_t), stream);
+    return check_launch("scan(empty)");
+  }
+  int64_t tiles = cdiv(n, kScanTile);
+  if (tiles == 1) {
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kScanThreads), 0, stream, in, n,
+                       (const int32_t*)nullptr, out, 1);
+    return check_launch("k_tile_scan");
+  }
+  Workspace w(ws, *ws_bytes);
+  int32_t* sums = w.take<int32_t>(tiles + 1);
+  size_t rest = w.cap > w.used ? w.cap - align_up(w.used, 256) : 0;
+  void* rest_p = w.base + align_up(w.used, 256);
+  if (!sums) return fail(HGNN_E_WS, "scan workspace too small");
+  hipLaunchKernelGGL(k_tile_sums, dim3(tiles), dim3(kScanThreads), 0, stream, in, n, sums);
+  if (int rc = check_launch("k_tile_sums")) return rc;
+  if (int rc = exclusive_scan_i32(sums, sums, tiles, rest_p, &rest, stream)) return rc;
+  hipLaunchKernelGGL(k_tile_scan, dim3(tiles), dim3(kScanThreads), 0, stream, in, n,
+                     (const int32_t*)sums, out, 1);
+  return check_launch("k_tile_scan");
+}
+
+// In-place use above (sums -> sums) is safe: k_tile_scan with a single tile reads all inputs into
+// registers before writing; with several tiles each block reads/writes only its own tile after
+// the tile sums were taken into a separate level.  (The nested call scans `sums` in place only
+// when it fits one tile, or recursively with its own level.)
+
+// ------------------------------------------------------------------------------------------
+// Stable LSD radix sort of (key32, idx32) pairs, 8-bit digits.
+// ------------------------------------------------------------------------------------------
+constexpr int kSortThreads = 256;
+constexpr int kSortRounds = 16;                           // one item per thread per round
+constexpr int kSortTile = kSortThreads * kSortRounds;     // 4096 items per block
+constexpr int kRadix = 256;
+
+// key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
+__global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
+                                                      int64_t E, int64_t n_keys, int64_t n_other,
+                                                      int32_t* key32, int32_t* invalid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int bad = 0;
+  if (i < E) {
+    int64_t k = key[i], o = other[i];
+    bool ok = k >= 0 && k < n_keys && o >= 0 && o < n_other;
+    key32[i] = ok ? (int32_t)k : (int32_t)n_keys;
+    bad = ok ? 0 : 1;
+  }
+  unsigned long long m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
+}
+
+// counts[digit * nblocks + block] for this block's tile.
+__global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
+                                                               int shift, int32_t* counts) {
+  __shared__ int hist[kRadix];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+#pragma unroll 4
+  for (int r = 0; r < kSortRounds; ++r) {
+    int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
+    if (i < E) atomicAdd(&hist[(keys[i] >> shift) & (kRadix - 1)], 1);
+  }
+  __syncthreads();
+  counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = hist[threadIdx.x];
+}
+
+// Stable scatter: rounds in order; within a round, items in thread order.  Per wave the match
+// set of a digit comes from 8 ballots; per-wave digit counts go through LDS.
+__global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
+    const int32_t* keys_in, const int32_t* vals_in, int64_t E, int shift, const int32_t* offs,
+    int32_t* keys_out, int32_t* vals_out, int identity_vals) {
+  __shared__ int base_off[kRadix];                 // global offset + running count per digit
+  __shared__ int wcount[kSortThreads / 64][kRadix];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  base_off[threadIdx.x] = offs[(int64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  for (int w = 0; w < kSortThreads / 64; ++w) wcount[w][threadIdx.x] = 0;
+  __syncthreads();
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  for (int r = 0; r < kSortRounds; ++r) {
+    int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
+    const bool valid = i < E;
+    int key = valid ? keys_in[i] : 0;
+    int val = valid ? (identity_vals ? (int)i : vals_in[i]) : 0;
+    int digit = (key >> shift) & (kRadix - 1);
+    unsigned long long match = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      unsigned long long m = __ballot((digit >> b) & 1);
+      match &= ((digit >> b) & 1) ? m : ~m;
+    }
+    int rank = __popcll(match & lt_mask);
+    if (valid && rank == 0) wcount[wid][digit] = __popcll(match);
+    __syncthreads();
+    if (valid) {
+      int pos = base_off[digit] + rank;
+      for (int w = 0; w < wid; ++w) pos += wcount[w][digit];
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();
+    {  // advance running offsets, clear the per-wave counts (one digit per thread)
+      int d = threadIdx.x, s = 0;
+      for (int w = 0; w < kSortThreads / 64; ++w) {
+        s += wcount[w][d];
+        wcount[w][d] = 0;
+      }
+      base_off[d] += s;
+    }
+    __syncthreads();
+  }
+}
+
+// rowptr[r] = #sorted keys < r for r in [0, n_keys]; col = other[perm].
+__global__ void __launch_bounds__(256) k_finish_csr(const int32_t* skey, const int32_t* sidx,
+                                                    const int64_t* other, int64_t E,
+                                                    int64_t n_keys, int32_t* rowptr,
+                                                    int32_t* col, int32_t* perm) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  int32_t k = skey[i];
+  int32_t e = sidx[i];
+  perm[i] = e;
+  col[i] = k < n_keys ? (int32_t)other[e] : 0;
+  int64_t prev = i > 0 ? skey[i - 1] : -1;
+  int64_t hi = k < n_keys ? k : n_keys;
+  for (int64_t r = prev + 1; r <= hi; ++r) rowptr[r] = (int32_t)i;
+  if (i == E - 1)
+    for (int64_t r = (int64_t)k + 1; r <= n_keys; ++r) rowptr[r] = (int32_t)E;
+}
+
+__global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+static int radix_passes(int64_t n_keys) {
+  int bits = 0;
+  while ((int64_t(1) << bits) <= n_keys) ++bits;   // keys in [0, n_keys] incl. sentinel
+  return (bits + 7) / 8;
+}
+
+static size_t sort_ws_bytes(int64_t E) {
+  int64_t nb = cdiv(E, kSortTile);
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, 0);
+  return 4 * align_up((size_t)E * 4, 256) + 2 * align_up((size_t)(nb * kRadix + 1) * 4, 256) +
+         scan_b + 1024;
+}
+
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_version(void) { return 100; }
+
+const char* hgnn_last_error_string(void) { return g_err; }
+
+size_t hgnn_coo_to_csr_ws_bytes(int64_t E, int64_t n_keys) {
+  (void)n_keys;
+  return sort_ws_bytes(E < 1 ? 1 : E);
+}
+
+int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t n_keys,
+                    int64_t n_other, int32_t* rowptr, int32_t* col, int32_t* perm,
+                    int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_keys < 0 || n_keys >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "coo_to_csr: E=%lld n_keys=%lld out of range", (long long)E,
+                (long long)n_keys);
+  if (!rowptr || !d_invalid || (E > 0 && (!key || !other || !col || !perm)))
+    return fail(HGNN_E_ARG, "coo_to_csr: null pointer");
+  (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
+  if (E == 0) {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
+                       n_keys + 1, 0);
+    return check_launch("coo_to_csr(E=0)");
+  }
+  if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "coo_to_csr: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* ka = w.take<int32_t>(E);
+  int32_t* kb = w.take<int32_t>(E);
+  int32_t* va = w.take<int32_t>(E);
+  int32_t* vb = w.take<int32_t>(E);
+  const int64_t nb = cdiv(E, kSortTile);
+  int32_t* counts = w.take<int32_t>(nb * kRadix + 1);
+  int32_t* offs = w.take<int32_t>(nb * kRadix + 1);
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, stream);
+  void* scan_ws = w.take<char>(scan_b);
+  if (!scan_ws) return fail(HGNN_E_WS, "coo_to_csr: workspace too small");
+
+  hipLaunchKernelGGL(k_prepare_keys, dim3(cdiv(E, 256)), dim3(256), 0, stream, key, other, E,
+                     n_keys, n_other, ka, d_invalid);
+  if (int rc = check_launch("k_prepare_keys")) return rc;
+  const int passes = radix_passes(n_keys);
+  int32_t *kin = ka, *kout = kb, *vin = va, *vout = vb;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    hipLaunchKernelGGL(k_digit_counts, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift,
+                       counts);
+    if (int rc = check_launch("k_digit_counts")) return rc;
+    if (int rc = exclusive_scan_i32(counts, offs, nb * kRadix, scan_ws, &scan_b, stream))
+      return rc;
+    hipLaunchKernelGGL(k_digit_scatter, dim3(nb), dim3(kSortThreads), 0, stream, kin, vin, E,
+                       shift, offs, kout, vout, p == 0 ? 1 : 0);
+    if (int rc = check_launch("k_digit_scatter")) return rc;
+    int32_t* t = kin; kin = kout; kout = t;
+    t = vin; vin = vout; vout = t;
+  }
+  if (passes == 0) {  // n_keys == 0: every edge is invalid; identity order
+    hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(1), 0, stream, rowptr, 1, 0);
+    return check_launch("coo_to_csr(n_keys=0)");
+  }
+  hipLaunchKernelGGL(k_finish_csr, dim3(cdiv(E, 256)), dim3(256), 0, stream, kin, vin, other, E,
+                     n_keys, rowptr, col, perm);
+  return check_launch("k_finish_csr");
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Degree-skew plan and 1/deg.
+// ------------------------------------------------------------------------------------------
+namespace hgnn {
+
+__global__ void k_plan_flags(const int32_t* rowptr, int64_t n, int32_t chunk, int32_t* heavy,
+                             int32_t* nch) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t deg = rowptr[i + 1] - rowptr[i];
+  bool h = deg > chunk;
+  heavy[i] = h ? 1 : 0;
+  nch[i] = h ? (deg + chunk - 1) / chunk : 0;
+}
+
+__global__ void k_plan_counts(const int32_t* hscan, const int32_t* cscan, int64_t n,
+                              int32_t* out2) {
+  out2[0] = hscan[n];
+  out2[1] = cscan[n];
+}
+
+__global__ void k_plan_scatter(const int32_t* heavy, const int32_t* hscan, const int32_t* cscan,
+                               int64_t n, int32_t* heavy_rows, int32_t* heavy_first) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && heavy[i]) {
+    heavy_rows[hscan[i]] = (int32_t)i;
+    heavy_first[hscan[i]] = cscan[i];
+  }
+  if (i == n) heavy_first[hscan[n]] = cscan[n];
+}
+
+__global__ void k_inv_degree(const int32_t* rowptr, int64_t n, float* inv) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t deg = rowptr[i + 1] - rowptr[i];
+  inv[i] = deg > 0 ? 1.0f / (float)deg : 0.0f;
+}
+
+static int plan_common(const int32_t* rowptr, int64_t n, int32_t chunk, void* ws, size_t ws_bytes,
+                       hipStream_t stream, int32_t** heavy, int32_t** hscan, int32_t** cscan) {
+  if (!rowptr || n < 0 || chunk <= 0) return fail(HGNN_E_ARG, "plan: bad arguments");
+  Workspace w(ws, ws_bytes);
+  *heavy = w.take<int32_t>(n + 1);
+  int32_t* nch = w.take<int32_t>(n + 1);
+  *hscan = w.take<int32_t>(n + 1);
+  *cscan = w.take<int32_t>(n + 1);
+  size_t sb = 0;
+  exclusive_scan_i32(nullptr, nullptr, n, nullptr, &sb, stream);
+  void* sws = w.take<char>(sb);
+  if (!sws) return fail(HGNN_E_WS, "plan: workspace too small");
+  if (n > 0) {
+    hipLaunchKernelGGL(k_plan_flags, dim3(cdiv(n, 256)), dim3(256), 0, stream, rowptr, n, chunk,
+                       *heavy, nch);
+    if (int rc = check_launch("k_plan_flags")) return rc;
+  }
+  if (int rc = exclusive_scan_i32(*heavy, *hscan, n, sws, &sb, stream)) return rc;
+  return exclusive_scan_i32(nch, *cscan, n, sws, &sb, stream);
+}
+
+}  // namespace hgnn
+
+extern "C" {
+
+size_t hgnn_plan_ws_bytes(int64_t n_rows) {
+  size_t sb = 0;
+  exclusive_scan_i32(nullptr, nullptr, n_rows, nullptr, &sb, 0);
+  return 4 * align_up((size_t)(n_rows + 1) * 4, 256) + sb + 2048;
+}
+
+int hgnn_plan_count(const int32_t* rowptr, int64_t n_rows, int32_t chunk, int32_t* d_counts2,
+                    void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  int32_t *heavy, *hscan, *cscan;
+  if (int rc = plan_common(rowptr, n_rows, chunk, ws, ws_bytes, stream, &heavy, &hscan, &cscan))
+    return rc;
+  hipLaunchKernelGGL(k_plan_counts, dim3(1), dim3(1), 0, stream, hscan, cscan, n_rows, d_counts2);
+  return check_launch("k_plan_counts");
+}
+
+int hgnn_plan_fill(const int32_t* rowptr, int64_t n_rows, int32_t chunk, int32_t* heavy_rows,
+                   int32_t* heavy_first, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  int32_t *heavy, *hscan, *cscan;
+  if (int rc = plan_common(rowptr, n_rows, chunk, ws, ws_bytes, stream, &heavy, &hscan, &cscan))
+    return rc;
+  hipLaunchKernelGGL(k_plan_scatter, dim3(cdiv(n_rows + 1, 256)), dim3(256), 0, stream, heavy,
+                     hscan, cscan, n_rows, heavy_rows, heavy_first);
+  return check_launch("k_plan_scatter");
+}
+
+int hgnn_inv_degree(const int32_t* rowptr, int64_t n_rows, float* inv_deg,
+                    hgnn_stream_t stream_) {
+  if (n_rows <= 0) return HGNN_OK;
+  if (!rowptr || !inv_deg) return fail(HGNN_E_ARG, "inv_degree: null pointer");
+  hipLaunchKernelGGL(k_inv_degree, dim3(cdiv(n_rows, 256)), dim3(256), 0, as_stream(stream_),
+                     rowptr, n_rows, inv_deg);
+  return check_launch("k_inv_degree");
+}
+
+}  // extern "C"

@@ -1,0 +1,293 @@
+// K1 / K2: segmented gather-reduce over a CSR — the E x d heart of SAGE mean aggregation.
+//
+//   out[i,:] (+)= s_i * sum_{p in row i} w_p * x[col[p], :]
+//
+// HBM-bound (algorithmic bytes per edge: 4 B index + 4*d B source row [+ 4 B weight]).
+// Mapping (wave64, one item per wave):
+//   * a row of d floats is read by LPR lanes, 16 B (float4) per lane and VPL vectors per lane,
+//     so a wave covers NS = 64/LPR rows per load instruction (d=64: 4 rows x 256 B = 1 KiB);
+//   * the wave pulls 64 column indices (and weights) of its row with one coalesced load, then
+//     each slot of LPR lanes takes every NS-th edge, UNROLL rows in flight per slot;
+//   * slots are combined with xor-shuffles; the first slot writes the row (full 256-B lines).
+// No atomics: each destination row is owned by one wave, so sums are deterministic.  Rows longer
+// than `chunk` edges (power-law heads) are split by the plan into chunk-sized items whose
+// partial sums go to a slab, then k_fixup adds them in chunk order.
+#include "hgnn_common.h"
+
+namespace hgnn {
+
+struct GatherArgs {
+  const float* x;
+  const int32_t* rowptr;
+  const int32_t* col;
+  const float* edge_w;
+  const float* col_w;
+  const int32_t* heavy_rows;
+  const int32_t* heavy_first;
+  float* slab;
+  float* out;
+  int64_t n_rows;
+  int64_t n_heavy;
+  int64_t n_items;
+  int32_t d;
+  int32_t chunk;
+  int32_t mean;
+  int32_t accumulate;
+};
+
+template <int W>
+struct Vec;
+template <>
+struct Vec<4> {
+  using T = float4;
+  static __device__ __forceinline__ T zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  static __device__ __forceinline__ T load(const float* p) {
+    return *reinterpret_cast<const float4*>(p);
+  }
+  static __device__ __forceinline__ void store(float* p, T v) {
+    *reinterpret_cast<float4*>(p) = v;
+  }
+  static __device__ __forceinline__ void fma(T& a, float w, T v) {
+    a.x = fmaf(w, v.x, a.x); a.y = fmaf(w, v.y, a.y);
+    a.z = fmaf(w, v.z, a.z); a.w = fmaf(w, v.w, a.w);
+  }
+  static __device__ __forceinline__ void add(T& a, T v) {
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  static __device__ __forceinline__ void scale(T& a, float s) {
+    a.x *= s; a.y *= s; a.z *= s; a.w *= s;
+  }
+  static __device__ __forceinline__ T shfl_xor(T v, int m) {
+    return make_float4(__shfl_xor(v.x, m, 64), __shfl_xor(v.y, m, 64), __shfl_xor(v.z, m, 64),
+                       __shfl_xor(v.w, m, 64));
+  }
+};
+template <>
+struct Vec<1> {
+  using T = float;
+  static __device__ __forceinline__ T zero() { return 0.f; }
+  static __device__ __forceinline__ T load(const float* p) { return *p; }
+  static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
+  static __device__ __forceinline__ void fma(T& a, float w, T v) { a = fmaf(w, v, a); }
+  static __device__ __forceinline__ void add(T& a, T v) { a += v; }
+  static __device__ __forceinline__ void scale(T& a, float s) { a *= s; }
+  static __device__ __forceinline__ T shfl_xor(T v, int m) { return __shfl_xor(v, m, 64); }
+};
+
+// Sum of row segment [beg, end) into acc (per lane: VPL vectors of width W).
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W>
+__device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, int64_t end,
+                                            typename Vec<W>::T (&acc)[VPL]) {
+  using V = Vec<W>;
+  constexpr int NS = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / LPR, sl = lane % LPR;
+  const int d = a.d;
+  for (int64_t base = beg; base < end; base += 64) {
+    const int n = (int)min<int64_t>(64, end - base);
+    int cidx = 0;
+    float wv = 1.f;
+    if (lane < n) {
+      cidx = a.col[base + lane];
+      if (HAS_W) {
+        wv = a.edge_w ? a.edge_w[base + lane] : 1.f;
+        if (a.col_w) wv *= a.col_w[cidx];
+      }
+    }
+    for (int j = 0; j < n; j += NS * UNROLL) {
+      typename V::T v[UNROLL][VPL];
+      float we[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int e = j + u * NS + slot;
+        const int src = __shfl(cidx, e & 63, 64);
+        we[u] = HAS_W ? __shfl(wv, e & 63, 64) : 1.f;
+        const float* xr = a.x + (int64_t)src * d;
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+          const int c = (q * LPR + sl) * W;
+          v[u][q] = (e < n && c < d) ? V::load(xr + c) : V::zero();
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+        for (int q = 0; q < VPL; ++q) {
+          if (HAS_W) V::fma(acc[q], we[u], v[u][q]);
+          else V::add(acc[q], v[u][q]);
+        }
+    }
+  }
+  // combine the NS slots (lanes sl, sl+LPR, ...)
+#pragma unroll
+  for (int m = LPR; m < 64; m <<= 1)
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) V::add(acc[q], V::shfl_xor(acc[q], m));
+}
+
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W>
+__global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
+  using V = Vec<W>;
+  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= a.n_items) return;
+  const int lane = threadIdx.x & 63;
+  const int sl = lane % LPR;
+  const bool writer = lane < LPR;
+  int64_t row, beg, end;
+  float* dst;
+  bool partial;
+  if (item < a.n_rows) {                       // light row: whole row in this wave
+    row = item;
+    beg = a.rowptr[row];
+    end = a.rowptr[row + 1];
+    if (end - beg > a.chunk) return;            // heavy: handled by chunks + fixup
+    dst = a.out + row * a.d;
+    partial = false;
+  } else {                                      // chunk of a heavy row -> slab slot
+    const int64_t slot = item - a.n_rows;
+    int64_t lo = 0, hi = a.n_heavy;             // heavy_first[h] <= slot < heavy_first[h+1]
+    while (hi - lo > 1) {
+      int64_t mid = (lo + hi) >> 1;
+      if (a.heavy_first[mid] <= slot) lo = mid; else hi = mid;
+    }
+    row = a.heavy_rows[lo];
+    const int64_t k = slot - a.heavy_first[lo];
+    beg = a.rowptr[row] + k * a.chunk;
+    end = min<int64_t>(beg + a.chunk, a.rowptr[row + 1]);
+    dst = a.slab + slot * a.d;
+    partial = true;
+  }
+  typename V::T acc[VPL];
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) acc[q] = V::zero();
+  segment_sum<LPR, VPL, W, UNROLL, HAS_W>(a, beg, end, acc);
+  if (!writer) return;
+  float s = 1.f;
+  if (!partial && a.mean) s = end > beg ? 1.f / (float)(end - beg) : 0.f;
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) {
+    const int c = (q * LPR + sl) * W;
+    if (c < a.d) {
+      typename V::T r = acc[q];
+      if (!partial) {
+        V::scale(r, s);
+        if (a.accumulate) V::add(r, V::load(dst + c));
+      }
+      V::store(dst + c, r);
+    }
+  }
+}
+
+// Heavy rows: out[row] (+)= s * sum_k slab[first + k]  (chunk order => deterministic).
+template <int W>
+__global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
+  using V = Vec<W>;
+  const int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (h >= a.n_heavy) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = a.heavy_rows[h];
+  const int64_t f0 = a.heavy_first[h], f1 = a.heavy_first[h + 1];
+  const int64_t deg = a.rowptr[row + 1] - a.rowptr[row];
+  const float s = a.mean ? (deg > 0 ? 1.f / (float)deg : 0.f) : 1.f;
+  for (int c = lane * W; c < a.d; c += 64 * W) {
+    typename V::T r = V::zero();
+    for (int64_t k = f0; k < f1; ++k) V::add(r, V::load(a.slab + k * a.d + c));
+    V::scale(r, s);
+    float* o = a.out + row * a.d + c;
+    if (a.accumulate) V::add(r, V::load(o));
+    V::store(o, r);
+  }
+}
+
+template <int LPR, int VPL, int W, int UNROLL>
+static int launch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) {
+  const dim3 grid((unsigned)cdiv(a.n_items, 4)), block(256);
+  if (has_w)
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, 0, stream, a);
+  else
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, 0, stream, a);
+  return check_launch("k_gather");
+}
+
+static int dispatch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) {
+  const int d = a.d;
+  if (d % 4 == 0) {
+    const int nv = d / 4;  // float4 vectors per row
+    if (nv <= 4) return launch_gather<4, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 8) return launch_gather<8, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 16) return launch_gather<16, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 32) return launch_gather<32, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 64) return launch_gather<64, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 128) return launch_gather<64, 2, 4, 2>(a, has_w, stream);
+    if (nv <= 256) return launch_gather<64, 4, 4, 2>(a, has_w, stream);
+    return fail(HGNN_E_UNSUPPORTED, "gather: d=%d > 1024", d);
+  }
+  if (d <= 16) return launch_gather<16, 1, 1, 4>(a, has_w, stream);
+  if (d <= 64) return launch_gather<64, 1, 1, 4>(a, has_w, stream);
+  if (d <= 256) return launch_gather<64, 4, 1, 2>(a, has_w, stream);
+  if (d <= 1024) return launch_gather<64, 16, 1, 1>(a, has_w, stream);
+  return fail(HGNN_E_UNSUPPORTED, "gather: d=%d > 1024", d);
+}
+
+static int run_gather(GatherArgs a, hipStream_t stream) {
+  if (a.d <= 0 || a.n_rows < 0 || a.n_heavy < 0 || a.chunk <= 0)
+    return fail(HGNN_E_ARG, "gather: bad sizes d=%d n_rows=%lld chunk=%d", a.d,
+                (long long)a.n_rows, a.chunk);
+  if (a.n_rows == 0) return HGNN_OK;
+  // x / col may be null only for a CSR without edges (nothing is dereferenced then)
+  if (!a.rowptr || !a.out) return fail(HGNN_E_ARG, "gather: null rowptr/out");
+  if (a.n_heavy > 0 && (!a.heavy_rows || !a.heavy_first || !a.slab))
+    return fail(HGNN_E_ARG, "gather: heavy rows without plan/slab");
+  const bool has_w = a.edge_w || a.col_w;
+  if (int rc = dispatch_gather(a, has_w, stream)) return rc;
+  if (a.n_heavy > 0) {
+    const dim3 grid((unsigned)cdiv(a.n_heavy, 4)), block(256);
+    if (a.d % 4 == 0) hipLaunchKernelGGL(k_fixup<4>, grid, block, 0, stream, a);
+    else hipLaunchKernelGGL(k_fixup<1>, grid, block, 0, stream, a);
+    return check_launch("k_fixup");
+  }
+  return HGNN_OK;
+}
+
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* rowptr,
+                       const int32_t* col, int64_t n_rows, const float* edge_w,
+                       const float* col_w, int32_t flags, const int32_t* heavy_rows,
+                       const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                       int32_t chunk, float* slab, float* out, hgnn_stream_t stream) {
+  (void)n_x;
+  GatherArgs a{};
+  a.x = x; a.rowptr = rowptr; a.col = col; a.edge_w = edge_w; a.col_w = col_w;
+  a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
+  a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
+  a.d = d; a.chunk = chunk; a.mean = (flags & HGNN_MEAN) ? 1 : 0;
+  a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+  return run_gather(a, as_stream(stream));
+}
+
+int hgnn_gather_mean_fwd(const float* x_src, int64_t n_src, int32_t d, const int32_t* rowptr,
+                         const int32_t* col, int64_t n_dst, const int32_t* heavy_rows,
+                         const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                         int32_t chunk, float* slab, float* aggr, hgnn_stream_t stream) {
+  return hgnn_gather_reduce(x_src, n_src, d, rowptr, col, n_dst, nullptr, nullptr, HGNN_MEAN,
+                            heavy_rows, heavy_first, n_heavy, n_chunks, chunk, slab, aggr,
+                            stream);
+}
+
+int hgnn_scatter_mean_bwd(const float* grad_aggr, int64_t n_dst, const float* inv_deg,
+                          const int32_t* t_rowptr, const int32_t* t_col, int64_t n_src,
+                          int32_t d, const int32_t* heavy_rows, const int32_t* heavy_first,
+                          int64_t n_heavy, int64_t n_chunks, int32_t chunk, float* slab,
+                          float* grad_x_src, int32_t accumulate, hgnn_stream_t stream) {
+  if (!inv_deg && n_src > 0) return fail(HGNN_E_ARG, "scatter_mean_bwd: inv_deg is null");
+  return hgnn_gather_reduce(grad_aggr, n_dst, d, t_rowptr, t_col, n_src, nullptr, inv_deg,
+                            accumulate ? HGNN_ACCUMULATE : 0, heavy_rows, heavy_first, n_heavy,
+                            n_chunks, chunk, slab, grad_x_src, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,419 @@
+// K3/K4: fused multi-segment linear on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact fp32 fma chain).
+//
+//   out[n, h] = act( sum_s X_s[n, K_s] @ W[:, off_s : off_s+K_s]^T + b )
+//
+// One call is a whole SAGE destination update: the segments are the per-relation mean
+// aggregates and the destination's own features, W is the K-concatenation of the relation
+// weights pre-scaled by the reference's fixed relation weights (train_gnn.py:163-164,187-198),
+// act = ReLU.  That fuses lin_l + lin_r + weighted sum + bias + ReLU into one pass over HBM.
+//
+// MFMA operand trick: for a 16-wide K chunk, lane (i = lane&15, g = lane>>4) loads the float4
+// X[row i][kc+4g .. kc+4g+3] and uses element q as the A operand of k-step q; B takes the same
+// k from W.  So k-step q sums k = kc+4g+q over g — every k of the chunk exactly once, with
+// contiguous 16-B loads (the k order inside a chunk is permuted, which only moves rounding).
+#include "hgnn_common.h"
+
+#include <algorithm>
+
+namespace hgnn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Seg {
+  const float* x;
+  float* dx;
+  int32_t k;
+  int32_t off;
+};
+
+struct LinArgs {
+  Seg seg[HGNN_MAX_SEG];
+  int32_t n_seg;
+  int32_t k_total;
+  const float* w;
+  const float* bias;
+  const float* dout;
+  const float* out_act;   // ReLU output for the backward mask (nullable)
+  float* out;
+  float* slab;            // wgrad partials [gx][h][k_total+1]
+  int64_t n;
+  int32_t h;
+  int32_t relu;
+  int64_t rows_per_block; // wgrad
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <bool VEC>
+__device__ __forceinline__ void load4(const float* p, int valid_elems, float (&v)[4]) {
+  if (VEC) {
+    if (valid_elems >= 4) {
+      float4 t = *reinterpret_cast<const float4*>(p);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+      v[0] = v[1] = v[2] = v[3] = 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = q < valid_elems ? p[q] : 0.f;
+  }
+}
+
+constexpr int RT = 2;             // 16-row tiles per wave
+constexpr int kRowsPerBlock = 4 * RT * 16;
+
+// ---------------------------------------------------------------- forward
+template <int NT, bool VEC>
+__global__ void __launch_bounds__(256) k_linear_fwd(const LinArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock + wave * (RT * 16);
+  const int c0 = blockIdx.y * (NT * 16);
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < a.n_seg; ++s) {
+    const Seg sg = a.seg[s];
+    for (int kc = 0; kc < sg.k; kc += 16) {
+      const int k = kc + 4 * g;
+      const int kv = sg.k - k;  // valid elements from k
+      float av[RT][4], bv[NT][4];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int64_t row = r0 + rt * 16 + i;
+        if (row < a.n) load4<VEC>(sg.x + row * sg.k + k, kv, av[rt]);
+        else av[rt][0] = av[rt][1] = av[rt][2] = av[rt][3] = 0.f;
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = c0 + t * 16 + i;
+        if (col < a.h) load4<VEC>(a.w + (int64_t)col * a.k_total + sg.off + k, kv, bv[t]);
+        else bv[t][0] = bv[t][1] = bv[t][2] = bv[t][3] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[rt][t] = mfma4(av[rt][q], bv[t][q], acc[rt][t]);
+    }
+  }
+  // C/D map of 16x16x4: col = lane&15, row = 4*(lane>>4) + reg
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = c0 + t * 16 + i;
+    if (col >= a.h) continue;
+    const float b = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t row = r0 + rt * 16 + 4 * g + j;
+        if (row < a.n) {
+          float v = acc[rt][t][j] + b;
+          if (a.relu) v = fmaxf(v, 0.f);
+          a.out[row * a.h + col] = v;
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------- dgrad: dX_s = dZ @ W_s
+template <bool VEC>
+__device__ __forceinline__ void load_dz(const LinArgs& a, int64_t row, int j, float (&v)[4]) {
+  const int jv = a.h - j;
+  if (row >= a.n) { v[0] = v[1] = v[2] = v[3] = 0.f; return; }
+  load4<VEC>(a.dout + row * a.h + j, jv, v);
+  if (a.out_act) {
+    float m[4];
+    load4<VEC>(a.out_act + row * a.h + j, jv, m);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = m[q] > 0.f ? v[q] : 0.f;
+  }
+}
+
+template <int NT, bool VEC>
+__global__ void __launch_bounds__(256) k_linear_dgrad(const LinArgs a) {
+  const int c0 = blockIdx.y * (NT * 16);
+  bool any = false;
+  for (int s = 0; s < a.n_seg; ++s)
+    any |= a.seg[s].dx && a.seg[s].off < c0 + NT * 16 && a.seg[s].off + a.seg[s].k > c0;
+  if (!any) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock + wave * (RT * 16);
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int jc = 0; jc < a.h; jc += 16) {
+    const int j = jc + 4 * g;
+    float av[RT][4], bv[NT][4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) load_dz<VEC>(a, r0 + rt * 16 + i, j, av[rt]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = c0 + t * 16 + i;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        bv[t][q] = (col < a.k_total && j + q < a.h) ? a.w[(int64_t)(j + q) * a.k_total + col]
+                                                    : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[rt][t] = mfma4(av[rt][q], bv[t][q], acc[rt][t]);
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = c0 + t * 16 + i;
+    if (col >= a.k_total) continue;
+    int s = 0;
+    while (s + 1 < a.n_seg && col >= a.seg[s].off + a.seg[s].k) ++s;
+    float* dx = a.seg[s].dx;
+    if (!dx) continue;
+    const int kk = col - a.seg[s].off, ks = a.seg[s].k;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int64_t row = r0 + rt * 16 + 4 * g + jj;
+        if (row < a.n) dx[row * ks + kk] = acc[rt][t][jj];
+      }
+  }
+}
+
+// ---------------------------------------------------------------- wgrad partials
+// Block: 4 waves, j range of 64 (blockIdx.z), k range of 128 over [X_0..X_{S-1}, 1] (blockIdx.y;
+// the trailing ones column gives db), rows [bx*rows_per_block, ...) staged 32 at a time in LDS.
+constexpr int WG_ROWS = 32;
+constexpr int WG_J = 64;
+constexpr int WG_K = 128;
+constexpr int DZ_LD = WG_J + 16;   // row stride = 16 mod 32 banks: lanes g and g+1 disjoint
+constexpr int X_LD = WG_K + 16;
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_linear_wgrad(const LinArgs a) {
+  __shared__ __attribute__((aligned(16))) float lds[WG_ROWS * DZ_LD + WG_ROWS * X_LD];
+  float* dz_l = lds;
+  float* x_l = lds + WG_ROWS * DZ_LD;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int j0 = blockIdx.z * WG_J, k0 = blockIdx.y * WG_K;
+  const int kext = a.k_total + 1;
+  const int64_t rb = (int64_t)blockIdx.x * a.rows_per_block;
+  const int64_t re = min<int64_t>(rb + a.rows_per_block, a.n);
+  f32x4 acc[WG_K / 16];
+#pragma unroll
+  for (int t = 0; t < WG_K / 16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t rs = rb; rs < re; rs += WG_ROWS) {
+    // stage dZ[32][64] (masked) and X[32][128]: one float4 per (row, 4 columns)
+    for (int idx = threadIdx.x; idx < WG_ROWS * (WG_J / 4); idx += 256) {
+      const int r = idx / (WG_J / 4), c4 = idx % (WG_J / 4);
+      float v[4];
+      load_dz<VEC>(a, rs + r < re ? rs + r : a.n, j0 + 4 * c4, v);
+      *reinterpret_cast<float4*>(dz_l + r * DZ_LD + 4 * c4) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    for (int idx = threadIdx.x; idx < WG_ROWS * (WG_K / 4); idx += 256) {
+      const int r = idx / (WG_K / 4), c4 = idx % (WG_K / 4);
+      const int64_t row = rs + r;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (row < re) {
+        const int kg = k0 + 4 * c4;
+        if (VEC && kg + 4 <= a.k_total) {
+          int s = 0;
+          while (s + 1 < a.n_seg && kg >= a.seg[s].off + a.seg[s].k) ++s;
+          const float4 t =
+              *reinterpret_cast<const float4*>(a.seg[s].x + row * a.seg[s].k + kg - a.seg[s].off);
+          v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int kq = kg + q;
+            if (kq < a.k_total) {
+              int s = 0;
+              while (s + 1 < a.n_seg && kq >= a.seg[s].off + a.seg[s].k) ++s;
+              v[q] = a.seg[s].x[row * a.seg[s].k + kq - a.seg[s].off];
+            } else if (kq == a.k_total) {
+              v[q] = 1.f;
+            }
+          }
+        }
+      }
+      *reinterpret_cast<float4*>(x_l + r * X_LD + 4 * c4) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    // A[i = j][kk = row] = dZ[row][j], B[kk = row][col = k] = X[row][k]; k-step s covers rows 4s..4s+3
+#pragma unroll
+    for (int s = 0; s < WG_ROWS / 4; ++s) {
+      const int r = 4 * s + g;
+      const float av = dz_l[r * DZ_LD + wave * 16 + i];
+#pragma unroll
+      for (int t = 0; t < WG_K / 16; ++t) acc[t] = mfma4(av, x_l[r * X_LD + t * 16 + i], acc[t]);
+    }
+    __syncthreads();
+  }
+  // partial tile: rows j = j0 + wave*16 + 4g + jj, cols k = k0 + 16t + i
+  float* slab = a.slab + (int64_t)blockIdx.x * a.h * kext;
+#pragma unroll
+  for (int t = 0; t < WG_K / 16; ++t) {
+    const int k = k0 + t * 16 + i;
+    if (k >= kext) continue;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int j = j0 + wave * 16 + 4 * g + jj;
+      if (j < a.h) slab[(int64_t)j * kext + k] = acc[t][jj];
+    }
+  }
+}
+
+// dw[j][k] = sum_b slab[b][j][k] (k < K), db[j] = sum_b slab[b][j][K]; fixed b order.
+__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
+                                                      int32_t kext, float* dw, float* db) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t total = (int64_t)h * kext;
+  const int64_t per = cdiv(nb, 4);
+  float s = 0.f;
+  if (e < total) {
+    const int64_t b0 = wave * per, b1 = min<int64_t>(b0 + per, nb);
+    for (int64_t b = b0; b < b1; ++b) s += slab[b * total + e];
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < total) {
+    const float v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    const int j = (int)(e / kext), k = (int)(e % kext);
+    if (k < kext - 1) { if (dw) dw[(int64_t)j * (kext - 1) + k] = v; }
+    else if (db) db[j] = v;
+  }
+}
+
+static int fill_args(LinArgs& a, int32_t n_seg, const float* const* xs, const int32_t* ks,
+                     float* const* dxs, int64_t n_rows, const float* w, int32_t h, bool* vec) {
+  if (n_seg < 1 || n_seg > HGNN_MAX_SEG) return fail(HGNN_E_ARG, "linear: n_seg=%d", n_seg);
+  if (h < 1 || n_rows < 0 || !w || !xs || !ks) return fail(HGNN_E_ARG, "linear: bad arguments");
+  a.n_seg = n_seg;
+  a.k_total = 0;
+  *vec = (h % 4 == 0);
+  for (int s = 0; s < n_seg; ++s) {
+    if (ks[s] < 1 || (n_rows > 0 && !xs[s])) return fail(HGNN_E_ARG, "linear: segment %d", s);
+    a.seg[s].x = xs[s];
+    a.seg[s].dx = dxs ? dxs[s] : nullptr;
+    a.seg[s].k = ks[s];
+    a.seg[s].off = a.k_total;
+    a.k_total += ks[s];
+    *vec = *vec && ks[s] % 4 == 0 && (reinterpret_cast<uintptr_t>(xs[s]) % 16 == 0);
+  }
+  *vec = *vec && reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  a.w = w;
+  a.n = n_rows;
+  a.h = h;
+  return HGNN_OK;
+}
+
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                    const float* w, int32_t h, const float* bias, int32_t relu, float* out,
+                    hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  LinArgs a{};
+  bool vec;
+  if (int rc = fill_args(a, n_seg, xs, ks, nullptr, n_rows, w, h, &vec)) return rc;
+  if (n_rows == 0) return HGNN_OK;
+  if (!out) return fail(HGNN_E_ARG, "linear_fwd: out is null");
+  vec = vec && reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  a.bias = bias;
+  a.out = out;
+  a.relu = relu;
+  const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
+  if (h <= 64) {
+    const dim3 grid(gx, 1);
+    if (vec) hipLaunchKernelGGL((k_linear_fwd<4, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_linear_fwd<4, false>), grid, dim3(256), 0, stream, a);
+  } else {
+    const dim3 grid(gx, (unsigned)cdiv(h, 128));
+    if (vec) hipLaunchKernelGGL((k_linear_fwd<8, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_linear_fwd<8, false>), grid, dim3(256), 0, stream, a);
+  }
+  return check_launch("k_linear_fwd");
+}
+
+static void wgrad_grid(int64_t n_rows, int32_t k_total, int32_t h, int64_t* gx, int64_t* rpb) {
+  const int64_t gy = cdiv(k_total + 1, WG_K), gz = cdiv(h, WG_J);
+  const int64_t tiles = cdiv(n_rows, WG_ROWS);
+  int64_t want = std::max<int64_t>(1, 1024 / (gy * gz));
+  const int64_t cap = std::max<int64_t>(1, (int64_t(64) << 20) / ((int64_t)h * (k_total + 1) * 4));
+  want = std::min(want, cap);
+  want = std::max<int64_t>(1, std::min(want, tiles));
+  *rpb = cdiv(tiles, want) * WG_ROWS;
+  *gx = std::max<int64_t>(1, cdiv(n_rows, *rpb));
+}
+
+size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h) {
+  int64_t gx, rpb;
+  wgrad_grid(n_rows < 1 ? 1 : n_rows, k_total, h, &gx, &rpb);
+  return align_up((size_t)gx * h * (k_total + 1) * 4, 256) + 256;
+}
+
+int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                    const float* w, int32_t h, const float* dout, const float* out,
+                    float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,
+                    hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  LinArgs a{};
+  bool vec;
+  if (int rc = fill_args(a, n_seg, xs, ks, dxs, n_rows, w, h, &vec)) return rc;
+  if (!dout && n_rows > 0) return fail(HGNN_E_ARG, "linear_bwd: dout is null");
+  a.dout = dout;
+  a.out_act = out;
+  vec = vec && reinterpret_cast<uintptr_t>(dout) % 16 == 0 &&
+        (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  for (int s = 0; s < n_seg; ++s)
+    vec = vec && (!a.seg[s].dx || reinterpret_cast<uintptr_t>(a.seg[s].dx) % 16 == 0);
+  if (n_rows == 0) {  // no rows: weight grads are zero
+    if (dw) (void)hipMemsetAsync(dw, 0, (size_t)h * a.k_total * 4, stream);
+    if (db) (void)hipMemsetAsync(db, 0, (size_t)h * 4, stream);
+    return check_launch("linear_bwd(n=0)");
+  }
+  bool any_dx = false;
+  for (int s = 0; s < n_seg; ++s) any_dx |= a.seg[s].dx != nullptr;
+  if (any_dx) {
+    const dim3 grid((unsigned)cdiv(n_rows, kRowsPerBlock), (unsigned)cdiv(a.k_total, 128));
+    if (vec) hipLaunchKernelGGL((k_linear_dgrad<8, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_linear_dgrad<8, false>), grid, dim3(256), 0, stream, a);
+    if (int rc = check_launch("k_linear_dgrad")) return rc;
+  }
+  if (dw || db) {
+    int64_t gx, rpb;
+    wgrad_grid(n_rows, a.k_total, h, &gx, &rpb);
+    const size_t need = (size_t)gx * h * (a.k_total + 1) * 4;
+    if (!ws || ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+    a.slab = static_cast<float*>(ws);
+    a.rows_per_block = rpb;
+    const dim3 grid((unsigned)gx, (unsigned)cdiv(a.k_total + 1, WG_K), (unsigned)cdiv(h, WG_J));
+    if (vec) hipLaunchKernelGGL(k_linear_wgrad<true>, grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(k_linear_wgrad<false>, grid, dim3(256), 0, stream, a);
+    if (int rc = check_launch("k_linear_wgrad")) return rc;
+    const int64_t total = (int64_t)h * (a.k_total + 1);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+                       a.slab, gx, h, a.k_total + 1, dw, db);
+    if (int rc = check_launch("k_wgrad_reduce")) return rc;
+  }
+  return HGNN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,235 @@
+"""Graph container and the device-resident CSR/CSC cache.
+
+``HeteroData`` is the slice of PyG's container the reference uses (``train_gnn.py:115-142,
+211-216``; ``test_gnn.py:73-109``; ``inference.py:410-419``): ``graph['user'].x = ...``,
+``graph['user','social','user'].edge_index = ...``, ``graph.to(device)``,
+``graph.edge_index_dict``, ``graph['user'].num_nodes``.
+
+``RelationCSR`` is what the kernels walk: for a COO ``edge_index`` [2,E] (row 0 = source,
+row 1 = destination, PyG's source_to_target flow) it holds the stable CSR grouped by destination
+(forward gather, K1) and, on demand, the stable CSC grouped by source (backward, K2), 1/deg, and
+the degree-skew plans.  Built on the GPU by K5 once per graph and cached, keyed by the edge
+tensor's storage pointer, version counter and shape.
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+import weakref
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+EdgeType = Tuple[str, str, str]
+
+
+# ----------------------------------------------------------------------------- HeteroData (lite)
+class _Storage:
+    def __init__(self):
+        object.__setattr__(self, "_d", {})
+
+    def __getattr__(self, k):
+        d = object.__getattribute__(self, "_d")
+        if k in d:
+            return d[k]
+        raise AttributeError(k)
+
+    def __setattr__(self, k, v):
+        self._d[k] = v
+
+    def __contains__(self, k):
+        return k in self._d
+
+    def items(self):
+        return self._d.items()
+
+
+class NodeStorage(_Storage):
+    @property
+    def num_nodes(self) -> int:
+        return int(self._d["x"].shape[0])
+
+
+class EdgeStorage(_Storage):
+    @property
+    def num_edges(self) -> int:
+        return int(self._d["edge_index"].shape[1])
+
+
+class HeteroData:
+    """Minimal PyG ``HeteroData``: node stores keyed by type, edge stores by (src, rel, dst)."""
+
+    def __init__(self):
+        self._nodes: Dict[str, NodeStorage] = {}
+        self._edges: Dict[EdgeType, EdgeStorage] = {}
+
+    def __getitem__(self, key):
+        if isinstance(key, str):
+            return self._nodes.setdefault(key, NodeStorage())
+        if isinstance(key, tuple) and len(key) == 3:
+            return self._edges.setdefault(tuple(key), EdgeStorage())
+        raise KeyError(key)
+
+    @property
+    def node_types(self):
+        return list(self._nodes)
+
+    @property
+    def edge_types(self):
+        return list(self._edges)
+
+    def metadata(self):
+        return self.node_types, self.edge_types
+
+    @property
+    def x_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v.x for k, v in self._nodes.items() if "x" in v}
+
+    @property
+    def edge_index_dict(self) -> Dict[EdgeType, torch.Tensor]:
+        return {k: v.edge_index for k, v in self._edges.items() if "edge_index" in v}
+
+    def to(self, device) -> "HeteroData":
+        for store in list(self._nodes.values()) + list(self._edges.values()):
+            for k, v in list(store.items()):
+                if torch.is_tensor(v):
+                    setattr(store, k, v.to(device))
+        return self
+
+
+# ----------------------------------------------------------------------------- CSR cache
+def default_chunk(num_edges: int) -> int:
+    """Split rows longer than about a quarter of one wave's share of the edges
+    (cdna_hip_programming.md App. B 'Scatter / gather'): 256 CUs x 32 waves in flight."""
+    share = max(num_edges // (256 * 32 * 4), 1)
+    c = 1 << (share.bit_length() - 1)
+    return int(min(max(c, 64), 1024))
+
+
+@dataclasses.dataclass
+class Plan:
+    chunk: int
+    n_heavy: int
+    n_chunks: int
+    heavy_rows: Optional[torch.Tensor]
+    heavy_first: Optional[torch.Tensor]
+
+
+@dataclasses.dataclass
+class GroupedEdges:
+    rowptr: torch.Tensor     # int32 [n_rows+1]
+    col: torch.Tensor        # int32 [E]
+    perm: torch.Tensor       # int32 [E] original edge id of each CSR position
+    plan: Plan
+    n_rows: int
+
+
+def _plan(rowptr: torch.Tensor, n_rows: int, chunk: int) -> Plan:
+    dev = rowptr.device
+    if n_rows == 0:
+        return Plan(chunk, 0, 0, None, None)
+    lib, s = N.lib(), N.stream_ptr(dev)
+    ws = N.workspace(lib.hgnn_plan_ws_bytes(n_rows), dev)
+    counts = torch.zeros(2, dtype=torch.int32, device=dev)
+    N.check(lib.hgnn_plan_count(N.ptr(rowptr), n_rows, chunk, N.ptr(counts), N.ptr(ws),
+                                ws.numel(), s), "hgnn_plan_count")
+    n_heavy, n_chunks = (int(v) for v in counts.tolist())   # host sync: once per graph
+    if n_heavy == 0:
+        return Plan(chunk, 0, 0, None, None)
+    heavy_rows = torch.empty(n_heavy, dtype=torch.int32, device=dev)
+    heavy_first = torch.empty(n_heavy + 1, dtype=torch.int32, device=dev)
+    N.check(lib.hgnn_plan_fill(N.ptr(rowptr), n_rows, chunk, N.ptr(heavy_rows),
+                               N.ptr(heavy_first), N.ptr(ws), ws.numel(), s), "hgnn_plan_fill")
+    return Plan(chunk, n_heavy, n_chunks, heavy_rows, heavy_first)
+
+
+def group_edges(key: torch.Tensor, other: torch.Tensor, n_keys: int, n_other: int,
+                chunk: Optional[int] = None) -> GroupedEdges:
+    """K5: stable grouping of COO by ``key`` (int64 device tensors) -> CSR + skew plan."""
+    dev = N.require_device(key, other)
+    E = int(key.numel())
+    if E >= 2**31 - 1 or n_keys >= 2**31 - 1 or n_other >= 2**31 - 1:
+        raise ValueError(f"graph too large for int32 CSR: E={E} n_keys={n_keys}")
+    key = key.contiguous().to(torch.int64)
+    other = other.contiguous().to(torch.int64)
+    lib, s = N.lib(), N.stream_ptr(dev)
+    rowptr = torch.empty(n_keys + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(E, dtype=torch.int32, device=dev)
+    perm = torch.empty(E, dtype=torch.int32, device=dev)
+    invalid = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = N.workspace(lib.hgnn_coo_to_csr_ws_bytes(E, n_keys), dev)
+    N.check(lib.hgnn_coo_to_csr(N.ptr(key), N.ptr(other), E, n_keys, n_other, N.ptr(rowptr),
+                                N.ptr(col), N.ptr(perm), N.ptr(invalid), N.ptr(ws), ws.numel(), s),
+            "hgnn_coo_to_csr")
+    bad = int(invalid.item())   # host sync: once per graph
+    if bad:
+        raise ValueError(f"edge_index has {bad} edge(s) with an endpoint out of range "
+                         f"(n_keys={n_keys}, n_other={n_other}); the reference masks these out "
+                         "before building the graph (train_gnn.py:128-133)")
+    c = chunk if chunk is not None else default_chunk(E)
+    return GroupedEdges(rowptr, col, perm, _plan(rowptr, n_keys, c), n_keys)
+
+
+class RelationCSR:
+    """Cached device structures for one relation (edge_index [2,E], n_src, n_dst)."""
+
+    def __init__(self, edge_index: torch.Tensor, n_src: int, n_dst: int,
+                 chunk: Optional[int] = None):
+        if edge_index.dim() != 2 or edge_index.shape[0] != 2:
+            raise ValueError(f"edge_index must be [2, E], got {tuple(edge_index.shape)}")
+        self.n_src, self.n_dst = int(n_src), int(n_dst)
+        self.num_edges = int(edge_index.shape[1])
+        self.chunk = chunk
+        self._ei = edge_index
+        self.fwd = group_edges(edge_index[1], edge_index[0], self.n_dst, self.n_src, chunk)
+        self.inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=edge_index.device)
+        N.check(N.lib().hgnn_inv_degree(N.ptr(self.fwd.rowptr), self.n_dst, N.ptr(self.inv_deg),
+                                        N.stream_ptr(edge_index.device)), "hgnn_inv_degree")
+        self._bwd: Optional[GroupedEdges] = None
+
+    @property
+    def bwd(self) -> GroupedEdges:
+        """Transposed grouping (by source), built on first backward that needs it."""
+        if self._bwd is None:
+            self._bwd = group_edges(self._ei[0], self._ei[1], self.n_src, self.n_dst, self.chunk)
+        return self._bwd
+
+    def release_coo(self):
+        """Drop the COO reference once the CSC exists (saves 16 B/edge of HBM)."""
+        if self._bwd is not None:
+            self._ei = None
+
+
+class _CsrCache:
+    def __init__(self, cap: int = 64):
+        self.cap = cap
+        self._d: "collections.OrderedDict" = collections.OrderedDict()
+
+    def get(self, edge_index: torch.Tensor, n_src: int, n_dst: int,
+            chunk: Optional[int] = None) -> RelationCSR:
+        key = (edge_index.data_ptr(), edge_index._version, tuple(edge_index.shape),
+               tuple(edge_index.stride()), edge_index.device, int(n_src), int(n_dst), chunk)
+        hit = self._d.get(key)
+        if hit is not None:
+            ref, csr = hit
+            if ref() is edge_index:
+                self._d.move_to_end(key)
+                return csr
+        csr = RelationCSR(edge_index, n_src, n_dst, chunk)
+        self._d[key] = (weakref.ref(edge_index), csr)
+        while len(self._d) > self.cap:
+            self._d.popitem(last=False)
+        return csr
+
+    def clear(self):
+        self._d.clear()
+
+
+CSR_CACHE = _CsrCache()
+
+
+def relation_csr(edge_index: torch.Tensor, n_src: int, n_dst: int,
+                 chunk: Optional[int] = None) -> RelationCSR:
+    return CSR_CACHE.get(edge_index, n_src, n_dst, chunk)

@@ -1,0 +1,284 @@
+"""Autograd operators over the HIP kernels.
+
+``hetero_layer`` is one full SAGE layer over every destination node type at once — the fused
+form of ``WeightedRGCN.forward`` (``train_gnn.py:166-200``):
+
+    y_dst = act( sum_r w_r * (mean_{src->dst} x_src @ W_l,r^T + b_r + x_dst @ W_r,r^T) )
+
+computed as: K1 ``gather_mean`` per relation, then ONE K3 multi-segment MFMA linear per
+destination over ``[aggr_1 .. aggr_R, x_dst]`` with the K-concatenated, relation-weighted
+weights (built by torch ops on the parameters, so autograd routes the gradients back to the
+reference's own per-conv parameters).  Backward: K3 dgrad/wgrad (ReLU mask fused), then K2
+``scatter_mean_bwd`` accumulating straight into the source-feature gradients, so the per-type
+gradient sums the reference's autograd would do with separate add kernels happen in-kernel.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _native as N
+from .graph import RelationCSR
+
+
+def _check_f32(t: torch.Tensor, what: str) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: hgnn computes in fp32 (the reference dtype); got {t.dtype}")
+    return t.contiguous()
+
+
+# ----------------------------------------------------------------------------- kernel timing
+class KernelTimer:
+    """Records HIP events around every kernel call this module makes (on the current stream,
+    the one the kernels are launched on), with each launch's algorithmic HBM bytes.  Used by
+    bench.py inside its timed region; ``None`` when off (zero overhead)."""
+
+    def __init__(self):
+        self.records = []   # (name, algorithmic bytes, start event, end event)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        agg = {}
+        for name, nbytes, s, e in self.records:
+            ms = s.elapsed_time(e)
+            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0})
+            a["launches"] += 1
+            a["ms"] += ms
+            a["bytes"] += nbytes
+        return agg
+
+
+_timer: Optional[KernelTimer] = None
+
+
+def set_timer(t: Optional[KernelTimer]) -> None:
+    global _timer
+    _timer = t
+
+
+class _timed:
+    def __init__(self, name, nbytes):
+        self.name, self.nbytes = name, nbytes
+
+    def __enter__(self):
+        if _timer is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if _timer is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            _timer.records.append((self.name, int(self.nbytes), self.s, e))
+
+
+def gather_bytes(n_edges: int, n_rows: int, d: int, weighted: bool) -> int:
+    """Algorithmic HBM bytes of one K1/K2 launch: per edge a 4-B index and one
+    4*d-B source row (+4 B weight for K2), rowptr, and the output rows."""
+    return 4 * n_edges * (1 + d + (1 if weighted else 0)) + 4 * (n_rows + 1) + 4 * n_rows * d
+
+
+# ----------------------------------------------------------------------------- raw kernel calls
+def gather_mean(x_src: torch.Tensor, csr: RelationCSR) -> torch.Tensor:
+    """K1: ``aggr[i] = mean_{(j->i)} x_src[j]`` (0 for an empty row)."""
+    x_src = _check_f32(x_src, "gather_mean")
+    dev = N.require_device(x_src, csr.fwd.rowptr)
+    if x_src.shape[0] != csr.n_src:
+        raise ValueError(f"x_src has {x_src.shape[0]} rows, relation expects {csr.n_src}")
+    d = int(x_src.shape[1])
+    out = torch.empty(csr.n_dst, d, dtype=torch.float32, device=dev)
+    _gather(x_src, csr.fwd, None, csr_mean=True, out=out, accumulate=False)
+    return out
+
+
+def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
+    p = grouped.plan
+    dev = out.device
+    slab = None
+    if p.n_heavy:
+        slab = torch.empty(p.n_chunks * out.shape[1], dtype=torch.float32, device=dev)
+    flags = (N.HGNN_MEAN if csr_mean else 0) | (N.HGNN_ACCUMULATE if accumulate else 0)
+    d = int(out.shape[1])
+    weighted = edge_w is not None or col_w is not None
+    name = f"gather_{'fwd' if csr_mean else 'bwd'}_d{d}"
+    with _timed(name, gather_bytes(int(grouped.col.numel()), grouped.n_rows, d, weighted)):
+        N.check(N.lib().hgnn_gather_reduce(
+            N.ptr(x), x.shape[0], d, N.ptr(grouped.rowptr), N.ptr(grouped.col),
+            grouped.n_rows, N.ptr(edge_w), N.ptr(col_w), flags, N.ptr(p.heavy_rows),
+            N.ptr(p.heavy_first), p.n_heavy, p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out),
+            N.stream_ptr(dev)), "hgnn_gather_reduce")
+
+
+def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K2: ``grad_x_src[j] (+)= sum_{(j->i)} grad_aggr[i] / deg_i`` over the CSC."""
+    grad_aggr = _check_f32(grad_aggr, "scatter_mean_bwd")
+    dev = grad_aggr.device
+    d = int(grad_aggr.shape[1])
+    acc = out is not None
+    if out is None:
+        out = torch.empty(csr.n_src, d, dtype=torch.float32, device=dev)
+    _gather(grad_aggr, csr.bwd, csr.inv_deg, csr_mean=False, out=out, accumulate=acc)
+    return out
+
+
+def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.Tensor],
+               relu: bool) -> torch.Tensor:
+    """K3/K4: ``act(sum_s segs[s] @ w[:, seg s]^T + b)``."""
+    n = int(segs[0].shape[0])
+    h = int(w.shape[0])
+    ks = [int(s.shape[1]) for s in segs]
+    if w.shape[1] != sum(ks):
+        raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(ks)}")
+    dev = w.device
+    out = torch.empty(n, h, dtype=torch.float32, device=dev)
+    with _timed(f"linear_fwd_h{h}", 4 * n * (sum(ks) + h)):
+        N.check(N.lib().hgnn_linear_fwd(len(segs), N.ptr_array(segs), N.int_array(ks), n,
+                                        N.ptr(w), h, N.ptr(b), 1 if relu else 0, N.ptr(out),
+                                        N.stream_ptr(dev)), "hgnn_linear_fwd")
+    return out
+
+
+def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], need_w: bool,
+               need_b: bool):
+    n = int(segs[0].shape[0])
+    h = int(w.shape[0])
+    ks = [int(s.shape[1]) for s in segs]
+    dev = w.device
+    dw = torch.empty_like(w) if need_w else None
+    db = torch.empty(h, dtype=torch.float32, device=dev) if need_b else None
+    ws = None
+    if need_w or need_b:
+        ws = N.workspace(N.lib().hgnn_linear_bwd_ws_bytes(n, sum(ks), h), dev)
+    nb = 4 * n * (2 * h + sum(ks) + sum(k for k, dx in zip(ks, dxs) if dx is not None))
+    with _timed(f"linear_bwd_h{h}", nb):
+        N.check(N.lib().hgnn_linear_bwd(
+            len(segs), N.ptr_array(segs), N.int_array(ks), n, N.ptr(w), h, N.ptr(dout),
+            N.ptr(out_act), N.ptr_array(dxs), N.ptr(dw), N.ptr(db), N.ptr(ws),
+            0 if ws is None else ws.numel(), N.stream_ptr(dev)), "hgnn_linear_bwd")
+    return dw, db
+
+
+# ----------------------------------------------------------------------------- layer spec
+@dataclasses.dataclass(frozen=True)
+class DstGroup:
+    dst: str
+    rels: Tuple[Tuple[str, RelationCSR], ...]   # (source type, relation structure)
+    root: bool                                   # x_dst segment present (root_weight)
+    relu: bool
+
+
+@dataclasses.dataclass(frozen=True)
+class LayerSpec:
+    types: Tuple[str, ...]                       # order of node-feature inputs
+    groups: Tuple[DstGroup, ...]
+
+
+class _HeteroLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec: LayerSpec, *flat):
+        nt = len(spec.types)
+        xs = dict(zip(spec.types, flat[:nt]))
+        wb = flat[nt:]
+        outs, aggrs_all = [], []
+        for gi, g in enumerate(spec.groups):
+            w, b = wb[2 * gi], wb[2 * gi + 1]
+            aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
+            segs = aggrs + ([xs[g.dst]] if g.root else [])
+            y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(), g.relu)
+            outs.append(y)
+            aggrs_all.extend(aggrs)
+        ctx.spec = spec
+        ctx.has_b = [b is not None for b in wb[1::2]]
+        ctx.save_for_backward(*flat[:nt], *[t for t in wb if t is not None], *aggrs_all, *outs)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        spec: LayerSpec = ctx.spec
+        nt, ng = len(spec.types), len(spec.groups)
+        saved = list(ctx.saved_tensors)
+        xs = dict(zip(spec.types, saved[:nt]))
+        pos = nt
+        wbs = []
+        for hb in ctx.has_b:
+            w = saved[pos]; pos += 1
+            b = None
+            if hb:
+                b = saved[pos]; pos += 1
+            wbs.append((w, b))
+        aggrs_all = saved[pos:pos + sum(len(g.rels) for g in spec.groups)]
+        pos += len(aggrs_all)
+        outs = saved[pos:pos + ng]
+        need = ctx.needs_input_grad[1:]
+        need_x = dict(zip(spec.types, need[:nt]))
+        gx: Dict[str, Optional[torch.Tensor]] = {t: None for t in spec.types}
+        gwb: List[Optional[torch.Tensor]] = [None] * (2 * ng)
+        pending = []   # (src type, dA, csr) for K2 after every root gradient is written
+        ai = 0
+        for gi, g in enumerate(spec.groups):
+            aggrs = aggrs_all[ai:ai + len(g.rels)]
+            ai += len(g.rels)
+            dout = douts[gi]
+            w, b = wbs[gi]
+            need_w, need_b = need[nt + 2 * gi], (b is not None and need[nt + 2 * gi + 1])
+            if dout is None:
+                continue
+            dout = dout.contiguous()
+            dxs: List[Optional[torch.Tensor]] = []
+            for (src, csr), a in zip(g.rels, aggrs):
+                if need_x[src] and csr.num_edges > 0:
+                    dA = torch.empty_like(a)
+                    dxs.append(dA)
+                    pending.append((src, dA, csr))
+                else:
+                    dxs.append(None)
+            segs = list(aggrs)
+            if g.root:
+                segs.append(xs[g.dst])
+                if need_x[g.dst]:
+                    gx[g.dst] = torch.empty_like(xs[g.dst])
+                    dxs.append(gx[g.dst])
+                else:
+                    dxs.append(None)
+            dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w, need_b)
+            gwb[2 * gi], gwb[2 * gi + 1] = dw, db
+        for src, dA, csr in pending:
+            if gx[src] is None:
+                gx[src] = scatter_mean_bwd(dA, csr)
+            else:
+                scatter_mean_bwd(dA, csr, out=gx[src])
+        return (None, *[gx[t] for t in spec.types], *gwb)
+
+
+def hetero_layer(spec: LayerSpec, x_dict: Dict[str, torch.Tensor],
+                 weights: Sequence[Tuple[torch.Tensor, Optional[torch.Tensor]]]
+                 ) -> Dict[str, torch.Tensor]:
+    flat: List[Optional[torch.Tensor]] = [x_dict[t] for t in spec.types]
+    for w, b in weights:
+        flat.extend([w, b])
+    N.require_device(*[t for t in flat if t is not None])
+    for t in flat[:len(spec.types)]:
+        _check_f32(t, "node features")
+    outs = _HeteroLayer.apply(spec, *flat)
+    return {g.dst: y for g, y in zip(spec.groups, outs)}
+
+
+# ----------------------------------------------------------------------------- link loss
+def link_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
+              neg_p: torch.Tensor, pos_weights: torch.Tensor) -> torch.Tensor:
+    """The reference training loss (train_gnn.py:259-281), on the device with torch ops.
+
+    ``BCEWithLogitsLoss()`` has mean reduction, so ``(pos_weights * pos_loss).mean()`` equals
+    ``mean(pos_weights) * pos_loss`` — reproduced as written."""
+    pos_u, pos_p = pos_edges[0], pos_edges[1]
+    u = user_emb[pos_u]
+    pos_scores = (u * post_emb[pos_p]).sum(dim=1)
+    neg_scores = (u * post_emb[neg_p]).sum(dim=1)
+    crit = torch.nn.functional.binary_cross_entropy_with_logits
+    pos_loss = crit(pos_scores, torch.ones_like(pos_scores))
+    neg_loss = crit(neg_scores, torch.zeros_like(neg_scores))
+    return (pos_weights * pos_loss).mean() + neg_loss
