@@ -134,8 +134,9 @@ def main():
     def step():
         opt.zero_grad(set_to_none=True)
         out = model(g.x_dict, g.edge_index_dict)
-        neg = torch.randint(0, cfg.num_posts, (pos.shape[1],), device=dev, generator=gen)
-        loss = ops.link_loss(out["user"], out["post"], pos, neg, pw)
+        neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
+        loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
+                                 check=False)
         loss.backward()
         if world > 1:
             flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])

@@ -53,6 +53,14 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
                     int64_t n_other, int32_t* rowptr, int32_t* col, int32_t* perm,
                     int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* Stable sort of int32 keys in [0,n_keys) carrying one or two int32 payloads (b may be NULL):
+ * rowptr[n_keys+1] over the sorted keys, payloads in key order.  Out-of-range keys are dropped
+ * and counted in *d_invalid.  Used per step to group the sampled negatives by post. */
+size_t hgnn_sort_pairs_ws_bytes(int64_t E, int64_t n_keys);
+int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b, int64_t E,
+                        int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
+                        int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- degree-skew plan ----------------------------------------------------------------------
  * Rows with more than `chunk` edges are split into ceil(deg/chunk) chunks, each summed by its own
  * wave into a partial slot, then reduced in chunk order (deterministic).  Two phases so the host
@@ -110,6 +118,22 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,
                     hgnn_stream_t stream);
+
+/* ---- edge scoring + weighted BCE (train_gnn.py:259-281), fused with its gradient --------------
+ * Positive edges grouped by user (rowptr_u/col_u = post ids); neg_u_order[k] = the negative post
+ * drawn for position k; to_post_pos[k] = that edge's position in the post-grouped CSR.
+ *   loss = c * mean softplus(-<U[u],P[p]>) + mean softplus(<U[u],P[n]>),  c = *cscale
+ *          (= mean(pos_weights): BCEWithLogitsLoss() reduces to a scalar first)
+ * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics), hpos[post-grouped pos]
+ * (weight of U[u] in dP[p]), and per position (neg_key, neg_user, neg_w) for the negatives' dP;
+ * part needs 2*hgnn_edge_score_parts(n_users) floats; *err counts out-of-range negatives. */
+int64_t hgnn_edge_score_parts(int64_t n_users);
+int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
+                        int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                        const int64_t* neg_u_order, const int32_t* to_post_pos, int64_t n_edges,
+                        const float* cscale, float* dU, float* hpos, int32_t* neg_key,
+                        int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
+                        hgnn_stream_t stream);
 
 #ifdef __cplusplus
 }

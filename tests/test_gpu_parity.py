@@ -239,3 +239,76 @@ def test_cfg2_full_size_linearity_checksum():
     rhs = (g.x_dict["user"].double() * outdeg[:, None]).sum(0)
     torch.testing.assert_close(lhs, rhs, rtol=1e-6, atol=1e-3)
     assert csr.fwd.plan.n_heavy > 0   # the Zipf head really exercised the chunked path
+
+
+# ----------------------------------------------------------------------------- fused link loss
+@pytest.mark.parametrize("d", [64, 128, 5, 200, 16])
+def test_edge_bce_loss_matches_oracle(d):
+    rng = np.random.default_rng(100 + d)
+    nu, npost, E = 300, 120, 5000
+    pos = torch.from_numpy(np.stack([rng.integers(0, nu, E),
+                                     synth._zipf_sample_np(rng, npost, E, 0.9)]).astype(np.int64))
+    neg = torch.from_numpy(rng.integers(0, npost, E).astype(np.int64))
+    pw = torch.from_numpy(np.where(rng.random(E) < 0.3, 3.0, 1.0).astype(np.float32))
+    U = torch.from_numpy(rng.standard_normal((nu, d)).astype(np.float32) * 0.3)
+    P = torch.from_numpy(rng.standard_normal((npost, d)).astype(np.float32) * 0.3)
+    Ur, Pr = U.clone().requires_grad_(), P.clone().requires_grad_()
+    ref = sage_ref.link_loss(Ur, Pr, pos, neg, pw)
+    (ref * 2.5).backward()
+    Ud, Pd = U.to(DEV).requires_grad_(), P.to(DEV).requires_grad_()
+    pos_d = pos.to(DEV)
+    got = ops.edge_bce_loss(Ud, Pd, pos_d, neg.to(DEV), pw.to(DEV))
+    (got * 2.5).backward()
+    close(got, ref)
+    close(Ud.grad, Ur.grad)
+    close(Pd.grad, Pr.grad)
+    # same draws presented in the user-grouped order give the same loss
+    csr = graph.relation_csr(pos_d, nu, npost)
+    neg_u = ops.negatives_in_user_order(csr, neg.to(DEV))
+    got2 = ops.edge_bce_loss(Ud.detach(), Pd.detach(), pos_d, neg_u, pw.to(DEV), neg_order="user")
+    assert torch.equal(got2, got.detach())
+
+
+def test_edge_bce_loss_rejects_bad_negatives():
+    pos = torch.tensor([[0, 1], [0, 1]], device=DEV)
+    U, P = torch.randn(2, 8, device=DEV), torch.randn(2, 8, device=DEV)
+    with pytest.raises(ValueError, match="out of range"):
+        ops.edge_bce_loss(U, P, pos, torch.tensor([0, 7], device=DEV), torch.ones(2, device=DEV))
+
+
+def test_weighted_rgcn_fused_loss_step_matches_golden():
+    z, x, e, params = _fixture_cfg1()
+    model = WeightedRGCN(hidden_dim=64).to(DEV)
+    model.load_state_dict(params)
+    out = model(x, e)
+    loss = ops.edge_bce_loss(out["user"], out["post"], e[synth.ENGAGES],
+                             torch.from_numpy(z["neg_p"]).to(DEV),
+                             torch.from_numpy(z["pos_weights"]).to(DEV))
+    assert abs(float(loss) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_sort_pairs_matches_numpy():
+    rng = np.random.default_rng(9)
+    E, nk = 100000, 70000
+    keys = torch.from_numpy(rng.integers(0, nk, E).astype(np.int32))
+    a = torch.arange(E, dtype=torch.int32)
+    b = torch.from_numpy(rng.integers(-5, 5, E).astype(np.int32))
+    from truth_recommendation_gnn_amd import _native as Nn
+    dev = torch.device(DEV)
+    rowptr = torch.empty(nk + 1, dtype=torch.int32, device=dev)
+    ao = torch.empty(E, dtype=torch.int32, device=dev)
+    bo = torch.empty(E, dtype=torch.int32, device=dev)
+    inv = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = Nn.workspace(Nn.lib().hgnn_sort_pairs_ws_bytes(E, nk), dev)
+    kd, ad, bd = keys.to(dev), a.to(dev), b.to(dev)
+    Nn.check(Nn.lib().hgnn_sort_pairs_i32(Nn.ptr(kd), Nn.ptr(ad), Nn.ptr(bd), E, nk, Nn.ptr(rowptr),
+                                          Nn.ptr(ao), Nn.ptr(bo), Nn.ptr(inv), Nn.ptr(ws), ws.numel(),
+                                          Nn.stream_ptr(dev)), "sort")
+    order = np.argsort(keys.numpy(), kind="stable")
+    assert np.array_equal(ao.cpu().numpy(), order)
+    assert np.array_equal(bo.cpu().numpy(), b.numpy()[order])
+    rp, _, _ = csr_ref.coo_to_csr(keys.numpy(), keys.numpy(), nk)
+    assert np.array_equal(rowptr.cpu().numpy(), rp)

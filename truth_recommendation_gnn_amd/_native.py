@@ -40,7 +40,11 @@ _SIGS = {
     "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
                                  _c_sz, _p]),
-    "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _p, _p, _p, _c_i64, _p, _p, _p, _p]),
+    "hgnn_sort_pairs_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_sort_pairs_i32": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_edge_score_parts": (_c_i64, [_c_i64]),
+    "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _p, _c_i64, _p,
+                                     _p, _p, _p, _p, _p, _p, _p, _p, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -183,10 +183,11 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
 }
 
 // Stable scatter: rounds in order; within a round, items in thread order.  Per wave the match
-// set of a digit comes from 8 ballots; per-wave digit counts go through LDS.
+// set of a digit comes from 8 ballots; per-wave digit counts go through LDS.  Carries up to two
+// 32-bit payloads (a: identity when a_in is null and identity_a is set; b optional).
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
-    const int32_t* keys_in, const int32_t* vals_in, int64_t E, int shift, const int32_t* offs,
-    int32_t* keys_out, int32_t* vals_out, int identity_vals) {
+    const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
+    const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
   __shared__ int base_off[kRadix];                 // global offset + running count per digit
   __shared__ int wcount[kSortThreads / 64][kRadix];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -199,13 +200,14 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
     const bool valid = i < E;
     int key = valid ? keys_in[i] : 0;
-    int val = valid ? (identity_vals ? (int)i : vals_in[i]) : 0;
+    int va = valid ? (identity_a ? (int)i : a_in[i]) : 0;
+    int vb = (valid && b_in) ? b_in[i] : 0;
     int digit = (key >> shift) & (kRadix - 1);
     unsigned long long match = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      unsigned long long m = __ballot((digit >> b) & 1);
-      match &= ((digit >> b) & 1) ? m : ~m;
+    for (int bit = 0; bit < 8; ++bit) {
+      unsigned long long m = __ballot((digit >> bit) & 1);
+      match &= ((digit >> bit) & 1) ? m : ~m;
     }
     int rank = __popcll(match & lt_mask);
     if (valid && rank == 0) wcount[wid][digit] = __popcll(match);
@@ -214,7 +216,8 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
       int pos = base_off[digit] + rank;
       for (int w = 0; w < wid; ++w) pos += wcount[w][digit];
       keys_out[pos] = key;
-      vals_out[pos] = val;
+      a_out[pos] = va;
+      if (b_out) b_out[pos] = vb;
     }
     __syncthreads();
     {  // advance running offsets, clear the per-wave counts (one digit per thread)
@@ -229,22 +232,40 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   }
 }
 
-// rowptr[r] = #sorted keys < r for r in [0, n_keys]; col = other[perm].
-__global__ void __launch_bounds__(256) k_finish_csr(const int32_t* skey, const int32_t* sidx,
-                                                    const int64_t* other, int64_t E,
-                                                    int64_t n_keys, int32_t* rowptr,
-                                                    int32_t* col, int32_t* perm) {
+// rowptr[r] = #sorted keys < r for r in [0, n_keys] (keys == n_keys are dropped sentinels).
+__global__ void __launch_bounds__(256) k_rowptr_from_sorted(const int32_t* skey, int64_t E,
+                                                            int64_t n_keys, int32_t* rowptr) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E) return;
   int32_t k = skey[i];
-  int32_t e = sidx[i];
-  perm[i] = e;
-  col[i] = k < n_keys ? (int32_t)other[e] : 0;
   int64_t prev = i > 0 ? skey[i - 1] : -1;
   int64_t hi = k < n_keys ? k : n_keys;
   for (int64_t r = prev + 1; r <= hi; ++r) rowptr[r] = (int32_t)i;
   if (i == E - 1)
     for (int64_t r = (int64_t)k + 1; r <= n_keys; ++r) rowptr[r] = (int32_t)E;
+}
+
+__global__ void __launch_bounds__(256) k_gather_other(const int32_t* perm, const int32_t* skey,
+                                                      const int64_t* other, int64_t E,
+                                                      int64_t n_keys, int32_t* col) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < E) col[i] = skey[i] < n_keys ? (int32_t)other[perm[i]] : 0;
+}
+
+// key32 = key if in [0, n_keys) else n_keys (sentinel); counts invalid keys.
+__global__ void __launch_bounds__(256) k_prepare_keys32(const int32_t* key, int64_t E,
+                                                        int64_t n_keys, int32_t* key32,
+                                                        int32_t* invalid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int bad = 0;
+  if (i < E) {
+    int32_t k = key[i];
+    bool ok = k >= 0 && k < n_keys;
+    key32[i] = ok ? k : (int32_t)n_keys;
+    bad = ok ? 0 : 1;
+  }
+  unsigned long long m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
 }
 
 __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
@@ -262,8 +283,50 @@ static size_t sort_ws_bytes(int64_t E) {
   int64_t nb = cdiv(E, kSortTile);
   size_t scan_b = 0;
   exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, 0);
-  return 4 * align_up((size_t)E * 4, 256) + 2 * align_up((size_t)(nb * kRadix + 1) * 4, 256) +
-         scan_b + 1024;
+  return 5 * align_up((size_t)E * 4, 256) + 2 * align_up((size_t)(nb * kRadix + 1) * 4, 256) +
+         scan_b + 2048;
+}
+
+// LSD sort of prepared keys (ka, values in [0, n_keys]) with payload a (identity if a_in null)
+// and optional b.  The last pass lands the payloads in a_out / b_out; the sorted keys end in
+// *k_sorted (a workspace buffer).
+static int radix_sort_pairs(int32_t* ka, int64_t E, int64_t n_keys, const int32_t* a_in,
+                            const int32_t* b_in, int32_t* a_out, int32_t* b_out, Workspace& w,
+                            hipStream_t stream, const int32_t** k_sorted) {
+  int32_t* kb = w.take<int32_t>(E);
+  int32_t* ta = w.take<int32_t>(E);
+  int32_t* tb = b_in ? w.take<int32_t>(E) : nullptr;
+  const int64_t nb = cdiv(E, kSortTile);
+  int32_t* counts = w.take<int32_t>(nb * kRadix + 1);
+  int32_t* offs = w.take<int32_t>(nb * kRadix + 1);
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, stream);
+  void* scan_ws = w.take<char>(scan_b);
+  if (!scan_ws) return fail(HGNN_E_WS, "radix sort: workspace too small");
+  const int passes = radix_passes(n_keys);
+  const int32_t* kin = ka;
+  const int32_t* ain = a_in;
+  const int32_t* bin = b_in;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    const bool to_out = ((passes - 1 - p) % 2) == 0;
+    int32_t* kout = (kin == ka) ? kb : ka;
+    int32_t* aout = to_out ? a_out : ta;
+    int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
+    hipLaunchKernelGGL(k_digit_counts, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift,
+                       counts);
+    if (int rc = check_launch("k_digit_counts")) return rc;
+    if (int rc = exclusive_scan_i32(counts, offs, nb * kRadix, scan_ws, &scan_b, stream))
+      return rc;
+    hipLaunchKernelGGL(k_digit_scatter, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, bin,
+                       E, shift, offs, kout, aout, bout, (p == 0 && a_in == nullptr) ? 1 : 0);
+    if (int rc = check_launch("k_digit_scatter")) return rc;
+    kin = kout;
+    ain = aout;
+    bin = bout;
+  }
+  *k_sorted = kin;
+  return HGNN_OK;
 }
 
 }  // namespace hgnn
@@ -272,7 +335,7 @@ using namespace hgnn;
 
 extern "C" {
 
-int hgnn_version(void) { return 100; }
+int hgnn_version(void) { return 101; }
 
 const char* hgnn_last_error_string(void) { return g_err; }
 
@@ -291,50 +354,63 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
   if (!rowptr || !d_invalid || (E > 0 && (!key || !other || !col || !perm)))
     return fail(HGNN_E_ARG, "coo_to_csr: null pointer");
   (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
-  if (E == 0) {
+  if (E == 0 || n_keys == 0) {
     hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
                        n_keys + 1, 0);
-    return check_launch("coo_to_csr(E=0)");
+    if (E > 0)  // every edge is out of range
+      hipLaunchKernelGGL(k_prepare_keys, dim3(cdiv(E, 256)), dim3(256), 0, stream, key, other,
+                         E, n_keys, n_other, col, d_invalid);
+    return check_launch("coo_to_csr(empty)");
   }
   if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "coo_to_csr: workspace too small");
   Workspace w(ws, ws_bytes);
   int32_t* ka = w.take<int32_t>(E);
-  int32_t* kb = w.take<int32_t>(E);
-  int32_t* va = w.take<int32_t>(E);
-  int32_t* vb = w.take<int32_t>(E);
-  const int64_t nb = cdiv(E, kSortTile);
-  int32_t* counts = w.take<int32_t>(nb * kRadix + 1);
-  int32_t* offs = w.take<int32_t>(nb * kRadix + 1);
-  size_t scan_b = 0;
-  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, stream);
-  void* scan_ws = w.take<char>(scan_b);
-  if (!scan_ws) return fail(HGNN_E_WS, "coo_to_csr: workspace too small");
-
   hipLaunchKernelGGL(k_prepare_keys, dim3(cdiv(E, 256)), dim3(256), 0, stream, key, other, E,
                      n_keys, n_other, ka, d_invalid);
   if (int rc = check_launch("k_prepare_keys")) return rc;
-  const int passes = radix_passes(n_keys);
-  int32_t *kin = ka, *kout = kb, *vin = va, *vout = vb;
-  for (int p = 0; p < passes; ++p) {
-    const int shift = 8 * p;
-    hipLaunchKernelGGL(k_digit_counts, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift,
-                       counts);
-    if (int rc = check_launch("k_digit_counts")) return rc;
-    if (int rc = exclusive_scan_i32(counts, offs, nb * kRadix, scan_ws, &scan_b, stream))
-      return rc;
-    hipLaunchKernelGGL(k_digit_scatter, dim3(nb), dim3(kSortThreads), 0, stream, kin, vin, E,
-                       shift, offs, kout, vout, p == 0 ? 1 : 0);
-    if (int rc = check_launch("k_digit_scatter")) return rc;
-    int32_t* t = kin; kin = kout; kout = t;
-    t = vin; vin = vout; vout = t;
+  const int32_t* sk = nullptr;
+  if (int rc = radix_sort_pairs(ka, E, n_keys, nullptr, nullptr, perm, nullptr, w, stream, &sk))
+    return rc;
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+                     n_keys, rowptr);
+  if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
+  hipLaunchKernelGGL(k_gather_other, dim3(cdiv(E, 256)), dim3(256), 0, stream, perm, sk, other,
+                     E, n_keys, col);
+  return check_launch("k_gather_other");
+}
+
+size_t hgnn_sort_pairs_ws_bytes(int64_t E, int64_t n_keys) {
+  (void)n_keys;
+  return sort_ws_bytes(E < 1 ? 1 : E);
+}
+
+int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b, int64_t E,
+                        int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
+                        int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_keys < 0 || n_keys >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "sort_pairs: E=%lld n_keys=%lld out of range", (long long)E,
+                (long long)n_keys);
+  if (!rowptr || !d_invalid || (E > 0 && (!keys || !a || !a_sorted || (b && !b_sorted))))
+    return fail(HGNN_E_ARG, "sort_pairs: null pointer");
+  (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
+  if (E == 0 || n_keys == 0) {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
+                       n_keys + 1, 0);
+    return check_launch("sort_pairs(empty)");
   }
-  if (passes == 0) {  // n_keys == 0: every edge is invalid; identity order
-    hipLaunchKernelGGL(k_fill_i32, dim3(1), dim3(1), 0, stream, rowptr, 1, 0);
-    return check_launch("coo_to_csr(n_keys=0)");
-  }
-  hipLaunchKernelGGL(k_finish_csr, dim3(cdiv(E, 256)), dim3(256), 0, stream, kin, vin, other, E,
-                     n_keys, rowptr, col, perm);
-  return check_launch("k_finish_csr");
+  if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "sort_pairs: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* ka = w.take<int32_t>(E);
+  hipLaunchKernelGGL(k_prepare_keys32, dim3(cdiv(E, 256)), dim3(256), 0, stream, keys, E, n_keys,
+                     ka, d_invalid);
+  if (int rc = check_launch("k_prepare_keys32")) return rc;
+  const int32_t* sk = nullptr;
+  if (int rc = radix_sort_pairs(ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
+    return rc;
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+                     n_keys, rowptr);
+  return check_launch("k_rowptr_from_sorted");
 }
 
 }  // extern "C"

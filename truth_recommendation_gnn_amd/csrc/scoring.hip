@@ -1,0 +1,243 @@
+// Edge scoring + weighted BCE of the reference training step (train_gnn.py:259-281), fused.
+//
+//   s_pos[e] = <U[u_e], P[p_e]>,  s_neg[e] = <U[u_e], P[n_e]>
+//   loss = mean(pos_weights) * mean_e softplus(-s_pos) + mean_e softplus(s_neg)
+//
+// (BCEWithLogitsLoss() reduces to a scalar, so the per-edge interaction weights collapse to their
+// mean — the reference's own arithmetic, reproduced.)
+//
+// Pass A (this file) walks the positive edges grouped by user (the CSC of the engages relation):
+// one wave per user keeps U[u] in registers, gathers P[p_e] and P[n_e] per edge, and in the same
+// pass produces the loss partials AND dL/dU for a unit upstream gradient
+//   dU[u] = sum_e  c/E (sigma(s_pos)-1) P[p_e] + 1/E sigma(s_neg) P[n_e]
+// with no atomics (the wave owns the row).  It also emits each edge's weights for dP:
+//   hpos (written at the edge's post-grouped position) and (n_e, u_e, hneg) for the negatives.
+// dP is then two K1-style weighted gathers of U rows (gather.hip): positives over the post-
+// grouped CSR, negatives over the (n_e)-sorted list (hgnn_sort_pairs_i32).  Deterministic.
+#include "hgnn_common.h"
+
+namespace hgnn {
+
+struct ScoreArgs {
+  const float* U;
+  const float* P;
+  const int32_t* rowptr;       // user-grouped CSR of the positive edges
+  const int32_t* col;          // post id per position
+  const int64_t* neg;          // negative post id per position (user-grouped order)
+  const int32_t* to_post_pos;  // position -> post-grouped position (for hpos)
+  const float* cscale;         // device scalar mean(pos_weights)
+  float* dU;
+  float* hpos;
+  int32_t* neg_key;
+  int32_t* neg_u;
+  float* neg_w;
+  float* part;                 // [gridDim.x][2]
+  int32_t* err;
+  int64_t n_users;
+  int64_t n_posts;
+  float inv_e;
+  int32_t d;
+};
+
+__device__ __forceinline__ float softplus(float x) {
+  return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int LPR, int VPL, int W>
+__device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
+                                          const typename Vec<W>::T (&b)[VPL]) {
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) {
+    if constexpr (W == 4) {
+      s = fmaf(a[q].x, b[q].x, s); s = fmaf(a[q].y, b[q].y, s);
+      s = fmaf(a[q].z, b[q].z, s); s = fmaf(a[q].w, b[q].w, s);
+    } else {
+      s = fmaf(a[q], b[q], s);
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) s += __shfl_xor(s, m, 64);
+  return s;
+}
+
+template <int LPR, int VPL, int W, int UNROLL>
+__global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
+  using V = Vec<W>;
+  constexpr int NS = 64 / LPR;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane / LPR, sl = lane % LPR;
+  const int64_t u = (int64_t)blockIdx.x * 4 + wave;
+  const float c = *a.cscale;
+  const int d = a.d;
+  float lpos = 0.f, lneg = 0.f;   // per-lane loss sums (edge = lane)
+  if (u < a.n_users) {
+    const int64_t beg = a.rowptr[u], end = a.rowptr[u + 1];
+    typename V::T uv[VPL], acc[VPL];
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) {
+      const int cc = (q * LPR + sl) * W;
+      uv[q] = cc < d ? V::load(a.U + u * d + cc) : V::zero();
+      acc[q] = V::zero();
+    }
+    for (int64_t base = beg; base < end; base += 64) {
+      const int n = (int)min<int64_t>(64, end - base);
+      int pid = 0, nid = 0;
+      if (lane < n) {
+        pid = a.col[base + lane];
+        const int64_t nn = a.neg[base + lane];
+        if (nn < 0 || nn >= a.n_posts) atomicAdd(a.err, 1);
+        else nid = (int)nn;
+      }
+      float my_hp = 0.f, my_hn = 0.f, my_sp = 0.f, my_sn = 0.f;
+      for (int j = 0; j < n; j += NS * UNROLL) {
+        typename V::T vp[UNROLL][VPL], vn[UNROLL][VPL];
+#pragma unroll
+        for (int uu = 0; uu < UNROLL; ++uu) {
+          const int e = j + uu * NS + slot;
+          const int pp = __shfl(pid, e & 63, 64), qq = __shfl(nid, e & 63, 64);
+#pragma unroll
+          for (int q = 0; q < VPL; ++q) {
+            const int cc = (q * LPR + sl) * W;
+            const bool ok = e < n && cc < d;
+            vp[uu][q] = ok ? V::load(a.P + (int64_t)pp * d + cc) : V::zero();
+            vn[uu][q] = ok ? V::load(a.P + (int64_t)qq * d + cc) : V::zero();
+          }
+        }
+#pragma unroll
+        for (int uu = 0; uu < UNROLL; ++uu) {
+          const int e0 = j + uu * NS;
+          const int e = e0 + slot;
+          const float sp = slot_dot<LPR, VPL, W>(uv, vp[uu]);
+          const float sn = slot_dot<LPR, VPL, W>(uv, vn[uu]);
+          float hp = c * a.inv_e * (sigmoid(sp) - 1.f);
+          float hn = a.inv_e * sigmoid(sn);
+          if (e >= n) hp = hn = 0.f;
+#pragma unroll
+          for (int q = 0; q < VPL; ++q) {
+            V::fma(acc[q], hp, vp[uu][q]);
+            V::fma(acc[q], hn, vn[uu][q]);
+          }
+          // hand edge e's values to lane e (lanes e0 .. e0+NS-1 read from slot lane*LPR)
+          const int src = ((lane - e0) & (NS - 1)) * LPR;
+          const float thp = __shfl(hp, src, 64), thn = __shfl(hn, src, 64);
+          const float tsp = __shfl(softplus(-sp), src, 64), tsn = __shfl(softplus(sn), src, 64);
+          if (lane >= e0 && lane < e0 + NS) {
+            my_hp = thp; my_hn = thn; my_sp = tsp; my_sn = tsn;
+          }
+        }
+      }
+      if (lane < n) {
+        const int64_t k = base + lane;
+        lpos += my_sp;
+        lneg += my_sn;
+        a.hpos[a.to_post_pos[k]] = my_hp;
+        a.neg_key[k] = nid;
+        a.neg_u[k] = (int32_t)u;
+        a.neg_w[k] = my_hn;
+      }
+    }
+#pragma unroll
+    for (int m = LPR; m < 64; m <<= 1)
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) V::add(acc[q], V::shfl_xor(acc[q], m));
+    if (lane < LPR) {
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) {
+        const int cc = (q * LPR + sl) * W;
+        if (cc < d) V::store(a.dU + u * d + cc, acc[q]);
+      }
+    }
+  }
+  // deterministic block partials: wave tree, then waves in order
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    lpos += __shfl_xor(lpos, m, 64);
+    lneg += __shfl_xor(lneg, m, 64);
+  }
+  if (lane == 0) {
+    red[0][wave] = lpos;
+    red[1][wave] = lneg;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.part[2 * blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+    a.part[2 * blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+  }
+}
+
+// loss = c * inv_e * sum(part[:,0]) + inv_e * sum(part[:,1]); one block, fixed order, double.
+__global__ void __launch_bounds__(256) k_loss_reduce(const float* part, int64_t n_part,
+                                                     const float* cscale, float inv_e,
+                                                     float* loss) {
+  __shared__ double sp[256], sn[256];
+  double p = 0.0, q = 0.0;
+  for (int64_t i = threadIdx.x; i < n_part; i += 256) {
+    p += part[2 * i];
+    q += part[2 * i + 1];
+  }
+  sp[threadIdx.x] = p;
+  sn[threadIdx.x] = q;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sp[threadIdx.x] += sp[threadIdx.x + s];
+      sn[threadIdx.x] += sn[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    *loss = (float)((double)*cscale * (double)inv_e * sp[0] + (double)inv_e * sn[0]);
+}
+
+template <int LPR, int VPL, int W, int UNROLL>
+static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream) {
+  hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), dim3((unsigned)nblocks), dim3(256), 0,
+                     stream, a);
+  return check_launch("k_edge_score");
+}
+
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int64_t hgnn_edge_score_parts(int64_t n_users) { return cdiv(n_users, 4); }
+
+int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
+                        int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                        const int64_t* neg_u_order, const int32_t* to_post_pos, int64_t n_edges,
+                        const float* cscale, float* dU, float* hpos, int32_t* neg_key,
+                        int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
+                        hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (d < 1 || n_users < 0 || n_posts < 0 || n_edges < 0)
+    return fail(HGNN_E_ARG, "edge_score: bad sizes");
+  if (!cscale || !loss || !err || (n_users > 0 && (!U || !rowptr_u || !dU || !part)))
+    return fail(HGNN_E_ARG, "edge_score: null pointer");
+  (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);
+  ScoreArgs a{};
+  a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order;
+  a.to_post_pos = to_post_pos; a.cscale = cscale; a.dU = dU; a.hpos = hpos; a.neg_key = neg_key;
+  a.neg_u = neg_user; a.neg_w = neg_w; a.part = part; a.err = err; a.n_users = n_users;
+  a.n_posts = n_posts; a.inv_e = n_edges > 0 ? 1.f / (float)n_edges : 0.f; a.d = d;
+  const int64_t nb = hgnn_edge_score_parts(n_users);
+  int rc = HGNN_OK;
+  if (nb > 0) {
+    if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4, 2>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 128) rc = launch_score<32, 1, 4, 2>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 256) rc = launch_score<64, 1, 4, 2>(a, nb, stream);
+    else if (d <= 64) rc = launch_score<64, 1, 1, 1>(a, nb, stream);
+    else if (d <= 512) rc = launch_score<64, 8, 1, 1>(a, nb, stream);
+    else return fail(HGNN_E_UNSUPPORTED, "edge_score: d=%d", d);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(256), 0, stream, part, nb, cscale, a.inv_e,
+                     loss);
+  return check_launch("k_loss_reduce");
+}
+
+}  // extern "C"

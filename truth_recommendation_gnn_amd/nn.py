@@ -39,6 +39,8 @@ def _materialize(lin: torch.nn.Module, in_features: int) -> None:
         dev = lin.weight.device
         lin.initialize_parameters(torch.empty(0, in_features, device=dev))
     if isinstance(lin, torch.nn.LazyLinear) and not lin.has_uninitialized_params():
+        # materialised by load_state_dict (its load hook does not set in_features)
+        lin.in_features = int(lin.weight.shape[1])
         # what LazyModuleMixin._infer_parameters does after the first call
         lin._initialize_hook.remove()
         lin._load_hook.remove()

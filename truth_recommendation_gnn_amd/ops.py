@@ -282,3 +282,106 @@ def link_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.T
     pos_loss = crit(pos_scores, torch.ones_like(pos_scores))
     neg_loss = crit(neg_scores, torch.zeros_like(neg_scores))
     return (pos_weights * pos_loss).mean() + neg_loss
+
+
+# ----------------------------------------------------------------------------- fused link loss
+def _user_to_post_pos(csr: RelationCSR) -> torch.Tensor:
+    """Static per graph: user-grouped position k -> the same edge's post-grouped position."""
+    m = getattr(csr, "_u2p", None)
+    if m is None:
+        E = csr.num_edges
+        dev = csr.fwd.rowptr.device
+        inv = torch.empty(E, dtype=torch.int32, device=dev)
+        inv[csr.fwd.perm.long()] = torch.arange(E, dtype=torch.int32, device=dev)
+        m = inv[csr.bwd.perm.long()].contiguous()
+        csr._u2p = m
+    return m
+
+
+def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tensor:
+    """Re-order negatives drawn per COO edge (train_gnn.py:272) to the user-grouped order the
+    fused kernel walks."""
+    return neg_p.to(torch.int64)[csr.bwd.perm.long()].contiguous()
+
+
+class _EdgeBCELoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool):
+        U = _check_f32(U, "edge_bce_loss user_emb")
+        P = _check_f32(P, "edge_bce_loss post_emb")
+        dev = N.require_device(U, P, neg_u_order)
+        lib, s = N.lib(), N.stream_ptr(dev)
+        nu, np_, d, E = U.shape[0], P.shape[0], int(U.shape[1]), csr.num_edges
+        if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
+            raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
+        ub, pf = csr.bwd, csr.fwd
+        to_post = _user_to_post_pos(csr)
+        dU = torch.empty_like(U)
+        hpos = torch.empty(E, dtype=torch.float32, device=dev)
+        neg_key = torch.empty(E, dtype=torch.int32, device=dev)
+        neg_user = torch.empty(E, dtype=torch.int32, device=dev)
+        neg_w = torch.empty(E, dtype=torch.float32, device=dev)
+        part = torch.empty(2 * max(int(lib.hgnn_edge_score_parts(nu)), 1), dtype=torch.float32,
+                           device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        err = torch.zeros(2, dtype=torch.int32, device=dev)
+        c = cscale.to(torch.float32).reshape(()).contiguous()
+        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 2 + 2 + 4) + 8 * nu * d):
+            N.check(lib.hgnn_edge_score_fwd(
+                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                N.ptr(neg_u_order), N.ptr(to_post), E, N.ptr(c), N.ptr(dU), N.ptr(hpos),
+                N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), N.ptr(part), N.ptr(loss),
+                N.ptr(err), s), "hgnn_edge_score_fwd")
+        # negatives grouped by post (a fresh draw every step) -> weighted gather of U rows
+        rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
+        nu_s = torch.empty(E, dtype=torch.int32, device=dev)
+        nw_s = torch.empty(E, dtype=torch.float32, device=dev)
+        ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
+        with _timed("sort_negatives", 4 * E * 6 * 2):
+            N.check(lib.hgnn_sort_pairs_i32(
+                N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), E, np_, N.ptr(rowptr_n),
+                N.ptr(nu_s), N.ptr(nw_s), N.ptr(err[1:]), N.ptr(ws), ws.numel(), s),
+                "hgnn_sort_pairs_i32")
+        dP = torch.empty_like(P)
+        _gather(U, pf, None, csr_mean=False, out=dP, accumulate=False, edge_w=hpos)
+        from .graph import GroupedEdges, Plan
+        negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
+        _gather(U, negs, None, csr_mean=False, out=dP, accumulate=True, edge_w=nw_s)
+        if check and int(err[0]):
+            raise ValueError("edge_bce_loss: negative post id out of range")
+        ctx.save_for_backward(dU, dP)
+        return loss
+
+    @staticmethod
+    def backward(ctx, go):
+        dU, dP = ctx.saved_tensors
+        return dU.mul_(go), dP.mul_(go), None, None, None, None
+
+
+def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
+                  neg_p: torch.Tensor, pos_weights: torch.Tensor, neg_order: str = "edge",
+                  check: bool = True) -> torch.Tensor:
+    """Fused HIP version of :func:`link_loss` (same value, same gradients).
+
+    ``neg_order='edge'``: ``neg_p[e]`` is the negative of COO edge e (the reference's layout);
+    ``'user'``: already in the user-grouped order (what :func:`sample_negatives` draws).
+    ``check`` costs one host sync (the reference syncs every step with ``loss.item()``)."""
+    csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
+    if neg_p.shape[0] != csr.num_edges:
+        raise ValueError("one negative per positive edge is required (train_gnn.py:272)")
+    neg_u = negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
+    cscale = pos_weights.to(torch.float32).mean()
+    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check)
+
+
+def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:
+    from .graph import relation_csr
+    return relation_csr(pos_edges, n_users, n_posts)
+
+
+def sample_negatives(pos_edges: torch.Tensor, num_posts: int,
+                     generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """One uniform negative post per positive edge (train_gnn.py:272's ``torch.randint``), drawn
+    directly in the user-grouped order: the draws are iid, so only their labels move."""
+    return torch.randint(0, num_posts, (pos_edges.shape[1],), device=pos_edges.device,
+                         generator=generator)
