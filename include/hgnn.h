@@ -126,7 +126,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
  *          (= mean(pos_weights): BCEWithLogitsLoss() reduces to a scalar first)
  * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics), hpos[post-grouped pos]
  * (weight of U[u] in dP[p]), and per position (neg_key, neg_user, neg_w) for the negatives' dP;
- * part needs 2*hgnn_edge_score_parts(n_users) floats; *err counts out-of-range negatives. */
+ * part needs hgnn_edge_score_parts(n_users) floats (16-B aligned); *err counts out-of-range negatives. */
 int64_t hgnn_edge_score_parts(int64_t n_users);
 int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
                         int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,

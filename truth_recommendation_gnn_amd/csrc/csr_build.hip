@@ -148,7 +148,7 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, siz
 constexpr int kSortThreads = 256;
 constexpr int kSortRounds = 16;                           // one item per thread per round
 constexpr int kSortTile = kSortThreads * kSortRounds;     // 4096 items per block
-constexpr int kRadix = 256;
+constexpr int kMaxRadix = 512;
 
 // key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
 __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
@@ -166,33 +166,40 @@ __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const 
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
 }
 
-// counts[digit * nblocks + block] for this block's tile.
+// counts[digit * nblocks + block] for this block's tile (RADIX = 1 << BITS digits).
+template <int BITS>
 __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
                                                                int shift, int32_t* counts) {
-  __shared__ int hist[kRadix];
-  hist[threadIdx.x] = 0;
+  constexpr int R = 1 << BITS;
+  __shared__ int hist[R];
+  for (int dd = threadIdx.x; dd < R; dd += kSortThreads) hist[dd] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
 #pragma unroll 4
   for (int r = 0; r < kSortRounds; ++r) {
     int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
-    if (i < E) atomicAdd(&hist[(keys[i] >> shift) & (kRadix - 1)], 1);
+    if (i < E) atomicAdd(&hist[(keys[i] >> shift) & (R - 1)], 1);
   }
   __syncthreads();
-  counts[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = hist[threadIdx.x];
+  for (int dd = threadIdx.x; dd < R; dd += kSortThreads)
+    counts[(int64_t)dd * gridDim.x + blockIdx.x] = hist[dd];
 }
 
 // Stable scatter: rounds in order; within a round, items in thread order.  Per wave the match
-// set of a digit comes from 8 ballots; per-wave digit counts go through LDS.  Carries up to two
-// 32-bit payloads (a: identity when a_in is null and identity_a is set; b optional).
+// set of a digit comes from BITS ballots; per-wave digit counts go through LDS.  Carries up to
+// two 32-bit payloads (a: identity when identity_a is set; b optional).
+template <int BITS>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
     const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
-  __shared__ int base_off[kRadix];                 // global offset + running count per digit
-  __shared__ int wcount[kSortThreads / 64][kRadix];
+  constexpr int R = 1 << BITS;
+  __shared__ int base_off[R];                 // global offset + running count per digit
+  __shared__ int wcount[kSortThreads / 64][R];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  base_off[threadIdx.x] = offs[(int64_t)threadIdx.x * gridDim.x + blockIdx.x];
-  for (int w = 0; w < kSortThreads / 64; ++w) wcount[w][threadIdx.x] = 0;
+  for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
+    base_off[dd] = offs[(int64_t)dd * gridDim.x + blockIdx.x];
+    for (int w = 0; w < kSortThreads / 64; ++w) wcount[w][dd] = 0;
+  }
   __syncthreads();
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t base = (int64_t)blockIdx.x * kSortTile;
@@ -202,10 +209,10 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     int key = valid ? keys_in[i] : 0;
     int va = valid ? (identity_a ? (int)i : a_in[i]) : 0;
     int vb = (valid && b_in) ? b_in[i] : 0;
-    int digit = (key >> shift) & (kRadix - 1);
+    int digit = (key >> shift) & (R - 1);
     unsigned long long match = __ballot(valid);
 #pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
+    for (int bit = 0; bit < BITS; ++bit) {
       unsigned long long m = __ballot((digit >> bit) & 1);
       match &= ((digit >> bit) & 1) ? m : ~m;
     }
@@ -220,13 +227,14 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
       if (b_out) b_out[pos] = vb;
     }
     __syncthreads();
-    {  // advance running offsets, clear the per-wave counts (one digit per thread)
-      int d = threadIdx.x, s = 0;
+    // advance running offsets, clear the per-wave counts
+    for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
+      int sum = 0;
       for (int w = 0; w < kSortThreads / 64; ++w) {
-        s += wcount[w][d];
-        wcount[w][d] = 0;
+        sum += wcount[w][dd];
+        wcount[w][dd] = 0;
       }
-      base_off[d] += s;
+      base_off[dd] += sum;
     }
     __syncthreads();
   }
@@ -273,17 +281,20 @@ __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   if (i < n) p[i] = v;
 }
 
-static int radix_passes(int64_t n_keys) {
-  int bits = 0;
-  while ((int64_t(1) << bits) <= n_keys) ++bits;   // keys in [0, n_keys] incl. sentinel
-  return (bits + 7) / 8;
+// Digit width: 9 bits when that saves a pass (17-18-bit keys: 2 passes instead of 3), else 8.
+static void radix_plan(int64_t n_keys, int* passes, int* bits) {
+  int b = 0;
+  while ((int64_t(1) << b) <= n_keys) ++b;   // keys in [0, n_keys] incl. sentinel
+  const int p8 = (b + 7) / 8, p9 = (b + 8) / 9;
+  *bits = p9 < p8 ? 9 : 8;
+  *passes = p9 < p8 ? p9 : p8;
 }
 
 static size_t sort_ws_bytes(int64_t E) {
   int64_t nb = cdiv(E, kSortTile);
   size_t scan_b = 0;
-  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, 0);
-  return 5 * align_up((size_t)E * 4, 256) + 2 * align_up((size_t)(nb * kRadix + 1) * 4, 256) +
+  exclusive_scan_i32(nullptr, nullptr, nb * kMaxRadix, nullptr, &scan_b, 0);
+  return 5 * align_up((size_t)E * 4, 256) + 2 * align_up((size_t)(nb * kMaxRadix + 1) * 4, 256) +
          scan_b + 2048;
 }
 
@@ -297,29 +308,39 @@ static int radix_sort_pairs(int32_t* ka, int64_t E, int64_t n_keys, const int32_
   int32_t* ta = w.take<int32_t>(E);
   int32_t* tb = b_in ? w.take<int32_t>(E) : nullptr;
   const int64_t nb = cdiv(E, kSortTile);
-  int32_t* counts = w.take<int32_t>(nb * kRadix + 1);
-  int32_t* offs = w.take<int32_t>(nb * kRadix + 1);
+  int32_t* counts = w.take<int32_t>(nb * kMaxRadix + 1);
+  int32_t* offs = w.take<int32_t>(nb * kMaxRadix + 1);
+  int passes, bits;
+  radix_plan(n_keys, &passes, &bits);
+  const int64_t ncount = nb * ((int64_t)1 << bits);
   size_t scan_b = 0;
-  exclusive_scan_i32(nullptr, nullptr, nb * kRadix, nullptr, &scan_b, stream);
+  exclusive_scan_i32(nullptr, nullptr, ncount, nullptr, &scan_b, stream);
   void* scan_ws = w.take<char>(scan_b);
   if (!scan_ws) return fail(HGNN_E_WS, "radix sort: workspace too small");
-  const int passes = radix_passes(n_keys);
   const int32_t* kin = ka;
   const int32_t* ain = a_in;
   const int32_t* bin = b_in;
   for (int p = 0; p < passes; ++p) {
-    const int shift = 8 * p;
+    const int shift = bits * p;
     const bool to_out = ((passes - 1 - p) % 2) == 0;
     int32_t* kout = (kin == ka) ? kb : ka;
     int32_t* aout = to_out ? a_out : ta;
     int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
-    hipLaunchKernelGGL(k_digit_counts, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift,
-                       counts);
+    const int ident = (p == 0 && a_in == nullptr) ? 1 : 0;
+    if (bits == 9)
+      hipLaunchKernelGGL(k_digit_counts<9>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E,
+                         shift, counts);
+    else
+      hipLaunchKernelGGL(k_digit_counts<8>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E,
+                         shift, counts);
     if (int rc = check_launch("k_digit_counts")) return rc;
-    if (int rc = exclusive_scan_i32(counts, offs, nb * kRadix, scan_ws, &scan_b, stream))
-      return rc;
-    hipLaunchKernelGGL(k_digit_scatter, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, bin,
-                       E, shift, offs, kout, aout, bout, (p == 0 && a_in == nullptr) ? 1 : 0);
+    if (int rc = exclusive_scan_i32(counts, offs, ncount, scan_ws, &scan_b, stream)) return rc;
+    if (bits == 9)
+      hipLaunchKernelGGL(k_digit_scatter<9>, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain,
+                         bin, E, shift, offs, kout, aout, bout, ident);
+    else
+      hipLaunchKernelGGL(k_digit_scatter<8>, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain,
+                         bin, E, shift, offs, kout, aout, bout, ident);
     if (int rc = check_launch("k_digit_scatter")) return rc;
     kin = kout;
     ain = aout;

@@ -139,24 +139,54 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
   }
 }
 
-// Heavy rows: out[row] (+)= s * sum_k slab[first + k]  (chunk order => deterministic).
+// Heavy rows: out[row] (+)= s * sum_k slab[first + k].  One block per heavy row: S slices of
+// the chunk list (strided) x the row's vectors, then a fixed-order LDS tree => deterministic.
 template <int W>
 __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
   using V = Vec<W>;
-  const int64_t h = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (h >= a.n_heavy) return;
-  const int lane = threadIdx.x & 63;
+  __shared__ typename V::T buf[256];
+  const int64_t h = blockIdx.x;
   const int64_t row = a.heavy_rows[h];
   const int64_t f0 = a.heavy_first[h], f1 = a.heavy_first[h + 1];
   const int64_t deg = a.rowptr[row + 1] - a.rowptr[row];
   const float s = a.mean ? (deg > 0 ? 1.f / (float)deg : 0.f) : 1.f;
-  for (int c = lane * W; c < a.d; c += 64 * W) {
+  const int nvec = (a.d + W - 1) / W;
+  int cpb = 1;
+  while (cpb < nvec && cpb < 256) cpb <<= 1;
+  const int S = 256 / cpb;
+  const int slice = threadIdx.x / cpb, cv = threadIdx.x % cpb;
+  for (int c0 = 0; c0 < nvec; c0 += cpb) {
+    const int c = (c0 + cv) * W;
     typename V::T r = V::zero();
-    for (int64_t k = f0; k < f1; ++k) V::add(r, V::load(a.slab + k * a.d + c));
-    V::scale(r, s);
-    float* o = a.out + row * a.d + c;
-    if (a.accumulate) V::add(r, V::load(o));
-    V::store(o, r);
+    if (c < a.d) {
+      int64_t k = f0 + slice;
+      for (; k + 3 * S < f1; k += 4 * S) {   // 4 independent loads in flight
+        typename V::T x0 = V::load(a.slab + k * a.d + c);
+        typename V::T x1 = V::load(a.slab + (k + S) * a.d + c);
+        typename V::T x2 = V::load(a.slab + (k + 2 * S) * a.d + c);
+        typename V::T x3 = V::load(a.slab + (k + 3 * S) * a.d + c);
+        V::add(x0, x1); V::add(x2, x3); V::add(x0, x2); V::add(r, x0);
+      }
+      for (; k < f1; k += S) V::add(r, V::load(a.slab + k * a.d + c));
+    }
+    buf[threadIdx.x] = r;
+    __syncthreads();
+    for (int st = S / 2; st >= 1; st >>= 1) {
+      if (slice < st) {
+        typename V::T t = buf[threadIdx.x];
+        V::add(t, buf[threadIdx.x + st * cpb]);
+        buf[threadIdx.x] = t;
+      }
+      __syncthreads();
+    }
+    if (slice == 0 && c < a.d) {
+      typename V::T t = buf[threadIdx.x];
+      V::scale(t, s);
+      float* o = a.out + row * a.d + c;
+      if (a.accumulate) V::add(t, V::load(o));
+      V::store(o, t);
+    }
+    __syncthreads();
   }
 }
 
@@ -202,7 +232,7 @@ static int run_gather(GatherArgs a, hipStream_t stream) {
   const bool has_w = a.edge_w || a.col_w;
   if (int rc = dispatch_gather(a, has_w, stream)) return rc;
   if (a.n_heavy > 0) {
-    const dim3 grid((unsigned)cdiv(a.n_heavy, 4)), block(256);
+    const dim3 grid((unsigned)a.n_heavy), block(256);
     if (a.d % 4 == 0) hipLaunchKernelGGL(k_fixup<4>, grid, block, 0, stream, a);
     else hipLaunchKernelGGL(k_fixup<1>, grid, block, 0, stream, a);
     return check_launch("k_fixup");

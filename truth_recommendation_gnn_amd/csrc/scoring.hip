@@ -168,13 +168,17 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   }
 }
 
-// loss = c * inv_e * sum(part[:,0]) + inv_e * sum(part[:,1]); one block, fixed order, double.
-__global__ void __launch_bounds__(256) k_loss_reduce(const float* part, int64_t n_part,
-                                                     const float* cscale, float inv_e,
-                                                     float* loss) {
+// Deterministic two-level reduction of the block partials: 64 blocks each sum a contiguous
+// range (double), then one block sums the 64 and forms the loss.
+constexpr int kRedBlocks = 64;
+
+__global__ void __launch_bounds__(256) k_loss_partial(const float* part, int64_t n_part,
+                                                      double* red) {
   __shared__ double sp[256], sn[256];
+  const int64_t per = cdiv(n_part, kRedBlocks);
+  const int64_t b0 = blockIdx.x * per, b1 = min<int64_t>(b0 + per, n_part);
   double p = 0.0, q = 0.0;
-  for (int64_t i = threadIdx.x; i < n_part; i += 256) {
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) {
     p += part[2 * i];
     q += part[2 * i + 1];
   }
@@ -188,8 +192,21 @@ __global__ void __launch_bounds__(256) k_loss_reduce(const float* part, int64_t 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0)
-    *loss = (float)((double)*cscale * (double)inv_e * sp[0] + (double)inv_e * sn[0]);
+  if (threadIdx.x == 0) {
+    red[2 * blockIdx.x] = sp[0];
+    red[2 * blockIdx.x + 1] = sn[0];
+  }
+}
+
+// loss = c * inv_e * sum(pos) + inv_e * sum(neg)
+__global__ void k_loss_final(const double* red, const float* cscale, float inv_e, float* loss) {
+  if (threadIdx.x != 0) return;
+  double p = 0.0, q = 0.0;
+  for (int i = 0; i < kRedBlocks; ++i) {
+    p += red[2 * i];
+    q += red[2 * i + 1];
+  }
+  *loss = (float)((double)*cscale * (double)inv_e * p + (double)inv_e * q);
 }
 
 template <int LPR, int VPL, int W, int UNROLL>
@@ -205,7 +222,10 @@ using namespace hgnn;
 
 extern "C" {
 
-int64_t hgnn_edge_score_parts(int64_t n_users) { return cdiv(n_users, 4); }
+// floats of `part` scratch: 2 per block (4 users) + room for 2*64 doubles, 16-B aligned
+int64_t hgnn_edge_score_parts(int64_t n_users) {
+  return (int64_t)align_up((size_t)(2 * cdiv(n_users, 4)), 4) + 4 * kRedBlocks;
+}
 
 int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
                         int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
@@ -224,7 +244,7 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   a.to_post_pos = to_post_pos; a.cscale = cscale; a.dU = dU; a.hpos = hpos; a.neg_key = neg_key;
   a.neg_u = neg_user; a.neg_w = neg_w; a.part = part; a.err = err; a.n_users = n_users;
   a.n_posts = n_posts; a.inv_e = n_edges > 0 ? 1.f / (float)n_edges : 0.f; a.d = d;
-  const int64_t nb = hgnn_edge_score_parts(n_users);
+  const int64_t nb = cdiv(n_users, 4);   // blocks of 4 user-waves
   int rc = HGNN_OK;
   if (nb > 0) {
     if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4, 2>(a, nb, stream);
@@ -235,9 +255,12 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
     else return fail(HGNN_E_UNSUPPORTED, "edge_score: d=%d", d);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(k_loss_reduce, dim3(1), dim3(256), 0, stream, part, nb, cscale, a.inv_e,
-                     loss);
-  return check_launch("k_loss_reduce");
+  // the reduction scratch lives after the block partials: part holds 2*nb floats + 2*64 doubles
+  double* red = reinterpret_cast<double*>(part + align_up((size_t)(2 * nb), 4));
+  hipLaunchKernelGGL(k_loss_partial, dim3(kRedBlocks), dim3(256), 0, stream, part, nb, red);
+  if (int rc2 = check_launch("k_loss_partial")) return rc2;
+  hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, stream, red, cscale, a.inv_e, loss);
+  return check_launch("k_loss_final");
 }
 
 }  // extern "C"

@@ -321,8 +321,7 @@ class _EdgeBCELoss(torch.autograd.Function):
         neg_key = torch.empty(E, dtype=torch.int32, device=dev)
         neg_user = torch.empty(E, dtype=torch.int32, device=dev)
         neg_w = torch.empty(E, dtype=torch.float32, device=dev)
-        part = torch.empty(2 * max(int(lib.hgnn_edge_score_parts(nu)), 1), dtype=torch.float32,
-                           device=dev)
+        part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         err = torch.zeros(2, dtype=torch.int32, device=dev)
         c = cscale.to(torch.float32).reshape(()).contiguous()
