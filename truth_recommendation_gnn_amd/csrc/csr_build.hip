@@ -185,58 +185,115 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
     counts[(int64_t)dd * gridDim.x + blockIdx.x] = hist[dd];
 }
 
-// Stable scatter: rounds in order; within a round, items in thread order.  Per wave the match
-// set of a digit comes from BITS ballots; per-wave digit counts go through LDS.  Carries up to
-// two 32-bit payloads (a: identity when identity_a is set; b optional).
+// Stable scatter, block-local sort first.  Tile = 4096 items; wave w owns the contiguous
+// items [w*1024, (w+1)*1024) and walks them in 16 rounds of 64, ranking each item among equal
+// digits with BITS ballots and a wave-private running count in LDS (no block barrier per round).
+// The tile is then reordered by (digit, original index) in LDS and written out in per-digit
+// runs, so global stores are contiguous runs instead of scattered words.  Carries up to two
+// 32-bit payloads (a: identity when identity_a is set; b optional).
 template <int BITS>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
     const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
   constexpr int R = 1 << BITS;
-  __shared__ int base_off[R];                 // global offset + running count per digit
-  __shared__ int wcount[kSortThreads / 64][R];
+  constexpr int NW = kSortThreads / 64;
+  constexpr int PER_WAVE = kSortTile / NW;       // 1024
+  __shared__ int wcount[NW][R];                  // running count -> wave offset within tile
+  __shared__ int dstart[R];                      // tile-local start of each digit
+  __shared__ int gbase[R];                       // global start of this tile's digit run
+  __shared__ int skey[kSortTile];
+  __shared__ int sa[kSortTile];
+  __shared__ int sb[kSortTile];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
-    base_off[dd] = offs[(int64_t)dd * gridDim.x + blockIdx.x];
-    for (int w = 0; w < kSortThreads / 64; ++w) wcount[w][dd] = 0;
+    for (int w = 0; w < NW; ++w) wcount[w][dd] = 0;
+    gbase[dd] = offs[(int64_t)dd * gridDim.x + blockIdx.x];
   }
   __syncthreads();
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
+  const int64_t tile0 = (int64_t)blockIdx.x * kSortTile;
+  const int64_t wave0 = tile0 + (int64_t)wid * PER_WAVE;
+  int key[kSortRounds], rank[kSortRounds], va[kSortRounds], vb[kSortRounds];
+#pragma unroll
   for (int r = 0; r < kSortRounds; ++r) {
-    int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
+    const int64_t i = wave0 + r * 64 + lane;
     const bool valid = i < E;
-    int key = valid ? keys_in[i] : 0;
-    int va = valid ? (identity_a ? (int)i : a_in[i]) : 0;
-    int vb = (valid && b_in) ? b_in[i] : 0;
-    int digit = (key >> shift) & (R - 1);
+    key[r] = valid ? keys_in[i] : 0;
+    va[r] = valid ? (identity_a ? (int)i : a_in[i]) : 0;
+    vb[r] = (valid && b_in) ? b_in[i] : 0;
+    const int digit = (key[r] >> shift) & (R - 1);
     unsigned long long match = __ballot(valid);
 #pragma unroll
     for (int bit = 0; bit < BITS; ++bit) {
-      unsigned long long m = __ballot((digit >> bit) & 1);
+      const unsigned long long m = __ballot((digit >> bit) & 1);
       match &= ((digit >> bit) & 1) ? m : ~m;
     }
-    int rank = __popcll(match & lt_mask);
-    if (valid && rank == 0) wcount[wid][digit] = __popcll(match);
-    __syncthreads();
-    if (valid) {
-      int pos = base_off[digit] + rank;
-      for (int w = 0; w < wid; ++w) pos += wcount[w][digit];
-      keys_out[pos] = key;
-      a_out[pos] = va;
-      if (b_out) b_out[pos] = vb;
+    const int before = valid ? wcount[wid][digit] : 0;    // read, then the leader bumps it
+    rank[r] = valid ? before + __popcll(match & lt_mask) : -1;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && __popcll(match & lt_mask) == 0) wcount[wid][digit] = before + __popcll(match);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // tile-local digit starts (exclusive scan over digits of the tile totals) and wave offsets
+  {
+    __shared__ int part[kSortThreads];
+    constexpr int DPT = (R + kSortThreads - 1) / kSortThreads;   // digits per thread (1 or 2)
+    int tot[DPT], s = 0;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+      const int dd = threadIdx.x * DPT + q;
+      int t = 0;
+      if (dd < R)
+        for (int w = 0; w < NW; ++w) t += wcount[w][dd];
+      tot[q] = t;
+      s += t;
     }
+    part[threadIdx.x] = s;
     __syncthreads();
-    // advance running offsets, clear the per-wave counts
-    for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
-      int sum = 0;
-      for (int w = 0; w < kSortThreads / 64; ++w) {
-        sum += wcount[w][dd];
-        wcount[w][dd] = 0;
+    // Hillis-Steele inclusive scan of the 256 per-thread sums
+    for (int o = 1; o < kSortThreads; o <<= 1) {
+      const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    int run = part[threadIdx.x] - s;
+#pragma unroll
+    for (int q = 0; q < DPT; ++q) {
+      const int dd = threadIdx.x * DPT + q;
+      if (dd < R) {
+        dstart[dd] = run;
+        int o = run;
+        for (int w = 0; w < NW; ++w) {
+          const int c = wcount[w][dd];
+          wcount[w][dd] = o;
+          o += c;
+        }
       }
-      base_off[dd] += sum;
+      run += tot[q];
     }
-    __syncthreads();
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kSortRounds; ++r) {
+    if (rank[r] >= 0) {
+      const int digit = (key[r] >> shift) & (R - 1);
+      const int pos = wcount[wid][digit] + rank[r];
+      skey[pos] = key[r];
+      sa[pos] = va[r];
+      sb[pos] = vb[r];
+    }
+  }
+  __syncthreads();
+  const int n_tile = (int)min<int64_t>(kSortTile, E - tile0);
+  for (int j = threadIdx.x; j < n_tile; j += kSortThreads) {
+    const int k = skey[j];
+    const int digit = (k >> shift) & (R - 1);
+    const int64_t pos = (int64_t)gbase[digit] + (j - dstart[digit]);
+    keys_out[pos] = k;
+    a_out[pos] = sa[j];
+    if (b_out) b_out[pos] = sb[j];
   }
 }
 

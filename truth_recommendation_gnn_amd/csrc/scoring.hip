@@ -16,6 +16,8 @@
 // grouped CSR, negatives over the (n_e)-sorted list (hgnn_sort_pairs_i32).  Deterministic.
 #include "hgnn_common.h"
 
+#include <stdlib.h>
+
 namespace hgnn {
 
 struct ScoreArgs {
@@ -39,10 +41,18 @@ struct ScoreArgs {
   int32_t d;
 };
 
-__device__ __forceinline__ float softplus(float x) {
-  return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x)));
+// Hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1-2 ulp): libm-accurate expf /
+// log1pf / division cost 2x the whole pass here.  t = exp(-|x|) in (0, 1] is shared by both:
+//   sigmoid(x) = x >= 0 ? 1/(1+t) : t/(1+t),   softplus(x) = max(x, 0) + log(1 + t)
+// (log(1+t) loses t below ~1e-7 absolute — far under the fp32 loss tolerance).
+__device__ __forceinline__ float exp_neg_abs(float x) { return __expf(-fabsf(x)); }
+__device__ __forceinline__ float sigmoid_t(float x, float t) {
+  const float r = __builtin_amdgcn_rcpf(1.f + t);
+  return x >= 0.f ? r : t * r;
 }
-__device__ __forceinline__ float sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+__device__ __forceinline__ float softplus(float x) {
+  return fmaxf(x, 0.f) + __logf(1.f + exp_neg_abs(x));
+}
 
 template <int LPR, int VPL, int W>
 __device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
@@ -62,7 +72,7 @@ __device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
   return s;
 }
 
-template <int LPR, int VPL, int W, int UNROLL>
+template <int LPR, int VPL, int W, int UNROLL, int ABL = 0>
 __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   using V = Vec<W>;
   constexpr int NS = 64 / LPR;
@@ -112,8 +122,12 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
           const int e = e0 + slot;
           const float sp = slot_dot<LPR, VPL, W>(uv, vp[uu]);
           const float sn = slot_dot<LPR, VPL, W>(uv, vn[uu]);
-          float hp = c * a.inv_e * (sigmoid(sp) - 1.f);
-          float hn = a.inv_e * sigmoid(sn);
+          float hp, hn;
+          if (ABL & 2) { hp = c * a.inv_e * sp; hn = a.inv_e * sn; }
+          else {
+            hp = c * a.inv_e * (sigmoid_t(sp, exp_neg_abs(sp)) - 1.f);
+            hn = a.inv_e * sigmoid_t(sn, exp_neg_abs(sn));
+          }
           if (e >= n) hp = hn = 0.f;
 #pragma unroll
           for (int q = 0; q < VPL; ++q) {
@@ -123,7 +137,7 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
           // hand edge e's values to lane e (lanes e0 .. e0+NS-1 read from slot lane*LPR)
           const int src = ((lane - e0) & (NS - 1)) * LPR;
           const float thp = __shfl(hp, src, 64), thn = __shfl(hn, src, 64);
-          const float tsp = __shfl(softplus(-sp), src, 64), tsn = __shfl(softplus(sn), src, 64);
+          const float tsp = __shfl(sp, src, 64), tsn = __shfl(sn, src, 64);
           if (lane >= e0 && lane < e0 + NS) {
             my_hp = thp; my_hn = thn; my_sp = tsp; my_sn = tsn;
           }
@@ -131,12 +145,16 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
       }
       if (lane < n) {
         const int64_t k = base + lane;
-        lpos += my_sp;
-        lneg += my_sn;
-        a.hpos[a.to_post_pos[k]] = my_hp;
-        a.neg_key[k] = nid;
-        a.neg_u[k] = (int32_t)u;
-        a.neg_w[k] = my_hn;
+        // the loss terms once per edge, on the lane that owns it
+        lpos += (ABL & 2) ? my_sp : softplus(-my_sp);
+        lneg += (ABL & 2) ? my_sn : softplus(my_sn);
+        if (ABL & 1) a.hpos[k] = my_hp;
+        else a.hpos[a.to_post_pos[k]] = my_hp;
+        if (!(ABL & 4)) {
+          a.neg_key[k] = nid;
+          a.neg_u[k] = (int32_t)u;
+          a.neg_w[k] = my_hn;
+        }
       }
     }
 #pragma unroll
@@ -211,8 +229,15 @@ __global__ void k_loss_final(const double* red, const float* cscale, float inv_e
 
 template <int LPR, int VPL, int W, int UNROLL>
 static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream) {
-  hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), dim3((unsigned)nblocks), dim3(256), 0,
-                     stream, a);
+  static const int abl = getenv("HGNN_SCORE_ABL") ? atoi(getenv("HGNN_SCORE_ABL")) : 0;
+  const dim3 g((unsigned)nblocks), b(256);
+  switch (abl) {
+    case 1: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 1>), g, b, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 2>), g, b, 0, stream, a); break;
+    case 4: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 4>), g, b, 0, stream, a); break;
+    case 7: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 7>), g, b, 0, stream, a); break;
+    default: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), g, b, 0, stream, a);
+  }
   return check_launch("k_edge_score");
 }
 

@@ -196,6 +196,18 @@ class RelationCSR:
             self._bwd = group_edges(self._ei[0], self._ei[1], self.n_src, self.n_dst, self.chunk)
         return self._bwd
 
+    @property
+    def bwd_weights(self) -> torch.Tensor:
+        """1/deg(dst) per CSC position (static): K2 streams it instead of a dependent random
+        lookup of inv_deg[dst] per edge."""
+        w = getattr(self, "_bwd_w", None)
+        if w is None:
+            g = self.bwd
+            w = self.inv_deg[g.col.long()].contiguous() if self.num_edges else \
+                torch.empty(0, dtype=torch.float32, device=self.inv_deg.device)
+            self._bwd_w = w
+        return w
+
     def release_coo(self):
         """Drop the COO reference once the CSC exists (saves 16 B/edge of HBM)."""
         if self._bwd is not None:

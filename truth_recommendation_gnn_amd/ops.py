@@ -121,7 +121,8 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
     acc = out is not None
     if out is None:
         out = torch.empty(csr.n_src, d, dtype=torch.float32, device=dev)
-    _gather(grad_aggr, csr.bwd, csr.inv_deg, csr_mean=False, out=out, accumulate=acc)
+    _gather(grad_aggr, csr.bwd, None, csr_mean=False, out=out, accumulate=acc,
+            edge_w=csr.bwd_weights)
     return out
 
 
