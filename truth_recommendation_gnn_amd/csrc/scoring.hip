@@ -236,6 +236,7 @@ static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream)
     case 2: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 2>), g, b, 0, stream, a); break;
     case 4: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 4>), g, b, 0, stream, a); break;
     case 7: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 7>), g, b, 0, stream, a); break;
+    case 8: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, 2, 0>), g, b, 0, stream, a); break;
     default: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), g, b, 0, stream, a);
   }
   return check_launch("k_edge_score");
@@ -272,9 +273,11 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   const int64_t nb = cdiv(n_users, 4);   // blocks of 4 user-waves
   int rc = HGNN_OK;
   if (nb > 0) {
-    if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4, 2>(a, nb, stream);
-    else if (d % 4 == 0 && d <= 128) rc = launch_score<32, 1, 4, 2>(a, nb, stream);
-    else if (d % 4 == 0 && d <= 256) rc = launch_score<64, 1, 4, 2>(a, nb, stream);
+    // UNROLL 1 measured fastest at d=64 (1.76 vs 1.92 ms at 2, 2.16 at 4 on cfg2): the pass is
+    // issue-bound, fewer registers buy more waves
+    if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4, 1>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 128) rc = launch_score<32, 1, 4, 1>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 256) rc = launch_score<64, 1, 4, 1>(a, nb, stream);
     else if (d <= 64) rc = launch_score<64, 1, 1, 1>(a, nb, stream);
     else if (d <= 512) rc = launch_score<64, 8, 1, 1>(a, nb, stream);
     else return fail(HGNN_E_UNSUPPORTED, "edge_score: d=%d", d);
