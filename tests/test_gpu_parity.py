@@ -107,8 +107,9 @@ def test_gather_is_deterministic_bitwise():
 
 # ----------------------------------------------------------------------------- K3 / K4
 @pytest.mark.parametrize("ks,h", [([64], 64), ([64, 64], 64), ([64, 64, 64], 64),
-                                  ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100)])
-@pytest.mark.parametrize("n", [1, 37, 1000])
+                                  ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100),
+                                  ([64], 128), ([32], 16), ([64, 32], 32)])
+@pytest.mark.parametrize("n", [1, 37, 1000, 20000])
 def test_linear_fwd_bwd_matches_torch(ks, h, n):
     gen = torch.Generator().manual_seed(n + h)
     segs = [torch.randn(n, k, generator=gen) for k in ks]

@@ -297,6 +297,232 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* slab, int64_t
   }
 }
 
+// ================================================================ LDS fast paths
+// When W fits in LDS (h*K*4 <= 64 KiB), h % 16 == 0, K % 16 == 0 and every segment is float4-
+// aligned: persistent blocks keep W (forward) or W^T (backward) resident in LDS for the whole
+// launch and stream 32-row tiles of the concatenated segments through LDS with coalesced 16-B
+// loads; MFMA fragments come from LDS (ds_read_b128 / b32), outputs leave as whole rows.
+constexpr int FT = 32;  // rows per tile
+
+// [FT x K] tile of the concatenated segments -> xs (row stride ld), zero rows past n.
+__device__ __forceinline__ void stage_x_tile(const LinArgs& a, int64_t r0, float* xs, int ld) {
+  const int k4 = a.k_total >> 2;
+  for (int idx = threadIdx.x; idx < FT * k4; idx += 256) {
+    const int r = idx / k4, k = (idx - r * k4) * 4;
+    int s = 0;
+    while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
+    const int64_t row = r0 + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < a.n)
+      v = *reinterpret_cast<const float4*>(a.seg[s].x + row * a.seg[s].k + (k - a.seg[s].off));
+    *reinterpret_cast<float4*>(xs + r * ld + k) = v;
+  }
+}
+
+// Forward: waves = 2 row halves x 2 column halves of the [FT x h] output tile.
+template <int NT>
+__global__ void __launch_bounds__(256) k_linear_fwd_lds(const LinArgs a, int64_t n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K = a.k_total, h = a.h;
+  const int ldw = K + 4, ldx = K + 4, ldo = h + 4;
+  float* ws = smem;              // [h][ldw]
+  float* xs = ws + h * ldw;      // [FT][ldx]; reused as the output staging tile [FT][ldo]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int rt = wave & 1, ch = wave >> 1;     // row tile (16 rows), column half
+  constexpr int NTW = NT / 2 > 0 ? NT / 2 : 1;
+  const int t0 = (NT >= 2) ? ch * NTW : 0;
+  const bool active_cols = NT >= 2 || ch == 0;
+  for (int idx = threadIdx.x; idx < h * (K >> 2); idx += 256) {
+    const int j = idx / (K >> 2), k = (idx - j * (K >> 2)) * 4;
+    *reinterpret_cast<float4*>(ws + j * ldw + k) =
+        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
+  }
+  float bias[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) bias[t] = a.bias ? a.bias[(t0 + t) * 16 + i] : 0.f;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * FT;
+    __syncthreads();
+    stage_x_tile(a, r0, xs, ldx);
+    __syncthreads();
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (active_cols) {
+      for (int kc = 0; kc < K; kc += 16) {
+        const float4 av = *reinterpret_cast<const float4*>(xs + (rt * 16 + i) * ldx + kc + 4 * g);
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) {
+          const float4 bv =
+              *reinterpret_cast<const float4*>(ws + ((t0 + t) * 16 + i) * ldw + kc + 4 * g);
+          acc[t] = mfma4(av.x, bv.x, acc[t]);
+          acc[t] = mfma4(av.y, bv.y, acc[t]);
+          acc[t] = mfma4(av.z, bv.z, acc[t]);
+          acc[t] = mfma4(av.w, bv.w, acc[t]);
+        }
+      }
+    }
+    __syncthreads();   // xs becomes the output staging tile
+    if (active_cols) {
+#pragma unroll
+      for (int t = 0; t < NTW; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[t][r] + bias[t];
+          if (a.relu) v = fmaxf(v, 0.f);
+          xs[(rt * 16 + 4 * g + r) * ldo + (t0 + t) * 16 + i] = v;
+        }
+    }
+    __syncthreads();
+    const int h4 = h >> 2;
+    for (int idx = threadIdx.x; idx < FT * h4; idx += 256) {
+      const int r = idx / h4, c = (idx - r * h4) * 4;
+      const int64_t row = r0 + r;
+      if (row < a.n)
+        *reinterpret_cast<float4*>(a.out + row * h + c) =
+            *reinterpret_cast<const float4*>(xs + r * ldo + c);
+    }
+  }
+}
+
+// Fused backward: per 32-row tile, dz = dout * (out > 0) and X staged once; dX = dz @ W (W^T in
+// LDS) and the block's dW (+ db as the column K) accumulated in registers across its tiles,
+// written once as a partial [h][K+1] slab (reduced in block order by k_wgrad_reduce).
+template <int NT, bool DX>
+__global__ void __launch_bounds__(256) k_linear_bwd_lds(const LinArgs a, int64_t n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K = a.k_total, h = a.h;
+  const int ldwt = h + 4, ldz = h + 16, ldx = K + 16;   // b32 reads: row stride = 16 mod 32
+  float* wt = smem;                 // [K][ldwt]  W^T
+  float* dz = wt + K * ldwt;        // [FT][ldz]
+  float* xs = dz + FT * ldz;        // [FT][ldx]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  constexpr int JT = NT >= 4 ? NT / 4 : 1;      // j tiles per wave (wgrad)
+  const bool wave_has_j = NT >= 4 || wave < NT;
+  const int KT = K >> 4;
+  if (DX) {
+    for (int idx = threadIdx.x; idx < h * K; idx += 256) {
+      const int j = idx / K, k = idx - j * K;
+      wt[k * ldwt + j] = a.w[(int64_t)j * K + k];
+    }
+  }
+  f32x4 acc[JT][8];   // K <= 128 on this path
+#pragma unroll
+  for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt) acc[jt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int h4 = h >> 2;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * FT;
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < FT * h4; idx += 256) {
+      const int r = idx / h4, c = (idx - r * h4) * 4;
+      const int64_t row = r0 + r;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < a.n) {
+        v = *reinterpret_cast<const float4*>(a.dout + row * h + c);
+        if (a.out_act) {
+          const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * h + c);
+          v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
+          v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
+        }
+      }
+      dbacc.x += v.x; dbacc.y += v.y; dbacc.z += v.z; dbacc.w += v.w;
+      *reinterpret_cast<float4*>(dz + r * ldz + c) = v;
+    }
+    stage_x_tile(a, r0, xs, ldx);
+    __syncthreads();
+    if (DX) {   // dX tile [FT x K]: wave = row tile (wave & 1) x column half (wave >> 1)
+      const int rt = wave & 1, half = wave >> 1;
+      const int ct0 = half * (KT >> 1), nct = KT >> 1;
+      for (int c = 0; c < nct; ++c) {
+        const int ct = ct0 + c;
+        f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int jc = 0; jc < h; jc += 16) {
+          const float4 av = *reinterpret_cast<const float4*>(dz + (rt * 16 + i) * ldz + jc + 4 * g);
+          const float4 bv = *reinterpret_cast<const float4*>(wt + (ct * 16 + i) * ldwt + jc + 4 * g);
+          o = mfma4(av.x, bv.x, o);
+          o = mfma4(av.y, bv.y, o);
+          o = mfma4(av.z, bv.z, o);
+          o = mfma4(av.w, bv.w, o);
+        }
+        const int col = ct * 16 + i;
+        int s = 0;
+        while (s + 1 < a.n_seg && col >= a.seg[s].off + a.seg[s].k) ++s;
+        float* dx = a.seg[s].dx;
+        if (dx) {
+          const int kk = col - a.seg[s].off, ks = a.seg[s].k;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + rt * 16 + 4 * g + r;
+            if (row < a.n) dx[row * ks + kk] = o[r];
+          }
+        }
+      }
+    }
+    if (wave_has_j) {   // wgrad: A[i=j][kk=row] = dz[row][j], B[kk=row][col=k] = X[row][k]
+#pragma unroll 2
+      for (int s4 = 0; s4 < FT / 4; ++s4) {
+        const int r = 4 * s4 + g;
+        float bv[8];
+#pragma unroll
+        for (int kt = 0; kt < 8; ++kt) bv[kt] = kt < KT ? xs[r * ldx + kt * 16 + i] : 0.f;
+#pragma unroll
+        for (int jt = 0; jt < JT; ++jt) {
+          const float av = dz[r * ldz + (wave + 4 * jt) * 16 + i];
+#pragma unroll
+          for (int kt = 0; kt < 8; ++kt)
+            if (kt < KT) acc[jt][kt] = mfma4(av, bv[kt], acc[jt][kt]);
+        }
+      }
+    }
+  }
+  // partial slab [blockIdx.x][h][K+1]
+  const int kext = K + 1;
+  float* slab = a.slab + (int64_t)blockIdx.x * h * kext;
+  if (wave_has_j) {
+#pragma unroll
+    for (int jt = 0; jt < JT; ++jt)
+#pragma unroll
+      for (int kt = 0; kt < 8; ++kt) {
+        if (kt >= KT) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = (wave + 4 * jt) * 16 + 4 * g + r;
+          slab[(int64_t)j * kext + kt * 16 + i] = acc[jt][kt][r];
+        }
+      }
+  }
+  __syncthreads();
+  float4* red = reinterpret_cast<float4*>(xs);     // [256] thread partials of db
+  red[threadIdx.x] = dbacc;
+  __syncthreads();
+  if (threadIdx.x < h4) {   // thread t staged columns 4*(t % h4) on every tile
+    float4 t = red[threadIdx.x];
+    for (int m = threadIdx.x + h4; m < 256; m += h4) {
+      const float4 u = red[m];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const int c = threadIdx.x * 4;
+    slab[(int64_t)(c + 0) * kext + K] = t.x;
+    slab[(int64_t)(c + 1) * kext + K] = t.y;
+    slab[(int64_t)(c + 2) * kext + K] = t.z;
+    slab[(int64_t)(c + 3) * kext + K] = t.w;
+  }
+}
+
+static bool fast_path_ok(const LinArgs& a, bool vec) {
+  return vec && a.h % 16 == 0 && a.h <= 128 && a.k_total % 32 == 0 && a.k_total <= 128 &&
+         (size_t)a.h * a.k_total * 4 <= 65536 && 256 % (a.h / 4) == 0;
+}
+
+static int fast_grid(int64_t n_tiles) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 512));
+}
+
 static int fill_args(LinArgs& a, int32_t n_seg, const float* const* xs, const int32_t* ks,
                      float* const* dxs, int64_t n_rows, const float* w, int32_t h, bool* vec) {
   if (n_seg < 1 || n_seg > HGNN_MAX_SEG) return fail(HGNN_E_ARG, "linear: n_seg=%d", n_seg);
@@ -339,6 +565,22 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.bias = bias;
   a.out = out;
   a.relu = relu;
+  if (fast_path_ok(a, vec)) {
+    const int64_t n_tiles = cdiv(n_rows, FT);
+    const size_t lds = ((size_t)h * (a.k_total + 4) +
+                        std::max<size_t>((size_t)FT * (a.k_total + 4), (size_t)FT * (h + 4))) * 4;
+    const dim3 grid(fast_grid(n_tiles)), block(256);
+    switch (h / 16) {
+      case 1: hipLaunchKernelGGL(k_linear_fwd_lds<1>, grid, block, lds, stream, a, n_tiles); break;
+      case 2: hipLaunchKernelGGL(k_linear_fwd_lds<2>, grid, block, lds, stream, a, n_tiles); break;
+      case 4: hipLaunchKernelGGL(k_linear_fwd_lds<4>, grid, block, lds, stream, a, n_tiles); break;
+      case 6: hipLaunchKernelGGL(k_linear_fwd_lds<6>, grid, block, lds, stream, a, n_tiles); break;
+      case 8: hipLaunchKernelGGL(k_linear_fwd_lds<8>, grid, block, lds, stream, a, n_tiles); break;
+      default: goto general;
+    }
+    return check_launch("k_linear_fwd_lds");
+  }
+general:
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
   if (h <= 64) {
     const dim3 grid(gx, 1);
@@ -366,6 +608,7 @@ static void wgrad_grid(int64_t n_rows, int32_t k_total, int32_t h, int64_t* gx, 
 size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h) {
   int64_t gx, rpb;
   wgrad_grid(n_rows < 1 ? 1 : n_rows, k_total, h, &gx, &rpb);
+  gx = std::max<int64_t>(gx, fast_grid(cdiv(n_rows < 1 ? 1 : n_rows, FT)));
   return align_up((size_t)gx * h * (k_total + 1) * 4, 256) + 256;
 }
 
@@ -391,6 +634,33 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   }
   bool any_dx = false;
   for (int s = 0; s < n_seg; ++s) any_dx |= a.seg[s].dx != nullptr;
+  if (fast_path_ok(a, vec) && (dw || db) && ws) {
+    const int64_t n_tiles = cdiv(n_rows, FT);
+    const int G = fast_grid(n_tiles);
+    const size_t need = (size_t)G * h * (a.k_total + 1) * 4;
+    if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+    a.slab = static_cast<float*>(ws);
+    const size_t lds = ((size_t)a.k_total * (h + 4) + (size_t)FT * (h + 16) +
+                        (size_t)FT * (a.k_total + 16)) * 4;
+    const dim3 grid(G), block(256);
+#define HGNN_BWD_LDS(NTV)                                                                      \
+  if (any_dx) hipLaunchKernelGGL((k_linear_bwd_lds<NTV, true>), grid, block, lds, stream, a,   \
+                                 n_tiles);                                                     \
+  else hipLaunchKernelGGL((k_linear_bwd_lds<NTV, false>), grid, block, lds, stream, a, n_tiles);
+    switch (h / 16) {
+      case 1: HGNN_BWD_LDS(1) break;
+      case 2: HGNN_BWD_LDS(2) break;
+      case 4: HGNN_BWD_LDS(4) break;
+      case 8: HGNN_BWD_LDS(8) break;
+      default: return fail(HGNN_E_UNSUPPORTED, "linear_bwd fast path: h=%d", h);
+    }
+#undef HGNN_BWD_LDS
+    if (int rc = check_launch("k_linear_bwd_lds")) return rc;
+    const int64_t total = (int64_t)h * (a.k_total + 1);
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+                       a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
+    return check_launch("k_wgrad_reduce");
+  }
   if (any_dx) {
     const dim3 grid((unsigned)cdiv(n_rows, kRowsPerBlock), (unsigned)cdiv(a.k_total, 128));
     if (vec) hipLaunchKernelGGL((k_linear_dgrad<8, true>), grid, dim3(256), 0, stream, a);
