@@ -8,10 +8,11 @@ step of ``train_gnn.py:242-285``: forward, the reference link loss over all 20M 
 with fresh ``torch.randint`` negatives, full backward, Adam.  Inputs resident in HBM before the
 timed region.  Metric numerator = sum over layers and relations of E_r = 80M edges/step.
 
-N>1 (``torch.distributed.run``): weak scaling — each rank owns one cfg2-sized destination shard
-(its own seeded graph), runs the same step, and the weight gradients are all-reduced over RCCL
-before the optimizer step (the only exchange this layout has).  value = all ranks' edges /
-max-over-ranks time.
+N>1 (``torch.distributed.run``): weak scaling — one global graph N times the cfg2 size (N·1M
+users, N·100k posts, N·20M engages), users sharded across ranks (each rank owns a cfg2-sized
+user range and its edges), posts replicated; the post aggregates and their gradients are
+all-reduced over RCCL every layer, weight gradients once per step (parallel.py).
+value = all ranks' edges / max-over-ranks time.
 
 Prints ONE JSON line (rank 0) with ``roofline`` for the dominant kernel (the K1 forward gather:
 algorithmic bytes per launch / HIP-event-timed duration inside the timed region) and
@@ -32,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from truth_recommendation_gnn_amd import HeteroSAGE, ops, synth  # noqa: E402
+from truth_recommendation_gnn_amd import parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
@@ -48,19 +50,11 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--profile-steps", action="store_true",
                    help="no per-kernel events (for rocprofv3 runs)")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
-
-
-def build(cfg, device, rank):
-    g = synth.make_graph(cfg, device=device)
-    if rank:  # a different destination shard per rank: reseed the edges
-        gen = torch.Generator(device=device).manual_seed(1000 + rank)
-        ei = g.edge_index_dict[synth.ENGAGES]
-        perm = torch.randperm(cfg.num_users, generator=gen, device=device)
-        ei = torch.stack([perm[ei[0]], ei[1]])
-        g.edge_index_dict[synth.ENGAGES] = ei
-        g.edge_index_dict[synth.REV_ENGAGES] = ei.flip(0)
-    return g
 
 
 def cpu_baseline(cfg, threads):
@@ -112,41 +106,62 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = synth.CONFIGS[args.config]
     if args.scale != 1.0:
         cfg = synth.scaled(args.config, args.scale)
-    g = build(cfg, dev, rank)
-    pos = g.edge_index_dict[synth.ENGAGES]
-    pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
     torch.manual_seed(synth.WEIGHT_SEED)
-    model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers).to(dev)
-    with torch.no_grad():
-        model(g.x_dict, g.edge_index_dict)      # materialise lazy weights, build + cache CSR/CSC
-    if world > 1:
+    gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED + rank)
+    if world == 1:
+        g = synth.make_graph(cfg, device=dev)
+        pos = g.edge_index_dict[synth.ENGAGES]
+        pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
+        model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers).to(dev)
+        with torch.no_grad():
+            model(g.x_dict, g.edge_index_dict)  # materialise lazy weights, build + cache CSR/CSC
+        edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
+
+        def forward_loss():
+            out = model(g.x_dict, g.edge_index_dict)
+            neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
+            return ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
+                                     check=False)
+    else:
+        env = parallel.DistEnv.from_torch()
+        gcfg = synth.replicated(args.config, world) if args.scale == 1.0 else cfg
+        g = synth.make_graph(gcfg, device=dev, device_gen=True)   # identical on every rank
+        pos_g = g.edge_index_dict[synth.ENGAGES]
+        pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
+        shard = parallel.UserShard(pos_g, gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g)
+        x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
+        x_post = g.x_dict["post"]
+        edges_step = gcfg.layers * 2 * int(pos_g.shape[1])   # global, both relations
+        del g, pos_g, pw_g
+        torch.cuda.empty_cache()
+        model = HeteroSAGE(gcfg.hidden, RELATIONS, num_layers=gcfg.layers).to(dev)
+        with torch.no_grad():
+            shard.forward(model, x_user, x_post)
         for p in model.parameters():
             dist.broadcast(p.data, 0)
+        cfg = gcfg
+
+        def forward_loss():
+            h_u, h_p = shard.forward(model, x_user, x_post)
+            neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
+            return shard.loss(h_u, h_p, neg, neg_order="user")
+
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-    gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED + rank)
 
     def step():
         opt.zero_grad(set_to_none=True)
-        out = model(g.x_dict, g.edge_index_dict)
-        neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
-        loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
-                                 check=False)
+        loss = forward_loss()
         loss.backward()
         if world > 1:
-            flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
-            dist.all_reduce(flat)
-            flat /= world
-            o = 0
-            for p in model.parameters():
-                n = p.numel()
-                p.grad.copy_(flat[o:o + n].view_as(p))
-                o += n
+            parallel.sync_grads(model, parallel.DistEnv.from_torch())
         opt.step()
         return loss
 
@@ -169,8 +184,7 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed)
-    edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
-    value = edges_step * args.steps * world / elapsed
+    value = edges_step * args.steps / elapsed     # edges_step is already the global count
     kern = timer.summary() if timer else {}
     if rank == 0:
         roof = None
@@ -197,8 +211,9 @@ def main():
             "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
                                    f"E_engage={cfg.num_engages} (+reverse), d=h={cfg.dim}, "
                                    f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
-                       "edges_per_step": edges_step, "global_batch": edges_step * world,
-                       "parallelism": f"dst-shard x{world}" if world > 1 else "single"},
+                       "edges_per_step": edges_step, "global_batch": edges_step,
+                       "parallelism": (f"user-shard x{world} (posts replicated, RCCL all-reduce)"
+                                       if world > 1 else "single")},
             "roofline": roof, "cpu_baseline": cpu,
             "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
                             "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}

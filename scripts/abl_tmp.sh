@@ -1,3 +1,3 @@
 cd $GRAFT_REPO_ROOT
-for a in 1 2 8 9; do echo "ABL=$a"; HGNN_SCORE_ABL=$a timeout -k 10 300 python scripts/microbench.py --reps 10 2>&1 | grep "edge_score"; done
-SKIP_TESTS=1 PROFILE=r1b bash scripts/gpu_round.sh --steps 20 --warmup 3
+timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider -k "linear or golden" > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -2 gpurun_out/gpu_tests.log; [ $rc -le 1 ] || exit $rc
+for v in 0 1; do echo "HGNN_LIN_GENERAL=$v"; HGNN_LIN_GENERAL=$v timeout -k 10 300 python scripts/microbench.py --reps 10 2>&1 | grep "K3"; done

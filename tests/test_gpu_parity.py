@@ -313,3 +313,38 @@ def test_sort_pairs_matches_numpy():
     assert np.array_equal(bo.cpu().numpy(), b.numpy()[order])
     rp, _, _ = csr_ref.coo_to_csr(keys.numpy(), keys.numpy(), nk)
     assert np.array_equal(rowptr.cpu().numpy(), rp)
+
+
+# ----------------------------------------------------------------------------- sharded path
+def test_user_shard_world1_matches_fused_model_and_oracle():
+    """parallel.UserShard on the HIP kernels (world=1, identity collectives) reproduces the fused
+    single-GPU model and the oracle: outputs, loss, gradients."""
+    from truth_recommendation_gnn_amd import parallel
+    z = np.load(GOLD / "cfg2_slice_hetero_sage.npz")
+    ei = torch.from_numpy(z["ei_engages"]).to(DEV)
+    x = {"user": torch.from_numpy(z["x_user"]).to(DEV), "post": torch.from_numpy(z["x_post"]).to(DEV)}
+    params = {k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")}
+    model = HeteroSAGE(64, parallel.RELATIONS, num_layers=2).to(DEV)
+    model.load_state_dict(params)
+    pw = torch.from_numpy(z["pos_weights"]).to(DEV)
+    shard = parallel.UserShard(ei, x["user"].shape[0], x["post"].shape[0], parallel.DistEnv(),
+                               pos_weights=pw)
+    h_u, h_p = shard.forward(model, x["user"], x["post"])
+    close(h_u, z["out_user"])
+    close(h_p, z["out_post"])
+    loss = shard.loss(h_u, h_p, torch.from_numpy(z["neg_p"]).to(DEV))
+    assert abs(float(loss) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_device_generated_graph_schema():
+    cfg = synth.scaled("cfg2", 0.01)
+    g = synth.make_graph(cfg, device=DEV, device_gen=True)
+    e = g.edge_index_dict[synth.ENGAGES]
+    assert e.shape == (2, cfg.num_engages) and e.dtype == torch.int64
+    assert int(e[0].max()) < cfg.num_users and int(e[1].max()) < cfg.num_posts
+    assert torch.equal(g.edge_index_dict[synth.REV_ENGAGES], e.flip(0))
+    g2 = synth.make_graph(cfg, device=DEV, device_gen=True)
+    assert torch.equal(g2.edge_index_dict[synth.ENGAGES], e)      # same on every rank

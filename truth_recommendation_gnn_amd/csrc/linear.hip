@@ -14,6 +14,7 @@
 #include "hgnn_common.h"
 
 #include <algorithm>
+#include <stdlib.h>
 
 namespace hgnn {
 
@@ -297,94 +298,48 @@ __global__ void __launch_bounds__(256) k_wgrad_reduce(const float* slab, int64_t
   }
 }
 
-// ================================================================ LDS fast paths
-// When W fits in LDS (h*K*4 <= 64 KiB), h % 16 == 0, K % 16 == 0 and every segment is float4-
-// aligned: persistent blocks keep W (forward) or W^T (backward) resident in LDS for the whole
-// launch and stream 32-row tiles of the concatenated segments through LDS with coalesced 16-B
-// loads; MFMA fragments come from LDS (ds_read_b128 / b32), outputs leave as whole rows.
+// ================================================================ fused backward (LDS path)
+// When W fits in LDS (h*K*4 <= 64 KiB), h % 16 == 0, K % 32 == 0 and every segment is float4-
+// aligned: persistent blocks keep W^T resident in LDS and stream 32-row tiles of dz and X
+// through LDS once (register prefetch of the next tile overlaps HBM with the MFMAs), computing
+// dX and the block's dW/db from the same staged tiles.  (An LDS-staged forward built the same
+// way measured no faster than the direct-fragment forward — 345 vs 325 us at N=1M, K=128, h=64,
+// both MFMA-issue bound at ~50 TF/s — so the forward keeps the direct kernel.)
 constexpr int FT = 32;  // rows per tile
 
-// [FT x K] tile of the concatenated segments -> xs (row stride ld), zero rows past n.
-__device__ __forceinline__ void stage_x_tile(const LinArgs& a, int64_t r0, float* xs, int ld) {
-  const int k4 = a.k_total >> 2;
-  for (int idx = threadIdx.x; idx < FT * k4; idx += 256) {
-    const int r = idx / k4, k = (idx - r * k4) * 4;
-    int s = 0;
-    while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
-    const int64_t row = r0 + r;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (row < a.n)
-      v = *reinterpret_cast<const float4*>(a.seg[s].x + row * a.seg[s].k + (k - a.seg[s].off));
-    *reinterpret_cast<float4*>(xs + r * ld + k) = v;
-  }
-}
-
-// Forward: waves = 2 row halves x 2 column halves of the [FT x h] output tile.
-template <int NT>
-__global__ void __launch_bounds__(256) k_linear_fwd_lds(const LinArgs a, int64_t n_tiles) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int K = a.k_total, h = a.h;
-  const int ldw = K + 4, ldx = K + 4, ldo = h + 4;
-  float* ws = smem;              // [h][ldw]
-  float* xs = ws + h * ldw;      // [FT][ldx]; reused as the output staging tile [FT][ldo]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int rt = wave & 1, ch = wave >> 1;     // row tile (16 rows), column half
-  constexpr int NTW = NT / 2 > 0 ? NT / 2 : 1;
-  const int t0 = (NT >= 2) ? ch * NTW : 0;
-  const bool active_cols = NT >= 2 || ch == 0;
-  for (int idx = threadIdx.x; idx < h * (K >> 2); idx += 256) {
-    const int j = idx / (K >> 2), k = (idx - j * (K >> 2)) * 4;
-    *reinterpret_cast<float4*>(ws + j * ldw + k) =
-        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
-  }
-  float bias[NTW];
+// Register prefetch of one [FT x K] tile (K <= 128 => at most 4 float4 per thread): issued
+// before the current tile's MFMAs so HBM latency overlaps compute, stored to LDS after.
+struct XPrefetch {
+  float4 v[4];
+  __device__ __forceinline__ void load(const LinArgs& a, int64_t r0) {
+    const int k4 = a.k_total >> 2;
 #pragma unroll
-  for (int t = 0; t < NTW; ++t) bias[t] = a.bias ? a.bias[(t0 + t) * 16 + i] : 0.f;
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int64_t r0 = tile * FT;
-    __syncthreads();
-    stage_x_tile(a, r0, xs, ldx);
-    __syncthreads();
-    f32x4 acc[NTW];
-#pragma unroll
-    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (active_cols) {
-      for (int kc = 0; kc < K; kc += 16) {
-        const float4 av = *reinterpret_cast<const float4*>(xs + (rt * 16 + i) * ldx + kc + 4 * g);
-#pragma unroll
-        for (int t = 0; t < NTW; ++t) {
-          const float4 bv =
-              *reinterpret_cast<const float4*>(ws + ((t0 + t) * 16 + i) * ldw + kc + 4 * g);
-          acc[t] = mfma4(av.x, bv.x, acc[t]);
-          acc[t] = mfma4(av.y, bv.y, acc[t]);
-          acc[t] = mfma4(av.z, bv.z, acc[t]);
-          acc[t] = mfma4(av.w, bv.w, acc[t]);
-        }
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < FT * k4) {
+        const int r = idx / k4, k = (idx - r * k4) * 4;
+        int s = 0;
+        while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
+        const int64_t row = r0 + r;
+        if (row < a.n)
+          v[q] = *reinterpret_cast<const float4*>(a.seg[s].x + row * a.seg[s].k +
+                                                  (k - a.seg[s].off));
       }
     }
-    __syncthreads();   // xs becomes the output staging tile
-    if (active_cols) {
+  }
+  __device__ __forceinline__ void store(const LinArgs& a, float* xs, int ld) const {
+    const int k4 = a.k_total >> 2;
 #pragma unroll
-      for (int t = 0; t < NTW; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[t][r] + bias[t];
-          if (a.relu) v = fmaxf(v, 0.f);
-          xs[(rt * 16 + 4 * g + r) * ldo + (t0 + t) * 16 + i] = v;
-        }
-    }
-    __syncthreads();
-    const int h4 = h >> 2;
-    for (int idx = threadIdx.x; idx < FT * h4; idx += 256) {
-      const int r = idx / h4, c = (idx - r * h4) * 4;
-      const int64_t row = r0 + r;
-      if (row < a.n)
-        *reinterpret_cast<float4*>(a.out + row * h + c) =
-            *reinterpret_cast<const float4*>(xs + r * ldo + c);
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      if (idx < FT * k4) {
+        const int r = idx / k4, k = (idx - r * k4) * 4;
+        *reinterpret_cast<float4*>(xs + r * ld + k) = v[q];
+      }
     }
   }
-}
+};
 
 // Fused backward: per 32-row tile, dz = dout * (out > 0) and X staged once; dX = dz @ W (W^T in
 // LDS) and the block's dW (+ db as the column K) accumulated in registers across its tiles,
@@ -415,26 +370,50 @@ __global__ void __launch_bounds__(256) k_linear_bwd_lds(const LinArgs a, int64_t
     for (int kt = 0; kt < 8; ++kt) acc[jt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
   float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int h4 = h >> 2;
+  // prefetch registers: dz (dout masked by out) <= 4 float4, X <= 4 float4 per thread
+  float4 zp[4];
+  XPrefetch pf;
+  auto load_dz = [&](int64_t r0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      zp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < FT * h4) {
+        const int r = idx / h4, c = (idx - r * h4) * 4;
+        const int64_t row = r0 + r;
+        if (row < a.n) {
+          float4 v = *reinterpret_cast<const float4*>(a.dout + row * h + c);
+          if (a.out_act) {
+            const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * h + c);
+            v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
+            v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
+          }
+          zp[q] = v;
+        }
+      }
+    }
+  };
+  load_dz((int64_t)blockIdx.x * FT);
+  pf.load(a, (int64_t)blockIdx.x * FT);
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t r0 = tile * FT;
     __syncthreads();
-    for (int idx = threadIdx.x; idx < FT * h4; idx += 256) {
-      const int r = idx / h4, c = (idx - r * h4) * 4;
-      const int64_t row = r0 + r;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row < a.n) {
-        v = *reinterpret_cast<const float4*>(a.dout + row * h + c);
-        if (a.out_act) {
-          const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * h + c);
-          v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
-          v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
-        }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = threadIdx.x + 256 * q;
+      if (idx < FT * h4) {
+        const int r = idx / h4, c = (idx - r * h4) * 4;
+        const float4 v = zp[q];
+        dbacc.x += v.x; dbacc.y += v.y; dbacc.z += v.z; dbacc.w += v.w;
+        *reinterpret_cast<float4*>(dz + r * ldz + c) = v;
       }
-      dbacc.x += v.x; dbacc.y += v.y; dbacc.z += v.z; dbacc.w += v.w;
-      *reinterpret_cast<float4*>(dz + r * ldz + c) = v;
     }
-    stage_x_tile(a, r0, xs, ldx);
+    pf.store(a, xs, ldx);
     __syncthreads();
+    if (tile + gridDim.x < n_tiles) {
+      load_dz((tile + gridDim.x) * FT);
+      pf.load(a, (tile + gridDim.x) * FT);
+    }
     if (DX) {   // dX tile [FT x K]: wave = row tile (wave & 1) x column half (wave >> 1)
       const int rt = wave & 1, half = wave >> 1;
       const int ct0 = half * (KT >> 1), nct = KT >> 1;
@@ -515,6 +494,8 @@ __global__ void __launch_bounds__(256) k_linear_bwd_lds(const LinArgs a, int64_t
 }
 
 static bool fast_path_ok(const LinArgs& a, bool vec) {
+  static const int off = getenv("HGNN_LIN_GENERAL") ? atoi(getenv("HGNN_LIN_GENERAL")) : 0;
+  if (off) return false;
   return vec && a.h % 16 == 0 && a.h <= 128 && a.k_total % 32 == 0 && a.k_total <= 128 &&
          (size_t)a.h * a.k_total * 4 <= 65536 && 256 % (a.h / 4) == 0;
 }
@@ -565,22 +546,6 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.bias = bias;
   a.out = out;
   a.relu = relu;
-  if (fast_path_ok(a, vec)) {
-    const int64_t n_tiles = cdiv(n_rows, FT);
-    const size_t lds = ((size_t)h * (a.k_total + 4) +
-                        std::max<size_t>((size_t)FT * (a.k_total + 4), (size_t)FT * (h + 4))) * 4;
-    const dim3 grid(fast_grid(n_tiles)), block(256);
-    switch (h / 16) {
-      case 1: hipLaunchKernelGGL(k_linear_fwd_lds<1>, grid, block, lds, stream, a, n_tiles); break;
-      case 2: hipLaunchKernelGGL(k_linear_fwd_lds<2>, grid, block, lds, stream, a, n_tiles); break;
-      case 4: hipLaunchKernelGGL(k_linear_fwd_lds<4>, grid, block, lds, stream, a, n_tiles); break;
-      case 6: hipLaunchKernelGGL(k_linear_fwd_lds<6>, grid, block, lds, stream, a, n_tiles); break;
-      case 8: hipLaunchKernelGGL(k_linear_fwd_lds<8>, grid, block, lds, stream, a, n_tiles); break;
-      default: goto general;
-    }
-    return check_launch("k_linear_fwd_lds");
-  }
-general:
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
   if (h <= 64) {
     const dim3 grid(gx, 1);

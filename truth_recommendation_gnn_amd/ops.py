@@ -307,7 +307,7 @@ def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tens
 
 class _EdgeBCELoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool):
+    def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int):
         U = _check_f32(U, "edge_bce_loss user_emb")
         P = _check_f32(P, "edge_bce_loss post_emb")
         dev = N.require_device(U, P, neg_u_order)
@@ -329,7 +329,7 @@ class _EdgeBCELoss(torch.autograd.Function):
         with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 2 + 2 + 4) + 8 * nu * d):
             N.check(lib.hgnn_edge_score_fwd(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                N.ptr(neg_u_order), N.ptr(to_post), E, N.ptr(c), N.ptr(dU), N.ptr(hpos),
+                N.ptr(neg_u_order), N.ptr(to_post), n_total, N.ptr(c), N.ptr(dU), N.ptr(hpos),
                 N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), N.ptr(part), N.ptr(loss),
                 N.ptr(err), s), "hgnn_edge_score_fwd")
         # negatives grouped by post (a fresh draw every step) -> weighted gather of U rows
@@ -355,23 +355,29 @@ class _EdgeBCELoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go):
         dU, dP = ctx.saved_tensors
-        return dU.mul_(go), dP.mul_(go), None, None, None, None
+        return dU.mul_(go), dP.mul_(go), None, None, None, None, None
 
 
 def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
-                  neg_p: torch.Tensor, pos_weights: torch.Tensor, neg_order: str = "edge",
-                  check: bool = True) -> torch.Tensor:
+                  neg_p: torch.Tensor, pos_weights: Optional[torch.Tensor],
+                  neg_order: str = "edge", check: bool = True,
+                  n_edges_total: Optional[int] = None,
+                  cscale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused HIP version of :func:`link_loss` (same value, same gradients).
 
     ``neg_order='edge'``: ``neg_p[e]`` is the negative of COO edge e (the reference's layout);
     ``'user'``: already in the user-grouped order (what :func:`sample_negatives` draws).
-    ``check`` costs one host sync (the reference syncs every step with ``loss.item()``)."""
+    ``check`` costs one host sync (the reference syncs every step with ``loss.item()``).
+    ``n_edges_total`` / ``cscale`` (= mean of ALL pos_weights) let a shard of the positive edges
+    produce its additive share of the global loss (parallel.py)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     if neg_p.shape[0] != csr.num_edges:
         raise ValueError("one negative per positive edge is required (train_gnn.py:272)")
     neg_u = negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
-    cscale = pos_weights.to(torch.float32).mean()
-    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check)
+    if cscale is None:
+        cscale = pos_weights.to(torch.float32).mean()
+    n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
+    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total)
 
 
 def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:
@@ -385,3 +391,76 @@ def sample_negatives(pos_edges: torch.Tensor, num_posts: int,
     directly in the user-grouped order: the draws are iid, so only their labels move."""
     return torch.randint(0, num_posts, (pos_edges.shape[1],), device=pos_edges.device,
                          generator=generator)
+
+
+# ----------------------------------------------------------------------------- composable ops
+# Differentiable single-kernel ops, used where a fused layer does not apply (the partitioned
+# multi-GPU path in parallel.py composes them around RCCL collectives).
+class _GatherMean(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_src, csr: RelationCSR):
+        ctx.csr = csr
+        return gather_mean(x_src, csr)
+
+    @staticmethod
+    def backward(ctx, g):
+        if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
+            return None, None
+        return scatter_mean_bwd(g.contiguous(), ctx.csr), None
+
+
+def mean_gather(x_src: torch.Tensor, csr: RelationCSR) -> torch.Tensor:
+    """Differentiable K1 (forward) / K2 (backward) mean aggregation."""
+    return _GatherMean.apply(x_src, csr)
+
+
+class _GatherWeighted(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_src, csr: RelationCSR, w_fwd, w_bwd):
+        x_src = _check_f32(x_src, "weighted_gather")
+        out = torch.empty(csr.n_dst, x_src.shape[1], dtype=torch.float32, device=x_src.device)
+        _gather(x_src, csr.fwd, None, csr_mean=False, out=out, accumulate=False, edge_w=w_fwd)
+        ctx.csr, ctx.w_bwd = csr, w_bwd
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
+            return None, None, None, None
+        csr = ctx.csr
+        out = torch.empty(csr.n_src, g.shape[1], dtype=torch.float32, device=g.device)
+        _gather(g.contiguous(), csr.bwd, None, csr_mean=False, out=out, accumulate=False,
+                edge_w=ctx.w_bwd)
+        return out, None, None, None
+
+
+def weighted_gather(x_src: torch.Tensor, csr: RelationCSR, w_fwd: torch.Tensor,
+                    w_bwd: torch.Tensor) -> torch.Tensor:
+    """``out[i] = sum_{p in row i} w_fwd[p] x_src[col[p]]`` (CSR order weights); backward walks
+    the CSC with ``w_bwd`` (CSC order) — the same edge weights, transposed."""
+    return _GatherWeighted.apply(x_src, csr, w_fwd, w_bwd)
+
+
+class _FusedLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, relu: bool, w, b, *segs):
+        segs = [_check_f32(s, "fused_linear") for s in segs]
+        y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(), relu)
+        ctx.relu, ctx.has_b = relu, b is not None
+        ctx.save_for_backward(w, y, *segs)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        w, y, *segs = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        dxs = [torch.empty_like(s) if need[3 + i] else None for i, s in enumerate(segs)]
+        dw, db = linear_bwd(segs, w, dy.contiguous(), y if ctx.relu else None, dxs, need[1],
+                            ctx.has_b and need[2])
+        return (None, dw, db, *dxs)
+
+
+def fused_linear(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.Tensor],
+                 relu: bool) -> torch.Tensor:
+    """Differentiable K3: ``act(sum_s segs[s] @ w[:, seg s]^T + b)``."""
+    return _FusedLinear.apply(relu, w, b, *segs)

@@ -1,0 +1,181 @@
+"""Multi-GPU hetero-SAGE: users sharded across ranks, posts replicated, RCCL all-reduce.
+
+One process per GPU (``torch.distributed``, backend ``nccl`` = RCCL over xGMI).  The user <-> post
+graph is partitioned by USER (contiguous id ranges, the 10x larger node type):
+
+* rank r owns users [lo_r, hi_r) and every engages edge whose user it owns, so
+  - the user-destination aggregation (``rev_engages``: post -> user, mean over the user's
+    in-edges) is complete on the owner — no exchange;
+  - the post-destination aggregation (``engages``: user -> post) is a per-rank PARTIAL sum over
+    the rank's edges, each edge pre-scaled by 1/deg_global(post) (K1 with per-edge weights), then
+    one RCCL all-reduce of the post-sized table gives every rank the exact mean;
+* post rows are replicated (their projection runs on every rank on identical data), user rows
+  never leave their owner;
+* backward: the all-reduce's adjoint is an all-reduce of the partial post gradients, then K2
+  (weights transposed) sends them to the owned users; parameter gradients are summed over ranks
+  with one flat all-reduce (the replicated post chain contributes per-rank partial gradients,
+  whose sum is the true gradient because every op on it is linear in its upstream gradient).
+* the link loss is sharded the same way: rank r scores the positive edges of its users against
+  the replicated post table; normalised by the GLOBAL edge count and mean(pos_weights), the
+  per-rank losses add up to the reference loss (``train_gnn.py:259-281``).
+
+Exchanged per step: 3 post-sized all-reduces (layer-1 and layer-2 post aggregates forward, the
+layer-2 post-aggregate gradient backward) + the weight gradients.  The compute ops are injected
+(``HipImpl`` here; the CPU gloo tests inject plain-torch ops to check the partitioning logic).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .graph import RelationCSR, relation_csr
+from .nn import HeteroSAGE, _fused_weights
+from .synth import ENGAGES, REV_ENGAGES
+
+RELATIONS = [(REV_ENGAGES, 1.0), (ENGAGES, 1.0)]
+
+
+@dataclasses.dataclass
+class DistEnv:
+    world: int = 1
+    rank: int = 0
+    group: Optional[object] = None
+
+    @classmethod
+    def from_torch(cls) -> "DistEnv":
+        if dist.is_available() and dist.is_initialized():
+            return cls(dist.get_world_size(), dist.get_rank())
+        return cls()
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+
+class _AllReduceSum(torch.autograd.Function):
+    """y = sum over ranks of x (replicated result); adjoint: the same all-reduce of gradients."""
+
+    @staticmethod
+    def forward(ctx, x, env: DistEnv):
+        ctx.env = env
+        return env.all_reduce_(x.contiguous().clone())
+
+    @staticmethod
+    def backward(ctx, g):
+        return ctx.env.all_reduce_(g.contiguous().clone()), None
+
+
+def all_reduce_sum(x: torch.Tensor, env: DistEnv) -> torch.Tensor:
+    return _AllReduceSum.apply(x, env)
+
+
+def user_range(n_users: int, world: int, rank: int) -> Tuple[int, int]:
+    m = -(-n_users // world)
+    lo = min(n_users, rank * m)
+    return lo, min(n_users, lo + m)
+
+
+class HipImpl:
+    """The MI355X kernels behind the partitioned step."""
+
+    def relation(self, edge_index, n_src, n_dst):
+        return relation_csr(edge_index, n_src, n_dst)   # cached: the loss finds the same one
+
+    def edge_weights_fwd(self, rel: RelationCSR, w_dst: torch.Tensor) -> torch.Tensor:
+        """w_dst[destination] per forward-CSR position (rows are destinations)."""
+        counts = (rel.fwd.rowptr[1:] - rel.fwd.rowptr[:-1]).long()
+        return torch.repeat_interleave(w_dst, counts).contiguous()
+
+    def edge_weights_bwd(self, rel: RelationCSR, w_dst: torch.Tensor) -> torch.Tensor:
+        """w_dst[destination] per CSC position (col holds the destination)."""
+        return w_dst[rel.bwd.col.long()].contiguous()
+
+    mean_gather = staticmethod(ops.mean_gather)
+    weighted_gather = staticmethod(ops.weighted_gather)
+    fused_linear = staticmethod(ops.fused_linear)
+
+    @staticmethod
+    def edge_bce_loss(U, P, pos, neg, n_total, cscale, neg_order="edge"):
+        return ops.edge_bce_loss(U, P, pos, neg, None, neg_order=neg_order, check=False,
+                                 n_edges_total=n_total, cscale=cscale)
+
+
+class UserShard:
+    """Static per-rank structures for the engages relation (and its reverse)."""
+
+    def __init__(self, engage_edges: torch.Tensor, n_users: int, n_posts: int, env: DistEnv,
+                 impl=None, pos_weights: Optional[torch.Tensor] = None):
+        impl = impl or HipImpl()
+        self.env, self.impl = env, impl
+        self.n_users, self.n_posts = n_users, n_posts
+        self.lo, self.hi = user_range(n_users, env.world, env.rank)
+        u, p = engage_edges[0], engage_edges[1]
+        self.mask = (u >= self.lo) & (u < self.hi)
+        self.pos_local = torch.stack([u[self.mask] - self.lo, p[self.mask]]).contiguous()
+        self.rev_local = self.pos_local.flip(0).contiguous()
+        self.n_own = self.hi - self.lo
+        self.num_edges_global = int(engage_edges.shape[1])
+        deg = torch.bincount(self.pos_local[1], minlength=n_posts).to(torch.float32)
+        env.all_reduce_(deg)
+        self.inv_deg_post = torch.where(deg > 0, 1.0 / deg.clamp(min=1.0), torch.zeros_like(deg))
+        self.rel_eng = impl.relation(self.pos_local, self.n_own, n_posts)
+        self.rel_rev = impl.relation(self.rev_local, n_posts, self.n_own)
+        self.w_eng_fwd = impl.edge_weights_fwd(self.rel_eng, self.inv_deg_post)
+        self.w_eng_bwd = impl.edge_weights_bwd(self.rel_eng, self.inv_deg_post)
+        self.cscale = None
+        if pos_weights is not None:   # global mean of the interaction weights (static)
+            s = torch.stack([pos_weights[self.mask].to(torch.float64).sum(),
+                             torch.tensor(float(self.mask.sum()), dtype=torch.float64,
+                                          device=pos_weights.device)])
+            env.all_reduce_(s)
+            self.cscale = (s[0] / s[1]).to(torch.float32)
+
+    def local_edges_of(self, per_edge: torch.Tensor) -> torch.Tensor:
+        """Slice a per-global-edge tensor (e.g. injected negatives) to this rank's edges."""
+        return per_edge[self.mask]
+
+    def forward(self, model: HeteroSAGE, x_user_own: torch.Tensor, x_post: torch.Tensor):
+        """Partitioned forward of ``model``; returns (owned user embeddings, all post
+        embeddings)."""
+        impl, env = self.impl, self.env
+        h_u, h_p = x_user_own, x_post
+        nu = "__".join(REV_ENGAGES)
+        np_ = "__".join(ENGAGES)
+        wts = dict(model.relations)
+        for convs in model.layers:
+            shapes = {"user": h_u, "post": h_p}
+            Wu, bu = _fused_weights(convs, [(nu, REV_ENGAGES, wts[REV_ENGAGES])], shapes)
+            Wp, bp = _fused_weights(convs, [(np_, ENGAGES, wts[ENGAGES])], shapes)
+            s_post = impl.weighted_gather(h_u, self.rel_eng, self.w_eng_fwd, self.w_eng_bwd)
+            a_user = impl.mean_gather(h_p, self.rel_rev)
+            h_u_next = impl.fused_linear([a_user, h_u], Wu, bu, True)
+            a_post = all_reduce_sum(s_post, env)
+            h_p_next = impl.fused_linear([a_post, h_p], Wp, bp, True)
+            h_u, h_p = h_u_next, h_p_next
+        return h_u, h_p
+
+    def loss(self, h_u_own, h_p, neg_local, neg_order="edge"):
+        """This rank's additive share of the reference loss."""
+        if self.cscale is None:
+            raise ValueError("UserShard built without pos_weights")
+        return self.impl.edge_bce_loss(h_u_own, h_p, self.pos_local, neg_local,
+                                       self.num_edges_global, self.cscale, neg_order=neg_order)
+
+
+def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
+    """Sum parameter gradients over ranks with one flat all-reduce."""
+    if env.world == 1:
+        return
+    params = [p for p in model.parameters() if p.grad is not None]
+    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    env.all_reduce_(flat)
+    o = 0
+    for p in params:
+        n = p.numel()
+        p.grad.copy_(flat[o:o + n].view_as(p))
+        o += n

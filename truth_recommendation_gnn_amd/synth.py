@@ -57,6 +57,17 @@ CONFIGS: Dict[str, GraphConfig] = {
 }
 
 
+def replicated(name: str, world: int) -> GraphConfig:
+    """Weak scaling: ``world`` copies' worth of nodes and edges in one global graph."""
+    c = CONFIGS[name]
+    if world == 1:
+        return c
+    return dataclasses.replace(c, name=f"{name}x{world}gpu", num_users=c.num_users * world,
+                               num_posts=c.num_posts * world, num_engages=c.num_engages * world,
+                               num_social=c.num_social * world,
+                               num_post_post=c.num_post_post * world)
+
+
 def scaled(name: str, factor: float) -> GraphConfig:
     """``name`` with every node and edge count multiplied by ``factor`` (>=1 node each)."""
     c = CONFIGS[name]
@@ -108,17 +119,21 @@ def _features_np(rng: np.random.Generator, n: int, d: int) -> np.ndarray:
     return (x / np.maximum(nrm, 1e-12)).astype(np.float32)
 
 
-def make_graph(cfg: GraphConfig | str, device: str | torch.device = "cpu") -> SynthGraph:
+def make_graph(cfg: GraphConfig | str, device: str | torch.device = "cpu",
+               device_gen: Optional[bool] = None) -> SynthGraph:
     """Build the seeded graph.  CPU generation is numpy PCG64 (bit-reproducible everywhere).
 
-    With a CUDA ``device`` and more than 50M edges, generation runs on the GPU with a seeded
-    torch generator (reproducible on the same device type, not equal to the numpy stream);
-    only benches use that, parity tests stay on the numpy path.
+    With a CUDA ``device`` and more than 50M edges (or ``device_gen=True``), generation runs on
+    the GPU with a seeded torch generator (reproducible on the same device type — every rank of a
+    multi-GPU run builds the identical global graph — not equal to the numpy stream); only
+    benches use that, parity tests stay on the numpy path.
     """
     if isinstance(cfg, str):
         cfg = CONFIGS[cfg]
     dev = torch.device(device)
     big = dev.type == "cuda" and (cfg.num_engages + cfg.num_social) > 50_000_000
+    if device_gen is not None:
+        big = device_gen and dev.type == "cuda"
     if big:
         return _make_graph_torch(cfg, dev)
     U, P = cfg.num_users, cfg.num_posts
