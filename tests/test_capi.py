@@ -62,6 +62,8 @@ def test_module_surface_matches_reference_state_dict_keys():
     fresh = WeightedRGCN(hidden_dim=64)
     fresh.load_state_dict(m.state_dict())
     assert fresh.msg_direct.lin_l.weight.shape == (64, 64)
+    fresh.msg_direct.materialize(64, 64)       # after a load the lazy layer knows its width
+    assert fresh.msg_direct.lin_l.in_features == 64
 
 
 def test_heterodata_lite():

@@ -348,3 +348,69 @@ def test_device_generated_graph_schema():
     assert torch.equal(g.edge_index_dict[synth.REV_ENGAGES], e.flip(0))
     g2 = synth.make_graph(cfg, device=DEV, device_gen=True)
     assert torch.equal(g2.edge_index_dict[synth.ENGAGES], e)      # same on every rank
+
+
+# ----------------------------------------------------------------------------- drop-in surface
+def test_reference_structured_model_over_our_sageconv_matches_golden():
+    """The reference's WeightedRGCN structure (train_gnn.py:147-200: three SAGEConv calls, torch
+    weighted sum + ReLU) with only the import switched."""
+    import torch.nn.functional as F
+
+    class RefStructured(torch.nn.Module):
+        def __init__(self, hidden_dim=64):
+            super().__init__()
+            self.msg_direct = SAGEConv((-1, -1), hidden_dim)
+            self.msg_social = SAGEConv((-1, -1), hidden_dim)
+            self.post_update = SAGEConv((-1, -1), hidden_dim)
+            self.w_direct, self.w_social = 1.0, 0.75
+
+        def forward(self, x_dict, edge_index_dict):
+            u, p = x_dict["user"], x_dict["post"]
+            md = self.msg_direct((p, u), edge_index_dict[("post", "rev_engages", "user")])
+            ms = self.msg_social((u, u), edge_index_dict[("user", "social", "user")])
+            uo = F.relu(self.w_direct * md + self.w_social * ms)
+            po = F.relu(self.post_update((u, p), edge_index_dict[("user", "engages", "post")]))
+            return {"user": uo, "post": po}
+
+    z, x, e, params = _fixture_cfg1()
+    model = RefStructured().to(DEV)
+    model.load_state_dict(params)
+    out = model(x, e)
+    close(out["user"], z["out_user"])
+    close(out["post"], z["out_post"])
+    loss = ops.link_loss(out["user"], out["post"], e[synth.ENGAGES],
+                         torch.from_numpy(z["neg_p"]).to(DEV),
+                         torch.from_numpy(z["pos_weights"]).to(DEV))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_integration_ctypes_snippet():
+    """raw C ABI through ctypes, no torch types across the boundary."""
+    import ctypes
+    from truth_recommendation_gnn_amd import _native as Nn
+    lib = ctypes.CDLL(str(Nn.LIB_PATH))
+    P, I, L, S = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t
+    lib.hgnn_coo_to_csr_ws_bytes.restype = S
+    lib.hgnn_coo_to_csr.argtypes = [P, P, L, L, L, P, P, P, P, P, S, P]
+    lib.hgnn_gather_mean_fwd.argtypes = [P, L, I, P, P, L, P, P, L, L, I, P, P, P]
+    p = lambda t: P(t.data_ptr()) if t is not None else None
+    stream = P(torch.cuda.current_stream().cuda_stream)
+    g = synth.make_graph("cfg1")
+    ei = g.edge_index_dict[synth.REV_ENGAGES].to(DEV)
+    src, dst = ei[0].contiguous(), ei[1].contiguous()
+    x_src, n_dst = g.x_dict["post"].to(DEV), g.num_users
+    E = src.numel()
+    rowptr = torch.empty(n_dst + 1, dtype=torch.int32, device=DEV)
+    col = torch.empty(E, dtype=torch.int32, device=DEV)
+    perm = torch.empty(E, dtype=torch.int32, device=DEV)
+    bad = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ws = torch.empty(lib.hgnn_coo_to_csr_ws_bytes(E, n_dst), dtype=torch.uint8, device=DEV)
+    assert lib.hgnn_coo_to_csr(p(dst), p(src), E, n_dst, x_src.shape[0], p(rowptr), p(col),
+                               p(perm), p(bad), p(ws), ws.numel(), stream) == 0
+    aggr = torch.empty(n_dst, x_src.shape[1], device=DEV)
+    assert lib.hgnn_gather_mean_fwd(p(x_src), x_src.shape[0], x_src.shape[1], p(rowptr), p(col),
+                                    n_dst, None, None, 0, 0, 2**30, None, p(aggr), stream) == 0
+    close(aggr, sage_ref.mean_aggregate(g.x_dict["post"], g.edge_index_dict[synth.REV_ENGAGES],
+                                        n_dst))

@@ -134,4 +134,4 @@ def test_synth_schema_and_determinism():
     assert torch.allclose(n, torch.ones_like(n), atol=1e-5)
     c = synth.make_graph(synth.scaled("cfg2", 0.001))
     deg = torch.bincount(c.edge_index_dict[synth.ENGAGES][1], minlength=c.num_posts)
-    assert int(deg.max()) > 20 * float(deg.float().mean()) ** 0 and int(deg.sum()) == 20000
+    assert int(deg.max()) > 5 * float(deg.float().mean()) and int(deg.sum()) == 20000

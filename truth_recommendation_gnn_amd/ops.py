@@ -103,7 +103,8 @@ def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
     flags = (N.HGNN_MEAN if csr_mean else 0) | (N.HGNN_ACCUMULATE if accumulate else 0)
     d = int(out.shape[1])
     weighted = edge_w is not None or col_w is not None
-    name = f"gather_{'fwd' if csr_mean else 'bwd'}_d{d}"
+    kind = "fwd" if csr_mean else "bwd"
+    name = f"gather_{kind}[{grouped.n_rows}<-{x.shape[0]}]x{d}"   # [dst rows <- src rows] x d
     with _timed(name, gather_bytes(int(grouped.col.numel()), grouped.n_rows, d, weighted)):
         N.check(N.lib().hgnn_gather_reduce(
             N.ptr(x), x.shape[0], d, N.ptr(grouped.rowptr), N.ptr(grouped.col),
