@@ -1,4 +1,8 @@
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc -le 1 ] || exit $rc
-timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --same-device --no-cpu-baseline > gpurun_out/bench_n2_rehearsal.log 2>&1; rc=$?; echo "n2 rehearsal rc=$rc"; tail -2 gpurun_out/bench_n2_rehearsal.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log
+export TMPDIR=/tmp
+timeout -k 10 300 python -m pytest tests -m gpu -x -q -k "linear or golden" > gpurun_out/t_v4.log 2>&1 || { tail -30 gpurun_out/t_v4.log; exit 1; }
+tail -1 gpurun_out/t_v4.log
+timeout -k 10 300 python scripts/microbench.py > gpurun_out/mb_v4.log 2>&1 || exit 1
+grep K3 gpurun_out/mb_v4.log
+HGNN_LIN_V3=1 timeout -k 10 300 python scripts/microbench.py > gpurun_out/mb_v3.log 2>&1 || exit 1
+grep "K3 bwd" gpurun_out/mb_v3.log

@@ -108,7 +108,8 @@ def test_gather_is_deterministic_bitwise():
 # ----------------------------------------------------------------------------- K3 / K4
 @pytest.mark.parametrize("ks,h", [([64], 64), ([64, 64], 64), ([64, 64, 64], 64),
                                   ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100),
-                                  ([64], 128), ([32], 16), ([64, 32], 32)])
+                                  ([64], 128), ([32], 16), ([64, 32], 32), ([64, 64], 128),
+                                  ([16, 48, 64], 64), ([32, 96], 64), ([48, 16], 128)])
 @pytest.mark.parametrize("n", [1, 37, 1000, 20000])
 def test_linear_fwd_bwd_matches_torch(ks, h, n):
     gen = torch.Generator().manual_seed(n + h)
@@ -116,19 +117,63 @@ def test_linear_fwd_bwd_matches_torch(ks, h, n):
     w = torch.randn(h, sum(ks), generator=gen) * 0.2
     b = torch.randn(h, generator=gen)
     dout = torch.randn(n, h, generator=gen)
-    ref_in = [s.clone().requires_grad_() for s in segs]
-    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
-    ref = torch.relu(torch.cat(ref_in, 1) @ wr.T + br)
-    ref.backward(dout)
     dsegs = [s.to(DEV) for s in segs]
     out = ops.linear_fwd(dsegs, w.to(DEV), b.to(DEV), relu=True)
-    close(out, ref)
+    close(out, torch.relu(torch.cat(segs, 1) @ w.T + b))
     dxs = [torch.empty_like(s) for s in dsegs]
     dw, db = ops.linear_bwd(dsegs, w.to(DEV), dout.to(DEV), out, dxs, True, True)
-    for gx, r in zip(dxs, ref_in):
-        close(gx, r.grad)
-    close(dw, wr.grad)
-    close(db, br.grad)
+    ref_dx, ref_dw, ref_db = _linear_bwd_ref(segs, w, dout, out)
+    for gx, r in zip(dxs, ref_dx):
+        close(gx, r)
+    close(dw, ref_dw)
+    close(db, ref_db)
+
+
+def _linear_bwd_ref(segs, w, dout, out_act):
+    """float64 backward of relu(X W^T + b) given the kernel's forward output: the ReLU mask is
+    taken from ``out_act`` itself, since a pre-activation within rounding of 0 may legitimately
+    land on either side in fp32 and flip one row's dX by dout*W."""
+    dz = dout.double()
+    if out_act is not None:
+        dz = dz * (out_act.detach().cpu() > 0)
+    x = torch.cat(segs, 1).double()
+    dx = dz @ w.double()
+    return list(dx.split([s.shape[1] for s in segs], 1)), dz.T @ x, dz.sum(0)
+
+
+@pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 64), ([64, 64], 128), ([16, 48], 128)])
+@pytest.mark.parametrize("mode", ["no_relu", "dx_subset", "wgrad_only", "db_only"])
+def test_linear_bwd_variants(ks, h, mode):
+    """The compile-time-shape K3 backward (two-role, double-buffered tiles) under every operand
+    combination the layers use: no activation mask, dX for a subset of segments, dW/db only."""
+    n = 64 * 300 + 17
+    gen = torch.Generator().manual_seed(7 * h + len(ks))
+    segs = [torch.randn(n, k, generator=gen) for k in ks]
+    w = torch.randn(h, sum(ks), generator=gen) * 0.2
+    b = torch.randn(h, generator=gen)
+    dout = torch.randn(n, h, generator=gen)
+    relu = mode != "no_relu"
+    z = torch.cat(segs, 1) @ w.T + b
+    dsegs = [s.to(DEV) for s in segs]
+    out = ops.linear_fwd(dsegs, w.to(DEV), b.to(DEV), relu=relu)
+    close(out, torch.relu(z) if relu else z)
+    ref_dx, ref_dw, ref_db = _linear_bwd_ref(segs, w, dout, out if relu else None)
+    dxs = [torch.full_like(s, 7.0) for s in dsegs]
+    if mode in ("wgrad_only", "db_only"):
+        dxs = [None] * len(ks)
+    elif mode == "dx_subset":
+        dxs[0] = None
+    need_w = mode != "db_only"
+    dw, db = ops.linear_bwd(dsegs, w.to(DEV), dout.to(DEV), out if relu else None, dxs,
+                            need_w, True)
+    for gx, r in zip(dxs, ref_dx):
+        if gx is not None:
+            close(gx, r)
+    if need_w:
+        close(dw, ref_dw)
+    else:
+        assert dw is None
+    close(db, ref_db)
 
 
 # ----------------------------------------------------------------------------- models

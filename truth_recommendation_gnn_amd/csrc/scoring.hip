@@ -237,6 +237,18 @@ static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream)
     case 4: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 4>), g, b, 0, stream, a); break;
     case 7: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 7>), g, b, 0, stream, a); break;
     case 8: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, 2, 0>), g, b, 0, stream, a); break;
+    case 10:
+      if (LPR == 16 && W == 4) {
+        hipLaunchKernelGGL((k_edge_score<8, 2, 4, 1, 0>), g, b, 0, stream, a);
+        break;
+      }
+      [[fallthrough]];
+    case 11:
+      if (LPR == 16 && W == 4) {
+        hipLaunchKernelGGL((k_edge_score<4, 4, 4, 1, 0>), g, b, 0, stream, a);
+        break;
+      }
+      [[fallthrough]];
     default: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), g, b, 0, stream, a);
   }
   return check_launch("k_edge_score");

@@ -15,6 +15,7 @@ gradient sums the reference's autograd would do with separate add kernels happen
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -179,20 +180,62 @@ class LayerSpec:
     groups: Tuple[DstGroup, ...]
 
 
+class _Lanes:
+    """Two in-order HIP streams (the caller's current stream + one side stream per device) for
+    independent kernel chains.  Every tensor that escapes a side-stream chain is allocated on the
+    main stream beforehand or record_stream()'d for it, and the main stream joins the side
+    stream before returning, so the caching allocator never hands out memory still in use.
+    Off by default: on cfg2 every overlapped pair slowed each other by as much as the overlap
+    saved (10.55 vs 10.51 ms/step; the gathers already saturate the memory system).
+    HGNN_STREAMS=1 turns it on."""
+
+    _side: Dict[torch.device, torch.cuda.Stream] = {}
+    enabled = os.environ.get("HGNN_STREAMS", "0") == "1"
+
+    def __init__(self, dev: torch.device, n_chains: int):
+        self.main = torch.cuda.current_stream(dev)
+        self.side = None
+        if self.enabled and n_chains > 1:
+            self.side = _Lanes._side.get(dev)
+            if self.side is None:
+                self.side = _Lanes._side[dev] = torch.cuda.Stream(dev)
+            self.side.wait_stream(self.main)
+
+    def stream(self, i: int):
+        return self.side if (self.side is not None and i % 2 == 1) else self.main
+
+    def escape(self, i: int, *tensors):
+        if self.side is not None and i % 2 == 1:
+            for t in tensors:
+                if t is not None:
+                    t.record_stream(self.main)
+
+    def join(self):
+        if self.side is not None:
+            self.main.wait_stream(self.side)
+
+
 class _HeteroLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec: LayerSpec, *flat):
         nt = len(spec.types)
         xs = dict(zip(spec.types, flat[:nt]))
         wb = flat[nt:]
-        outs, aggrs_all = [], []
-        for gi, g in enumerate(spec.groups):
+        ng = len(spec.groups)
+        outs, aggrs_by_g = [None] * ng, [None] * ng
+        dev = flat[0].device
+        lanes = _Lanes(dev, ng)
+        for gi, g in enumerate(spec.groups):   # destination types are independent chains
             w, b = wb[2 * gi], wb[2 * gi + 1]
-            aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
-            segs = aggrs + ([xs[g.dst]] if g.root else [])
-            y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(), g.relu)
-            outs.append(y)
-            aggrs_all.extend(aggrs)
+            with torch.cuda.stream(lanes.stream(gi)):
+                aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
+                segs = aggrs + ([xs[g.dst]] if g.root else [])
+                y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
+                               g.relu)
+            lanes.escape(gi, y, *aggrs)
+            outs[gi], aggrs_by_g[gi] = y, aggrs
+        lanes.join()
+        aggrs_all = [a for aggrs in aggrs_by_g for a in aggrs]
         ctx.spec = spec
         ctx.has_b = [b is not None for b in wb[1::2]]
         ctx.save_for_backward(*flat[:nt], *[t for t in wb if t is not None], *aggrs_all, *outs)
@@ -219,7 +262,10 @@ class _HeteroLayer(torch.autograd.Function):
         need_x = dict(zip(spec.types, need[:nt]))
         gx: Dict[str, Optional[torch.Tensor]] = {t: None for t in spec.types}
         gwb: List[Optional[torch.Tensor]] = [None] * (2 * ng)
-        pending = []   # (src type, dA, csr) for K2 after every root gradient is written
+        pending: Dict[str, list] = {}   # target type -> [(dA, csr)] for K2, after the roots
+        # phase 1: every destination type's K3 backward (independent chains); all outputs
+        # allocated here on the main stream
+        jobs = []
         ai = 0
         for gi, g in enumerate(spec.groups):
             aggrs = aggrs_all[ai:ai + len(g.rels)]
@@ -229,13 +275,12 @@ class _HeteroLayer(torch.autograd.Function):
             need_w, need_b = need[nt + 2 * gi], (b is not None and need[nt + 2 * gi + 1])
             if dout is None:
                 continue
-            dout = dout.contiguous()
             dxs: List[Optional[torch.Tensor]] = []
             for (src, csr), a in zip(g.rels, aggrs):
                 if need_x[src] and csr.num_edges > 0:
                     dA = torch.empty_like(a)
                     dxs.append(dA)
-                    pending.append((src, dA, csr))
+                    pending.setdefault(src, []).append((dA, csr))
                 else:
                     dxs.append(None)
             segs = list(aggrs)
@@ -246,13 +291,25 @@ class _HeteroLayer(torch.autograd.Function):
                     dxs.append(gx[g.dst])
                 else:
                     dxs.append(None)
-            dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w, need_b)
+            jobs.append((gi, g, segs, w, dout.contiguous(), dxs, need_w, need_b))
+        lanes = _Lanes(saved[0].device, len(jobs))
+        for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
+            with torch.cuda.stream(lanes.stream(li)):
+                dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w,
+                                    need_b)
+            lanes.escape(li, dw, db)
             gwb[2 * gi], gwb[2 * gi + 1] = dw, db
-        for src, dA, csr in pending:
-            if gx[src] is None:
-                gx[src] = scatter_mean_bwd(dA, csr)
-            else:
-                scatter_mean_bwd(dA, csr, out=gx[src])
+        lanes.join()
+        # phase 2: K2 per target type (different targets are independent chains)
+        for t in pending:
+            if gx[t] is None:
+                gx[t] = torch.zeros_like(xs[t])
+        lanes = _Lanes(saved[0].device, len(pending))
+        for li, (t, items) in enumerate(pending.items()):
+            with torch.cuda.stream(lanes.stream(li)):
+                for dA, csr in items:
+                    scatter_mean_bwd(dA, csr, out=gx[t])
+        lanes.join()
         return (None, *[gx[t] for t in spec.types], *gwb)
 
 
@@ -333,18 +390,23 @@ class _EdgeBCELoss(torch.autograd.Function):
                 N.ptr(neg_u_order), N.ptr(to_post), n_total, N.ptr(c), N.ptr(dU), N.ptr(hpos),
                 N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), N.ptr(part), N.ptr(loss),
                 N.ptr(err), s), "hgnn_edge_score_fwd")
-        # negatives grouped by post (a fresh draw every step) -> weighted gather of U rows
+        # dP = positives (post-grouped weighted gather of U rows, side stream) + negatives
+        # (fresh draw every step: sort by post, then weighted gather, main stream) — the sort is
+        # LDS/latency bound and overlaps the HBM-bound positive gather
         rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
         nu_s = torch.empty(E, dtype=torch.int32, device=dev)
         nw_s = torch.empty(E, dtype=torch.float32, device=dev)
+        dP = torch.empty_like(P)
+        lanes = _Lanes(dev, 2)
+        with torch.cuda.stream(lanes.stream(1)):
+            _gather(U, pf, None, csr_mean=False, out=dP, accumulate=False, edge_w=hpos)
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
         with _timed("sort_negatives", 4 * E * 6 * 2):
             N.check(lib.hgnn_sort_pairs_i32(
                 N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), E, np_, N.ptr(rowptr_n),
-                N.ptr(nu_s), N.ptr(nw_s), N.ptr(err[1:]), N.ptr(ws), ws.numel(), s),
-                "hgnn_sort_pairs_i32")
-        dP = torch.empty_like(P)
-        _gather(U, pf, None, csr_mean=False, out=dP, accumulate=False, edge_w=hpos)
+                N.ptr(nu_s), N.ptr(nw_s), N.ptr(err[1:]), N.ptr(ws), ws.numel(),
+                N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
+        lanes.join()
         from .graph import GroupedEdges, Plan
         negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
         _gather(U, negs, None, csr_mean=False, out=dP, accumulate=True, edge_w=nw_s)
