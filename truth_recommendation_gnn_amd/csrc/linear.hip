@@ -344,22 +344,34 @@ __global__ void __launch_bounds__(256) k_linear_wgrad(const LinArgs a) {
 }
 
 // dw[j][k] = sum_b slab[b][j][k] (k < K), db[j] = sum_b slab[b][j][K]; fixed b order.
-__global__ void __launch_bounds__(256) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
-                                                      int32_t kext, float* dw, float* db) {
-  __shared__ float part[4][64];
+__global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
+                                                       int32_t kext, float* dw, float* db) {
+  // 64 outputs per block (lanes), 16 waves each sum a contiguous range of slabs with 4
+  // independent accumulators, then wave 0 adds the 16 partials in order: a fixed summation
+  // order for a given nb (deterministic), and enough loads in flight to stream the slabs
+  __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + lane;
   const int64_t total = (int64_t)h * kext;
-  const int64_t per = cdiv(nb, 4);
-  float s = 0.f;
+  const int64_t per = cdiv(nb, 16);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (e < total) {
-    const int64_t b0 = wave * per, b1 = min<int64_t>(b0 + per, nb);
-    for (int64_t b = b0; b < b1; ++b) s += slab[b * total + e];
+    const int64_t b1 = min<int64_t>((wave + 1) * per, nb);
+    int64_t b = wave * per;
+    for (; b + 4 <= b1; b += 4) {
+      s0 += slab[b * total + e];
+      s1 += slab[(b + 1) * total + e];
+      s2 += slab[(b + 2) * total + e];
+      s3 += slab[(b + 3) * total + e];
+    }
+    for (; b < b1; ++b) s0 += slab[b * total + e];
   }
-  part[wave][lane] = s;
+  part[wave][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (wave == 0 && e < total) {
-    const float v = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) v += part[w][lane];
     const int j = (int)(e / kext), k = (int)(e % kext);
     if (k < kext - 1) { if (dw) dw[(int64_t)j * (kext - 1) + k] = v; }
     else if (db) db[j] = v;
@@ -647,6 +659,77 @@ __global__ void __launch_bounds__(256) k_linear_fwd_v3(const LinArgs a, const Ch
         *reinterpret_cast<float4*>(a.out + row * H + t * 16 + 4 * g) = v;
       }
     }
+  }
+}
+
+// Forward v4: persistent.  W is staged into LDS once per block; then each of the 8 waves streams
+// its own 16-row tiles (no further barriers), with the next tile's A fragments in flight during
+// the current tile's MFMAs.  Output tiles are computed transposed (out^T = W X^T) so every lane
+// stores one float4 per 16 output columns.
+template <int H, int K>
+__global__ void __launch_bounds__(512, (H <= 64 ? 4 : 3)) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
+                                                       int64_t n_tiles) {
+  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
+  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
+  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
+    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
+    *reinterpret_cast<float4*>(ws + j * LDW + k) =
+        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  auto load = [&](int64_t t, float4 (&v)[KC]) {
+    const int64_t row = t * 16 + i;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+      v[c] = row < a.n ? *reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] +
+                                                          tab.col[c] + 4 * g)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  float4 av[KC], an[KC];
+  if (t < n_tiles) load(t, av);
+  __syncthreads();
+  const int wl0 = i * LDW + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    if (t + nw < n_tiles) load(t + nw, an);
+    // opaque offset: keeps the loop-invariant W fragments as per-tile LDS reads instead of letting
+    // the compiler hoist all K*H/64 of them into VGPRs (measured 195 vs 204 us at N=1M, K=128, H=64,
+    // and no spill at H=128)
+    int wo = wl0;
+    asm volatile("" : "+v"(wo));
+    const float* wl = ws + wo;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        const float4 bv = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + c * 16);
+        acc[tt] = mfma4(bv.x, av[c].x, acc[tt]);
+        acc[tt] = mfma4(bv.y, av[c].y, acc[tt]);
+        acc[tt] = mfma4(bv.z, av[c].z, acc[tt]);
+        acc[tt] = mfma4(bv.w, av[c].w, acc[tt]);
+      }
+    const int64_t row = t * 16 + i;
+    if (row < a.n) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        // bias re-read per tile (L1-resident) rather than held in 4*NT VGPRs for the whole loop
+        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = make_float4(acc[tt][0] + bb.x, acc[tt][1] + bb.y, acc[tt][2] + bb.z,
+                               acc[tt][3] + bb.w);
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < KC; ++c) av[c] = an[c];
   }
 }
 
@@ -1069,6 +1152,24 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.out = out;
   a.relu = relu;
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
+  if (v3_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
+    const ChunkTab tab = chunk_table(a);
+    const int64_t n_tiles = cdiv(n_rows, 16);
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) /
+                                             ((size_t)h * (a.k_total + 8) * 4)));
+    const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
+                                                                      256 * per_cu))),
+        block(512);
+    if (h == 64 && a.k_total == 128)
+      hipLaunchKernelGGL((k_linear_fwd_v4<64, 128>), grid, block, 0, stream, a, tab, n_tiles);
+    else if (h == 64)
+      hipLaunchKernelGGL((k_linear_fwd_v4<64, 64>), grid, block, 0, stream, a, tab, n_tiles);
+    else if (a.k_total == 128)
+      hipLaunchKernelGGL((k_linear_fwd_v4<128, 128>), grid, block, 0, stream, a, tab, n_tiles);
+    else
+      hipLaunchKernelGGL((k_linear_fwd_v4<128, 64>), grid, block, 0, stream, a, tab, n_tiles);
+    return check_launch("k_linear_fwd_v4");
+  }
   if (v3_ok(a, vec)) {
     const ChunkTab tab = chunk_table(a);
     const dim3 grid(gx), block(256);
@@ -1177,7 +1278,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
 #undef HGNN_BWD4
     if (int rc = check_launch("k_linear_bwd_v4")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
                        a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
     return check_launch("k_wgrad_reduce");
   }
@@ -1202,7 +1303,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
 #undef HGNN_BWD3
     if (int rc = check_launch("k_linear_bwd_v3")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
                        a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
     return check_launch("k_wgrad_reduce");
   }
@@ -1229,7 +1330,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
 #undef HGNN_BWD_LDS
     if (int rc = check_launch("k_linear_bwd_lds")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
                        a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
     return check_launch("k_wgrad_reduce");
   }
@@ -1251,7 +1352,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     else hipLaunchKernelGGL(k_linear_wgrad<false>, grid, dim3(256), 0, stream, a);
     if (int rc = check_launch("k_linear_wgrad")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(256), 0, stream,
+    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
                        a.slab, gx, h, a.k_total + 1, dw, db);
     if (int rc = check_launch("k_wgrad_reduce")) return rc;
   }

@@ -16,7 +16,6 @@
 // grouped CSR, negatives over the (n_e)-sorted list (hgnn_sort_pairs_i32).  Deterministic.
 #include "hgnn_common.h"
 
-#include <stdlib.h>
 
 namespace hgnn {
 
@@ -50,8 +49,23 @@ __device__ __forceinline__ float sigmoid_t(float x, float t) {
   const float r = __builtin_amdgcn_rcpf(1.f + t);
   return x >= 0.f ? r : t * r;
 }
-__device__ __forceinline__ float softplus(float x) {
-  return fmaxf(x, 0.f) + __logf(1.f + exp_neg_abs(x));
+
+// Sum over the LPR lanes of a slot, result in every lane of the slot.  Within a 16-lane DPP row
+// the butterfly runs on DPP source modifiers (quad_perm xor 1 / xor 2, row_half_mirror,
+// row_mirror) fused into the adds: no LDS-pipe ds_bpermute.  Wider slots finish with shuffles.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int LPR>
+__device__ __forceinline__ float slot_sum(float s) {
+  if constexpr (LPR >= 2) s += dpp_mov<0xB1>(s);    // quad_perm [1,0,3,2]
+  if constexpr (LPR >= 4) s += dpp_mov<0x4E>(s);    // quad_perm [2,3,0,1]
+  if constexpr (LPR >= 8) s += dpp_mov<0x141>(s);   // row_half_mirror
+  if constexpr (LPR >= 16) s += dpp_mov<0x140>(s);  // row_mirror
+  if constexpr (LPR >= 32) s += __shfl_xor(s, 16, 64);
+  if constexpr (LPR >= 64) s += __shfl_xor(s, 32, 64);
+  return s;
 }
 
 template <int LPR, int VPL, int W>
@@ -67,12 +81,10 @@ __device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
       s = fmaf(a[q], b[q], s);
     }
   }
-#pragma unroll
-  for (int m = 1; m < LPR; m <<= 1) s += __shfl_xor(s, m, 64);
-  return s;
+  return slot_sum<LPR>(s);
 }
 
-template <int LPR, int VPL, int W, int UNROLL, int ABL = 0>
+template <int LPR, int VPL, int W>
 __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   using V = Vec<W>;
   constexpr int NS = 64 / LPR;
@@ -101,60 +113,56 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         if (nn < 0 || nn >= a.n_posts) atomicAdd(a.err, 1);
         else nid = (int)nn;
       }
-      float my_hp = 0.f, my_hn = 0.f, my_sp = 0.f, my_sn = 0.f;
-      for (int j = 0; j < n; j += NS * UNROLL) {
-        typename V::T vp[UNROLL][VPL], vn[UNROLL][VPL];
+      float my_hp = 0.f, my_hn = 0.f;
+      // software pipeline: step j+NS's row loads are in flight during step j's arithmetic
+      typename V::T vp[VPL], vn[VPL], wp[VPL], wn[VPL];
+      auto load_step = [&](int j, typename V::T (&xp)[VPL], typename V::T (&xn)[VPL]) {
+        const int e = j + slot;
+        const int pp = __shfl(pid, e & 63, 64), qq = __shfl(nid, e & 63, 64);
 #pragma unroll
-        for (int uu = 0; uu < UNROLL; ++uu) {
-          const int e = j + uu * NS + slot;
-          const int pp = __shfl(pid, e & 63, 64), qq = __shfl(nid, e & 63, 64);
-#pragma unroll
-          for (int q = 0; q < VPL; ++q) {
-            const int cc = (q * LPR + sl) * W;
-            const bool ok = e < n && cc < d;
-            vp[uu][q] = ok ? V::load(a.P + (int64_t)pp * d + cc) : V::zero();
-            vn[uu][q] = ok ? V::load(a.P + (int64_t)qq * d + cc) : V::zero();
-          }
+        for (int q = 0; q < VPL; ++q) {
+          const int cc = (q * LPR + sl) * W;
+          const bool ok = e < n && cc < d;
+          xp[q] = ok ? V::load(a.P + (int64_t)pp * d + cc) : V::zero();
+          xn[q] = ok ? V::load(a.P + (int64_t)qq * d + cc) : V::zero();
+        }
+      };
+      load_step(0, vp, vn);
+      for (int j = 0; j < n; j += NS) {
+        if (j + NS < n) load_step(j + NS, wp, wn);
+        const int e = j + slot;
+        const float sp = slot_dot<LPR, VPL, W>(uv, vp);
+        const float sn = slot_dot<LPR, VPL, W>(uv, vn);
+        const float tp = exp_neg_abs(sp), tn = exp_neg_abs(sn);
+        float hp = c * a.inv_e * (sigmoid_t(sp, tp) - 1.f);
+        float hn = a.inv_e * sigmoid_t(sn, tn);
+        if (e >= n) hp = hn = 0.f;
+        // loss terms once per edge, on the slot's first lane:
+        //   softplus(-sp) = max(-sp, 0) + log(1 + t),  softplus(sn) = max(sn, 0) + log(1 + t)
+        if (sl == 0 && e < n) {
+          lpos += fmaxf(-sp, 0.f) + __logf(1.f + tp);
+          lneg += fmaxf(sn, 0.f) + __logf(1.f + tn);
         }
 #pragma unroll
-        for (int uu = 0; uu < UNROLL; ++uu) {
-          const int e0 = j + uu * NS;
-          const int e = e0 + slot;
-          const float sp = slot_dot<LPR, VPL, W>(uv, vp[uu]);
-          const float sn = slot_dot<LPR, VPL, W>(uv, vn[uu]);
-          float hp, hn;
-          if (ABL & 2) { hp = c * a.inv_e * sp; hn = a.inv_e * sn; }
-          else {
-            hp = c * a.inv_e * (sigmoid_t(sp, exp_neg_abs(sp)) - 1.f);
-            hn = a.inv_e * sigmoid_t(sn, exp_neg_abs(sn));
-          }
-          if (e >= n) hp = hn = 0.f;
-#pragma unroll
-          for (int q = 0; q < VPL; ++q) {
-            V::fma(acc[q], hp, vp[uu][q]);
-            V::fma(acc[q], hn, vn[uu][q]);
-          }
-          // hand edge e's values to lane e (lanes e0 .. e0+NS-1 read from slot lane*LPR)
-          const int src = ((lane - e0) & (NS - 1)) * LPR;
-          const float thp = __shfl(hp, src, 64), thn = __shfl(hn, src, 64);
-          const float tsp = __shfl(sp, src, 64), tsn = __shfl(sn, src, 64);
-          if (lane >= e0 && lane < e0 + NS) {
-            my_hp = thp; my_hn = thn; my_sp = tsp; my_sn = tsn;
-          }
+        for (int q = 0; q < VPL; ++q) {
+          V::fma(acc[q], hp, vp[q]);
+          V::fma(acc[q], hn, vn[q]);
+          vp[q] = wp[q];
+          vn[q] = wn[q];
+        }
+        // hand edge e's weights to lane e (lanes j .. j+NS-1 read from slot lane*LPR)
+        const int src = ((lane - j) & (NS - 1)) * LPR;
+        const float thp = __shfl(hp, src, 64), thn = __shfl(hn, src, 64);
+        if (lane >= j && lane < j + NS) {
+          my_hp = thp; my_hn = thn;
         }
       }
       if (lane < n) {
         const int64_t k = base + lane;
-        // the loss terms once per edge, on the lane that owns it
-        lpos += (ABL & 2) ? my_sp : softplus(-my_sp);
-        lneg += (ABL & 2) ? my_sn : softplus(my_sn);
-        if (ABL & 1) a.hpos[k] = my_hp;
-        else a.hpos[a.to_post_pos[k]] = my_hp;
-        if (!(ABL & 4)) {
-          a.neg_key[k] = nid;
-          a.neg_u[k] = (int32_t)u;
-          a.neg_w[k] = my_hn;
-        }
+        a.hpos[a.to_post_pos[k]] = my_hp;
+        a.neg_key[k] = nid;
+        a.neg_u[k] = (int32_t)u;
+        a.neg_w[k] = my_hn;
       }
     }
 #pragma unroll
@@ -227,30 +235,10 @@ __global__ void k_loss_final(const double* red, const float* cscale, float inv_e
   *loss = (float)((double)*cscale * (double)inv_e * p + (double)inv_e * q);
 }
 
-template <int LPR, int VPL, int W, int UNROLL>
+template <int LPR, int VPL, int W>
 static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream) {
-  static const int abl = getenv("HGNN_SCORE_ABL") ? atoi(getenv("HGNN_SCORE_ABL")) : 0;
-  const dim3 g((unsigned)nblocks), b(256);
-  switch (abl) {
-    case 1: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 1>), g, b, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 2>), g, b, 0, stream, a); break;
-    case 4: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 4>), g, b, 0, stream, a); break;
-    case 7: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL, 7>), g, b, 0, stream, a); break;
-    case 8: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, 2, 0>), g, b, 0, stream, a); break;
-    case 10:
-      if (LPR == 16 && W == 4) {
-        hipLaunchKernelGGL((k_edge_score<8, 2, 4, 1, 0>), g, b, 0, stream, a);
-        break;
-      }
-      [[fallthrough]];
-    case 11:
-      if (LPR == 16 && W == 4) {
-        hipLaunchKernelGGL((k_edge_score<4, 4, 4, 1, 0>), g, b, 0, stream, a);
-        break;
-      }
-      [[fallthrough]];
-    default: hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, UNROLL>), g, b, 0, stream, a);
-  }
+  hipLaunchKernelGGL((k_edge_score<LPR, VPL, W>), dim3((unsigned)nblocks), dim3(256), 0,
+                     stream, a);
   return check_launch("k_edge_score");
 }
 
@@ -285,13 +273,13 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   const int64_t nb = cdiv(n_users, 4);   // blocks of 4 user-waves
   int rc = HGNN_OK;
   if (nb > 0) {
-    // UNROLL 1 measured fastest at d=64 (1.76 vs 1.92 ms at 2, 2.16 at 4 on cfg2): the pass is
-    // issue-bound, fewer registers buy more waves
-    if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4, 1>(a, nb, stream);
-    else if (d % 4 == 0 && d <= 128) rc = launch_score<32, 1, 4, 1>(a, nb, stream);
-    else if (d % 4 == 0 && d <= 256) rc = launch_score<64, 1, 4, 1>(a, nb, stream);
-    else if (d <= 64) rc = launch_score<64, 1, 1, 1>(a, nb, stream);
-    else if (d <= 512) rc = launch_score<64, 8, 1, 1>(a, nb, stream);
+    // one 4..16-edge step per iteration, next step's loads pipelined (an unrolled 2-step body
+    // measured slower: users average ~20 edges, so wider steps waste the tail)
+    if (d % 4 == 0 && d <= 64) rc = launch_score<16, 1, 4>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 128) rc = launch_score<32, 1, 4>(a, nb, stream);
+    else if (d % 4 == 0 && d <= 256) rc = launch_score<64, 1, 4>(a, nb, stream);
+    else if (d <= 64) rc = launch_score<64, 1, 1>(a, nb, stream);
+    else if (d <= 512) rc = launch_score<64, 8, 1>(a, nb, stream);
     else return fail(HGNN_E_UNSUPPORTED, "edge_score: d=%d", d);
     if (rc) return rc;
   }
