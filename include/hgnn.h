@@ -119,13 +119,28 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,
                     hgnn_stream_t stream);
 
+/* dP of the fused loss with each edge's weight recomputed from its score (no weight arrays):
+ *   out[r,:] (+)= sum_{p in row r} w(<x[col[p]],:>, rowvec[r,:]>) * x[col[p],:]
+ *   mode 1 (positive edges): w(s) = c*inv_e*(sigmoid(s) - 1), c = *cscale
+ *   mode 2 (negative edges): w(s) = inv_e*sigmoid(s)
+ * i.e. dL/dP[r] of hgnn_edge_score_fwd's loss (train_gnn.py:276-281) for x = U, rowvec = P.
+ * Heavy rows / slab as hgnn_gather_reduce. */
+int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t d,
+                      const int32_t* rowptr, const int32_t* col, int64_t n_rows, int32_t mode,
+                      const float* cscale, float inv_e, const int32_t* heavy_rows,
+                      const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                      int32_t chunk, float* slab, float* out, int32_t accumulate,
+                      hgnn_stream_t stream);
+
 /* ---- edge scoring + weighted BCE (train_gnn.py:259-281), fused with its gradient --------------
  * Positive edges grouped by user (rowptr_u/col_u = post ids); neg_u_order[k] = the negative post
  * drawn for position k; to_post_pos[k] = that edge's position in the post-grouped CSR.
  *   loss = c * mean softplus(-<U[u],P[p]>) + mean softplus(<U[u],P[n]>),  c = *cscale
  *          (= mean(pos_weights): BCEWithLogitsLoss() reduces to a scalar first)
- * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics), hpos[post-grouped pos]
- * (weight of U[u] in dP[p]), and per position (neg_key, neg_user, neg_w) for the negatives' dP;
+ * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics) and per position
+ * (neg_key, neg_user) for sorting the negatives by post.  Optional (may be NULL): hpos[post-grouped
+ * pos] (weight of U[u] in dP[p], needs to_post_pos) and neg_w (weight in dP[n]) — not needed when
+ * dP is formed by hgnn_score_gather, which recomputes both;
  * part needs hgnn_edge_score_parts(n_users) floats (16-B aligned); *err counts out-of-range negatives. */
 int64_t hgnn_edge_score_parts(int64_t n_users);
 int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,

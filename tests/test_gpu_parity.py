@@ -95,6 +95,29 @@ def test_scatter_mean_bwd_matches_autograd(d, chunk):
     close(acc, x.grad + 1.0)
 
 
+@pytest.mark.parametrize("d", [5, 64, 128])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_score_gather_matches_float64(d, mode):
+    """hgnn_score_gather: dP rows with each edge's weight recomputed from <U[u], P[row]>, heavy
+    rows split into chunks (chunk=16 on a skewed graph)."""
+    rng = np.random.default_rng(20 + d + mode)
+    n_u, n_p, E = 600, 250, 9000
+    ei = rand_coo(rng, n_u, n_p, E, skew=True)          # user -> post
+    U = torch.from_numpy(rng.standard_normal((n_u, d)).astype(np.float32) * 0.3)
+    P = torch.from_numpy(rng.standard_normal((n_p, d)).astype(np.float32) * 0.3)
+    c, inv_e = 1.7, 1.0 / 12345
+    s = (U.double()[ei[0]] * P.double()[ei[1]]).sum(1)
+    sg = torch.sigmoid(s)
+    w = c * inv_e * (sg - 1) if mode == 1 else inv_e * sg
+    ref = torch.zeros(n_p, d, dtype=torch.float64).index_add_(0, ei[1], w[:, None] * U.double()[ei[0]])
+    csr = graph.RelationCSR(ei.to(DEV), n_u, n_p, chunk=16)
+    assert csr.fwd.plan.n_heavy > 0
+    out = torch.full((n_p, d), 0.5, device=DEV)
+    ops._score_gather(U.to(DEV), P.to(DEV), csr.fwd, mode, torch.tensor(c, device=DEV), inv_e,
+                      out, True, "t")
+    close(out, ref + 0.5)
+
+
 def test_gather_is_deterministic_bitwise():
     rng = np.random.default_rng(5)
     ei = rand_coo(rng, 5000, 200, 100000, skew=True).to(DEV)

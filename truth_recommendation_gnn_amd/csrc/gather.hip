@@ -33,11 +33,19 @@ struct GatherArgs {
   int32_t chunk;
   int32_t mean;
   int32_t accumulate;
+  // score mode (hgnn_score_gather): w_p = f(<x[col[p]], rowvec[row]>) recomputed per edge
+  const float* rowvec;
+  const float* cscale;
+  float inv_e;
+  int32_t score;               // 1: c*inv_e*(sigmoid(s)-1)   2: inv_e*sigmoid(s)
 };
 
-// Sum of row segment [beg, end) into acc (per lane: VPL vectors of width W).
-template <int LPR, int VPL, int W, int UNROLL, bool HAS_W>
+// Sum of row segment [beg, end) into acc (per lane: VPL vectors of width W).  SC: the weight of
+// each edge is recomputed from the score <x[col[p]], rv> (rv = the row's own vector, e.g. P[post]
+// for the loss gradient dP), so no per-edge weight array is stored or read.
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC>
 __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, int64_t end,
+                                            const typename Vec<W>::T (&rv)[VPL],
                                             typename Vec<W>::T (&acc)[VPL]) {
   using V = Vec<W>;
   constexpr int NS = 64 / LPR;
@@ -70,11 +78,23 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
           v[u][q] = (e < n && c < d) ? V::load(xr + c) : V::zero();
         }
       }
+      if constexpr (SC) {
+        const float cw = a.score == 1 ? *a.cscale * a.inv_e : a.inv_e;
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+          float sdot = 0.f;
+#pragma unroll
+          for (int q = 0; q < VPL; ++q) sdot += V::dot(rv[q], v[u][q]);
+          sdot = slot_sum<LPR>(sdot);
+          const float sg = sigmoid_t(sdot, exp_neg_abs(sdot));
+          we[u] = cw * (a.score == 1 ? sg - 1.f : sg);
+        }
+      }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
-          if (HAS_W) V::fma(acc[q], we[u], v[u][q]);
+          if (HAS_W || SC) V::fma(acc[q], we[u], v[u][q]);
           else V::add(acc[q], v[u][q]);
         }
     }
@@ -86,7 +106,7 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
     for (int q = 0; q < VPL; ++q) V::add(acc[q], V::shfl_xor(acc[q], m));
 }
 
-template <int LPR, int VPL, int W, int UNROLL, bool HAS_W>
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC = false>
 __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
   using V = Vec<W>;
   const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -118,10 +138,14 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
     dst = a.slab + slot * a.d;
     partial = true;
   }
-  typename V::T acc[VPL];
+  typename V::T acc[VPL], rv[VPL];
 #pragma unroll
-  for (int q = 0; q < VPL; ++q) acc[q] = V::zero();
-  segment_sum<LPR, VPL, W, UNROLL, HAS_W>(a, beg, end, acc);
+  for (int q = 0; q < VPL; ++q) {
+    acc[q] = V::zero();
+    const int c = (q * LPR + sl) * W;
+    rv[q] = (SC && c < a.d) ? V::load(a.rowvec + row * a.d + c) : V::zero();
+  }
+  segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, beg, end, rv, acc);
   if (!writer) return;
   float s = 1.f;
   if (!partial && a.mean) s = end > beg ? 1.f / (float)(end - beg) : 0.f;
@@ -193,7 +217,9 @@ __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
 template <int LPR, int VPL, int W, int UNROLL>
 static int launch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) {
   const dim3 grid((unsigned)cdiv(a.n_items, 4)), block(256);
-  if (has_w)
+  if (a.score)
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false, true>), grid, block, 0, stream, a);
+  else if (has_w)
     hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, 0, stream, a);
   else
     hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, 0, stream, a);
@@ -230,6 +256,8 @@ static int run_gather(GatherArgs a, hipStream_t stream) {
   if (a.n_heavy > 0 && (!a.heavy_rows || !a.heavy_first || !a.slab))
     return fail(HGNN_E_ARG, "gather: heavy rows without plan/slab");
   const bool has_w = a.edge_w || a.col_w;
+  if (a.score && (has_w || a.mean || !a.rowvec || (a.score == 1 && !a.cscale)))
+    return fail(HGNN_E_ARG, "score_gather: bad mode/arguments");
   if (int rc = dispatch_gather(a, has_w, stream)) return rc;
   if (a.n_heavy > 0) {
     const dim3 grid((unsigned)a.n_heavy), block(256);
@@ -279,6 +307,23 @@ int hgnn_scatter_mean_bwd(const float* grad_aggr, int64_t n_dst, const float* in
   return hgnn_gather_reduce(grad_aggr, n_dst, d, t_rowptr, t_col, n_src, nullptr, inv_deg,
                             accumulate ? HGNN_ACCUMULATE : 0, heavy_rows, heavy_first, n_heavy,
                             n_chunks, chunk, slab, grad_x_src, stream);
+}
+
+int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t d,
+                      const int32_t* rowptr, const int32_t* col, int64_t n_rows, int32_t mode,
+                      const float* cscale, float inv_e, const int32_t* heavy_rows,
+                      const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
+                      int32_t chunk, float* slab, float* out, int32_t accumulate,
+                      hgnn_stream_t stream) {
+  (void)n_x;
+  if (mode != 1 && mode != 2) return fail(HGNN_E_ARG, "score_gather: mode=%d", mode);
+  GatherArgs a{};
+  a.x = x; a.rowptr = rowptr; a.col = col;
+  a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
+  a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
+  a.d = d; a.chunk = chunk; a.accumulate = accumulate ? 1 : 0;
+  a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = mode;
+  return run_gather(a, as_stream(stream));
 }
 
 }  // extern "C"

@@ -71,6 +71,9 @@ struct Vec<4> {
   static __device__ __forceinline__ void add(T& a, T v) {
     a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
   }
+  static __device__ __forceinline__ float dot(T a, T b) {
+    return fmaf(a.w, b.w, fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)));
+  }
   static __device__ __forceinline__ void scale(T& a, float s) {
     a.x *= s; a.y *= s; a.z *= s; a.w *= s;
   }
@@ -87,12 +90,39 @@ struct Vec<1> {
   static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
   static __device__ __forceinline__ void fma(T& a, float w, T v) { a = fmaf(w, v, a); }
   static __device__ __forceinline__ void add(T& a, T v) { a += v; }
+  static __device__ __forceinline__ float dot(T a, T b) { return a * b; }
   static __device__ __forceinline__ void scale(T& a, float s) { a *= s; }
   static __device__ __forceinline__ T shfl_xor(T v, int m) { return __shfl_xor(v, m, 64); }
 };
 
 // Device exclusive scan of int32 counts (n entries) -> out (n+1 entries, out[n] = total).
 // Workspace query with ws == nullptr.
+// Sum over aligned groups of LPR lanes (power of 2), result in every lane of the group.  Within a
+// 16-lane DPP row the butterfly runs on DPP moves (quad_perm xor 1 / xor 2, row_half_mirror,
+// row_mirror) instead of LDS-pipe ds_bpermute; wider groups finish with shuffles.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+template <int LPR>
+__device__ __forceinline__ float slot_sum(float s) {
+  if constexpr (LPR >= 2) s += dpp_mov<0xB1>(s);    // quad_perm [1,0,3,2]
+  if constexpr (LPR >= 4) s += dpp_mov<0x4E>(s);    // quad_perm [2,3,0,1]
+  if constexpr (LPR >= 8) s += dpp_mov<0x141>(s);   // row_half_mirror
+  if constexpr (LPR >= 16) s += dpp_mov<0x140>(s);  // row_mirror
+  if constexpr (LPR >= 32) s += __shfl_xor(s, 16, 64);
+  if constexpr (LPR >= 64) s += __shfl_xor(s, 32, 64);
+  return s;
+}
+
+// Hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1-2 ulp).  t = exp(-|x|) in
+// (0, 1] serves both:  sigmoid(x) = x >= 0 ? 1/(1+t) : t/(1+t),  softplus(x) = max(x,0) + log(1+t)
+__device__ __forceinline__ float exp_neg_abs(float x) { return __expf(-fabsf(x)); }
+__device__ __forceinline__ float sigmoid_t(float x, float t) {
+  const float r = __builtin_amdgcn_rcpf(1.f + t);
+  return x >= 0.f ? r : t * r;
+}
+
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t* ws_bytes,
                        hipStream_t stream);
 

@@ -40,34 +40,6 @@ struct ScoreArgs {
   int32_t d;
 };
 
-// Hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1-2 ulp): libm-accurate expf /
-// log1pf / division cost 2x the whole pass here.  t = exp(-|x|) in (0, 1] is shared by both:
-//   sigmoid(x) = x >= 0 ? 1/(1+t) : t/(1+t),   softplus(x) = max(x, 0) + log(1 + t)
-// (log(1+t) loses t below ~1e-7 absolute — far under the fp32 loss tolerance).
-__device__ __forceinline__ float exp_neg_abs(float x) { return __expf(-fabsf(x)); }
-__device__ __forceinline__ float sigmoid_t(float x, float t) {
-  const float r = __builtin_amdgcn_rcpf(1.f + t);
-  return x >= 0.f ? r : t * r;
-}
-
-// Sum over the LPR lanes of a slot, result in every lane of the slot.  Within a 16-lane DPP row
-// the butterfly runs on DPP source modifiers (quad_perm xor 1 / xor 2, row_half_mirror,
-// row_mirror) fused into the adds: no LDS-pipe ds_bpermute.  Wider slots finish with shuffles.
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-template <int LPR>
-__device__ __forceinline__ float slot_sum(float s) {
-  if constexpr (LPR >= 2) s += dpp_mov<0xB1>(s);    // quad_perm [1,0,3,2]
-  if constexpr (LPR >= 4) s += dpp_mov<0x4E>(s);    // quad_perm [2,3,0,1]
-  if constexpr (LPR >= 8) s += dpp_mov<0x141>(s);   // row_half_mirror
-  if constexpr (LPR >= 16) s += dpp_mov<0x140>(s);  // row_mirror
-  if constexpr (LPR >= 32) s += __shfl_xor(s, 16, 64);
-  if constexpr (LPR >= 64) s += __shfl_xor(s, 32, 64);
-  return s;
-}
-
 template <int LPR, int VPL, int W>
 __device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
                                           const typename Vec<W>::T (&b)[VPL]) {
@@ -159,10 +131,10 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
       }
       if (lane < n) {
         const int64_t k = base + lane;
-        a.hpos[a.to_post_pos[k]] = my_hp;
+        if (a.hpos) a.hpos[a.to_post_pos[k]] = my_hp;
         a.neg_key[k] = nid;
         a.neg_u[k] = (int32_t)u;
-        a.neg_w[k] = my_hn;
+        if (a.neg_w) a.neg_w[k] = my_hn;
       }
     }
 #pragma unroll
@@ -262,8 +234,10 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   hipStream_t stream = as_stream(stream_);
   if (d < 1 || n_users < 0 || n_posts < 0 || n_edges < 0)
     return fail(HGNN_E_ARG, "edge_score: bad sizes");
-  if (!cscale || !loss || !err || (n_users > 0 && (!U || !rowptr_u || !dU || !part)))
+  if (!cscale || !loss || !err ||
+      (n_users > 0 && (!U || !rowptr_u || !dU || !part || !neg_key || !neg_user)))
     return fail(HGNN_E_ARG, "edge_score: null pointer");
+  if (hpos && !to_post_pos) return fail(HGNN_E_ARG, "edge_score: hpos needs to_post_pos");
   (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);
   ScoreArgs a{};
   a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order;

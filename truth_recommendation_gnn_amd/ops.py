@@ -114,6 +114,24 @@ def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
             N.stream_ptr(dev)), "hgnn_gather_reduce")
 
 
+def _score_gather(U, P, grouped, mode, cscale, inv_e, out, accumulate, tag):
+    """dP rows from the loss: each edge's weight recomputed from <U[u], P[row]> (mode 1 positive,
+    2 negative) inside the gather — see hgnn_score_gather."""
+    p = grouped.plan
+    dev = out.device
+    d = int(out.shape[1])
+    slab = None
+    if p.n_heavy:
+        slab = torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
+    nb = gather_bytes(int(grouped.col.numel()), grouped.n_rows, d, False) + 4 * grouped.n_rows * d
+    with _timed(f"score_gather_{tag}[{grouped.n_rows}<-{U.shape[0]}]x{d}", nb):
+        N.check(N.lib().hgnn_score_gather(
+            N.ptr(U), U.shape[0], N.ptr(P), d, N.ptr(grouped.rowptr), N.ptr(grouped.col),
+            grouped.n_rows, mode, N.ptr(cscale), inv_e, N.ptr(p.heavy_rows), N.ptr(p.heavy_first),
+            p.n_heavy, p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out), 1 if accumulate else 0,
+            N.stream_ptr(dev)), "hgnn_score_gather")
+
+
 def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K2: ``grad_x_src[j] (+)= sum_{(j->i)} grad_aggr[i] / deg_i`` over the CSC."""
@@ -344,19 +362,6 @@ def link_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.T
 
 
 # ----------------------------------------------------------------------------- fused link loss
-def _user_to_post_pos(csr: RelationCSR) -> torch.Tensor:
-    """Static per graph: user-grouped position k -> the same edge's post-grouped position."""
-    m = getattr(csr, "_u2p", None)
-    if m is None:
-        E = csr.num_edges
-        dev = csr.fwd.rowptr.device
-        inv = torch.empty(E, dtype=torch.int32, device=dev)
-        inv[csr.fwd.perm.long()] = torch.arange(E, dtype=torch.int32, device=dev)
-        m = inv[csr.bwd.perm.long()].contiguous()
-        csr._u2p = m
-    return m
-
-
 def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tensor:
     """Re-order negatives drawn per COO edge (train_gnn.py:272) to the user-grouped order the
     fused kernel walks."""
@@ -374,42 +379,40 @@ class _EdgeBCELoss(torch.autograd.Function):
         if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
             raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
         ub, pf = csr.bwd, csr.fwd
-        to_post = _user_to_post_pos(csr)
         dU = torch.empty_like(U)
-        hpos = torch.empty(E, dtype=torch.float32, device=dev)
         neg_key = torch.empty(E, dtype=torch.int32, device=dev)
         neg_user = torch.empty(E, dtype=torch.int32, device=dev)
-        neg_w = torch.empty(E, dtype=torch.float32, device=dev)
         part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         err = torch.zeros(2, dtype=torch.int32, device=dev)
         c = cscale.to(torch.float32).reshape(()).contiguous()
-        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 2 + 2 + 4) + 8 * nu * d):
+        inv_e = 1.0 / n_total if n_total > 0 else 0.0
+        # pass A: loss + dU; the dP weights are not stored — the two dP gathers recompute them
+        # from <U[u], P[post]> with P[post] held per row (hgnn_score_gather)
+        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2 + 2) + 8 * nu * d):
             N.check(lib.hgnn_edge_score_fwd(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                N.ptr(neg_u_order), N.ptr(to_post), n_total, N.ptr(c), N.ptr(dU), N.ptr(hpos),
-                N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), N.ptr(part), N.ptr(loss),
+                N.ptr(neg_u_order), None, n_total, N.ptr(c), N.ptr(dU), None,
+                N.ptr(neg_key), N.ptr(neg_user), None, N.ptr(part), N.ptr(loss),
                 N.ptr(err), s), "hgnn_edge_score_fwd")
-        # dP = positives (post-grouped weighted gather of U rows, side stream) + negatives
-        # (fresh draw every step: sort by post, then weighted gather, main stream) — the sort is
-        # LDS/latency bound and overlaps the HBM-bound positive gather
+        # dP = positives (post-grouped CSR, side stream) + negatives (fresh draw every step:
+        # (post, user) sorted by post on the main stream, overlapping the HBM-bound gather)
         rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
         nu_s = torch.empty(E, dtype=torch.int32, device=dev)
-        nw_s = torch.empty(E, dtype=torch.float32, device=dev)
         dP = torch.empty_like(P)
         lanes = _Lanes(dev, 2)
         with torch.cuda.stream(lanes.stream(1)):
-            _gather(U, pf, None, csr_mean=False, out=dP, accumulate=False, edge_w=hpos)
+            _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-        with _timed("sort_negatives", 4 * E * 6 * 2):
+        with _timed("sort_negatives", 4 * E * 4 * 2):
             N.check(lib.hgnn_sort_pairs_i32(
-                N.ptr(neg_key), N.ptr(neg_user), N.ptr(neg_w), E, np_, N.ptr(rowptr_n),
-                N.ptr(nu_s), N.ptr(nw_s), N.ptr(err[1:]), N.ptr(ws), ws.numel(),
+                N.ptr(neg_key), N.ptr(neg_user), None, E, np_, N.ptr(rowptr_n),
+                N.ptr(nu_s), None, N.ptr(err[1:]), N.ptr(ws), ws.numel(),
                 N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
         lanes.join()
         from .graph import GroupedEdges, Plan
         negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
-        _gather(U, negs, None, csr_mean=False, out=dP, accumulate=True, edge_w=nw_s)
+        _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
         if check and int(err[0]):
             raise ValueError("edge_bce_loss: negative post id out of range")
         ctx.save_for_backward(dU, dP)
