@@ -120,6 +120,9 @@ def main():
         g = synth.make_graph(cfg, device=dev)
         pos = g.edge_index_dict[synth.ENGAGES]
         pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
+        # BCEWithLogitsLoss() collapses the per-edge interaction weights to their mean
+        # (train_gnn.py:276-281); the weights are static graph data, so the mean is taken once
+        cscale = pw.mean()
         model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers).to(dev)
         with torch.no_grad():
             model(g.x_dict, g.edge_index_dict)  # materialise lazy weights, build + cache CSR/CSC
@@ -129,7 +132,7 @@ def main():
             out = model(g.x_dict, g.edge_index_dict)
             neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
             return ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
-                                     check=False)
+                                     check=False, cscale=cscale)
     else:
         env = parallel.DistEnv.from_torch()
         gcfg = synth.replicated(args.config, world) if args.scale == 1.0 else cfg

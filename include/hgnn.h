@@ -55,7 +55,10 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
 
 /* Stable sort of int32 keys in [0,n_keys) carrying one or two int32 payloads (b may be NULL):
  * rowptr[n_keys+1] over the sorted keys, payloads in key order.  Out-of-range keys are dropped
- * and counted in *d_invalid.  Used per step to group the sampled negatives by post. */
+ * and counted in *d_invalid.  d_invalid == NULL declares the keys already validated (the fused
+ * loss validates its negatives in hgnn_edge_score_fwd): no extra pass over the keys then, and an
+ * out-of-range key is still never dereferenced, only misplaced.  `keys` is never written.
+ * Used per step to group the sampled negatives by post. */
 size_t hgnn_sort_pairs_ws_bytes(int64_t E, int64_t n_keys);
 int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b, int64_t E,
                         int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,

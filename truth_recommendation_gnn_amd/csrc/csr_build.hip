@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
 // The tile is then reordered by (digit, original index) in LDS and written out in per-digit
 // runs, so global stores are contiguous runs instead of scattered words.  Carries up to two
 // 32-bit payloads (a: identity when identity_a is set; b optional).
-template <int BITS>
+template <int BITS, bool HAS_B>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
     const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   __shared__ int gbase[R];                       // global start of this tile's digit run
   __shared__ int skey[kSortTile];
   __shared__ int sa[kSortTile];
-  __shared__ int sb[kSortTile];
+  __shared__ int sb[HAS_B ? kSortTile : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
     for (int w = 0; w < NW; ++w) wcount[w][dd] = 0;
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const bool valid = i < E;
     key[r] = valid ? keys_in[i] : 0;
     va[r] = valid ? (identity_a ? (int)i : a_in[i]) : 0;
-    vb[r] = (valid && b_in) ? b_in[i] : 0;
+    vb[r] = (HAS_B && valid) ? b_in[i] : 0;
     const int digit = (key[r] >> shift) & (R - 1);
     unsigned long long match = __ballot(valid);
 #pragma unroll
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
       const int pos = wcount[wid][digit] + rank[r];
       skey[pos] = key[r];
       sa[pos] = va[r];
-      sb[pos] = vb[r];
+      if (HAS_B) sb[pos] = vb[r];
     }
   }
   __syncthreads();
@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int64_t pos = (int64_t)gbase[digit] + (j - dstart[digit]);
     keys_out[pos] = k;
     a_out[pos] = sa[j];
-    if (b_out) b_out[pos] = sb[j];
+    if (HAS_B) b_out[pos] = sb[j];
   }
 }
 
@@ -358,9 +358,10 @@ static size_t sort_ws_bytes(int64_t E) {
 // LSD sort of prepared keys (ka, values in [0, n_keys]) with payload a (identity if a_in null)
 // and optional b.  The last pass lands the payloads in a_out / b_out; the sorted keys end in
 // *k_sorted (a workspace buffer).
-static int radix_sort_pairs(int32_t* ka, int64_t E, int64_t n_keys, const int32_t* a_in,
-                            const int32_t* b_in, int32_t* a_out, int32_t* b_out, Workspace& w,
-                            hipStream_t stream, const int32_t** k_sorted) {
+static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t n_keys,
+                            const int32_t* a_in, const int32_t* b_in, int32_t* a_out,
+                            int32_t* b_out, Workspace& w, hipStream_t stream,
+                            const int32_t** k_sorted) {
   int32_t* kb = w.take<int32_t>(E);
   int32_t* ta = w.take<int32_t>(E);
   int32_t* tb = b_in ? w.take<int32_t>(E) : nullptr;
@@ -374,13 +375,13 @@ static int radix_sort_pairs(int32_t* ka, int64_t E, int64_t n_keys, const int32_
   exclusive_scan_i32(nullptr, nullptr, ncount, nullptr, &scan_b, stream);
   void* scan_ws = w.take<char>(scan_b);
   if (!scan_ws) return fail(HGNN_E_WS, "radix sort: workspace too small");
-  const int32_t* kin = ka;
+  const int32_t* kin = k_in;   // read-only input; passes ping-pong between ka and kb
   const int32_t* ain = a_in;
   const int32_t* bin = b_in;
   for (int p = 0; p < passes; ++p) {
     const int shift = bits * p;
     const bool to_out = ((passes - 1 - p) % 2) == 0;
-    int32_t* kout = (kin == ka) ? kb : ka;
+    int32_t* kout = (kin == ka) ? kb : ka;   // (k_in itself is never written)
     int32_t* aout = to_out ? a_out : ta;
     int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
     const int ident = (p == 0 && a_in == nullptr) ? 1 : 0;
@@ -392,12 +393,12 @@ static int radix_sort_pairs(int32_t* ka, int64_t E, int64_t n_keys, const int32_
                          shift, counts);
     if (int rc = check_launch("k_digit_counts")) return rc;
     if (int rc = exclusive_scan_i32(counts, offs, ncount, scan_ws, &scan_b, stream)) return rc;
-    if (bits == 9)
-      hipLaunchKernelGGL(k_digit_scatter<9>, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain,
-                         bin, E, shift, offs, kout, aout, bout, ident);
-    else
-      hipLaunchKernelGGL(k_digit_scatter<8>, dim3(nb), dim3(kSortThreads), 0, stream, kin, ain,
-                         bin, E, shift, offs, kout, aout, bout, ident);
+#define HGNN_SCATTER(BV, HB)                                                                 \
+  hipLaunchKernelGGL((k_digit_scatter<BV, HB>), dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, \
+                     bin, E, shift, offs, kout, aout, bout, ident)
+    if (bits == 9) { if (b_in) HGNN_SCATTER(9, true); else HGNN_SCATTER(9, false); }
+    else { if (b_in) HGNN_SCATTER(8, true); else HGNN_SCATTER(8, false); }
+#undef HGNN_SCATTER
     if (int rc = check_launch("k_digit_scatter")) return rc;
     kin = kout;
     ain = aout;
@@ -447,7 +448,8 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
                      n_keys, n_other, ka, d_invalid);
   if (int rc = check_launch("k_prepare_keys")) return rc;
   const int32_t* sk = nullptr;
-  if (int rc = radix_sort_pairs(ka, E, n_keys, nullptr, nullptr, perm, nullptr, w, stream, &sk))
+  if (int rc = radix_sort_pairs(ka, ka, E, n_keys, nullptr, nullptr, perm, nullptr, w, stream,
+                                &sk))
     return rc;
   hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);
@@ -469,9 +471,9 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_keys < 0 || n_keys >= (int64_t(1) << 31) - 1)
     return fail(HGNN_E_ARG, "sort_pairs: E=%lld n_keys=%lld out of range", (long long)E,
                 (long long)n_keys);
-  if (!rowptr || !d_invalid || (E > 0 && (!keys || !a || !a_sorted || (b && !b_sorted))))
+  if (!rowptr || (E > 0 && (!keys || !a || !a_sorted || (b && !b_sorted))))
     return fail(HGNN_E_ARG, "sort_pairs: null pointer");
-  (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
+  if (d_invalid) (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
   if (E == 0 || n_keys == 0) {
     hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
                        n_keys + 1, 0);
@@ -480,11 +482,15 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "sort_pairs: workspace too small");
   Workspace w(ws, ws_bytes);
   int32_t* ka = w.take<int32_t>(E);
-  hipLaunchKernelGGL(k_prepare_keys32, dim3(cdiv(E, 256)), dim3(256), 0, stream, keys, E, n_keys,
-                     ka, d_invalid);
-  if (int rc = check_launch("k_prepare_keys32")) return rc;
+  const int32_t* kin = keys;   // d_invalid == NULL: the caller guarantees keys in [0, n_keys)
+  if (d_invalid) {
+    hipLaunchKernelGGL(k_prepare_keys32, dim3(cdiv(E, 256)), dim3(256), 0, stream, keys, E,
+                       n_keys, ka, d_invalid);
+    if (int rc = check_launch("k_prepare_keys32")) return rc;
+    kin = ka;
+  }
   const int32_t* sk = nullptr;
-  if (int rc = radix_sort_pairs(ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
+  if (int rc = radix_sort_pairs(kin, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
     return rc;
   hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);

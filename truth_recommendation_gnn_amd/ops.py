@@ -407,7 +407,7 @@ class _EdgeBCELoss(torch.autograd.Function):
         with _timed("sort_negatives", 4 * E * 4 * 2):
             N.check(lib.hgnn_sort_pairs_i32(
                 N.ptr(neg_key), N.ptr(neg_user), None, E, np_, N.ptr(rowptr_n),
-                N.ptr(nu_s), None, N.ptr(err[1:]), N.ptr(ws), ws.numel(),
+                N.ptr(nu_s), None, None, N.ptr(ws), ws.numel(),
                 N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
         lanes.join()
         from .graph import GroupedEdges, Plan
