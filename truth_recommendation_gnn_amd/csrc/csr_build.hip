@@ -191,6 +191,16 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
 // The tile is then reordered by (digit, original index) in LDS and written out in per-digit
 // runs, so global stores are contiguous runs instead of scattered words.  Carries up to two
 // 32-bit payloads (a: identity when identity_a is set; b optional).
+// XCD-aware tile order: workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2), so hardware block b runs on XCD b % 8.  Giving each XCD a contiguous range of tiles puts the
+// neighbouring runs of every digit (tile t, t+1) in the same L2, where their partial lines merge
+// before write-back.  Bijective for any nb.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
+  constexpr int kXcd = 8;
+  const int64_t q = nb / kXcd, r = nb % kXcd, x = b % kXcd, i = b / kXcd;
+  return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
 template <int BITS, bool HAS_B>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
@@ -205,13 +215,14 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   __shared__ int sa[kSortTile];
   __shared__ int sb[HAS_B ? kSortTile : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
     for (int w = 0; w < NW; ++w) wcount[w][dd] = 0;
-    gbase[dd] = offs[(int64_t)dd * gridDim.x + blockIdx.x];
+    gbase[dd] = offs[(int64_t)dd * gridDim.x + tile];
   }
   __syncthreads();
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t tile0 = (int64_t)blockIdx.x * kSortTile;
+  const int64_t tile0 = tile * kSortTile;
   const int64_t wave0 = tile0 + (int64_t)wid * PER_WAVE;
   int key[kSortRounds], rank[kSortRounds], va[kSortRounds], vb[kSortRounds];
 #pragma unroll
