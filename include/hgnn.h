@@ -64,6 +64,12 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
                         int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
                         int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* As hgnn_sort_pairs_i32 for int64 keys (e.g. torch.randint negatives as drawn): out-of-range
+ * keys always go to the dropped sentinel and are counted in *d_invalid (required). */
+int hgnn_sort_pairs_i64(const int64_t* keys, const int32_t* a, const int32_t* b, int64_t E,
+                        int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
+                        int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- degree-skew plan ----------------------------------------------------------------------
  * Rows with more than `chunk` edges are split into ceil(deg/chunk) chunks, each summed by its own
  * wave into a partial slot, then reduced in chunk order (deterministic).  Two phases so the host
@@ -140,8 +146,9 @@ int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t 
  * drawn for position k; to_post_pos[k] = that edge's position in the post-grouped CSR.
  *   loss = c * mean softplus(-<U[u],P[p]>) + mean softplus(<U[u],P[n]>),  c = *cscale
  *          (= mean(pos_weights): BCEWithLogitsLoss() reduces to a scalar first)
- * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics) and per position
- * (neg_key, neg_user) for sorting the negatives by post.  Optional (may be NULL): hpos[post-grouped
+ * Writes dU (dL/dU for a unit upstream gradient, row-owned, no atomics).  Optional (may be NULL):
+ * per position (neg_key, neg_user) — the validated negative and its user, for sorting by post;
+ * hpos[post-grouped
  * pos] (weight of U[u] in dP[p], needs to_post_pos) and neg_w (weight in dP[n]) — not needed when
  * dP is formed by hgnn_score_gather, which recomputes both;
  * part needs hgnn_edge_score_parts(n_users) floats (16-B aligned); *err counts out-of-range negatives. */

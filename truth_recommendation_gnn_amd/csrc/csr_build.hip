@@ -344,6 +344,22 @@ __global__ void __launch_bounds__(256) k_prepare_keys32(const int32_t* key, int6
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
 }
 
+// int64 keys -> int32 key32 (out-of-range -> n_keys sentinel); counts invalid keys.
+__global__ void __launch_bounds__(256) k_prepare_keys64(const int64_t* key, int64_t E,
+                                                        int64_t n_keys, int32_t* key32,
+                                                        int32_t* invalid) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int bad = 0;
+  if (i < E) {
+    const int64_t k = key[i];
+    const bool ok = k >= 0 && k < n_keys;
+    key32[i] = ok ? (int32_t)k : (int32_t)n_keys;
+    bad = ok ? 0 : 1;
+  }
+  unsigned long long m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
+}
+
 __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
@@ -502,6 +518,38 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   }
   const int32_t* sk = nullptr;
   if (int rc = radix_sort_pairs(kin, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
+    return rc;
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+                     n_keys, rowptr);
+  return check_launch("k_rowptr_from_sorted");
+}
+
+int hgnn_sort_pairs_i64(const int64_t* keys, const int32_t* a, const int32_t* b, int64_t E,
+                        int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
+                        int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_keys < 0 || n_keys >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "sort_pairs_i64: E=%lld n_keys=%lld out of range", (long long)E,
+                (long long)n_keys);
+  if (!rowptr || !d_invalid || (E > 0 && (!keys || !a || !a_sorted || (b && !b_sorted))))
+    return fail(HGNN_E_ARG, "sort_pairs_i64: null pointer");
+  (void)hipMemsetAsync(d_invalid, 0, sizeof(int32_t), stream);
+  if (E == 0 || n_keys == 0) {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
+                       n_keys + 1, 0);
+    if (E > 0)
+      hipLaunchKernelGGL(k_prepare_keys64, dim3(cdiv(E, 256)), dim3(256), 0, stream, keys, E,
+                         n_keys, a_sorted, d_invalid);   // (count only; payloads are undefined)
+    return check_launch("sort_pairs_i64(empty)");
+  }
+  if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "sort_pairs_i64: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* ka = w.take<int32_t>(E);
+  hipLaunchKernelGGL(k_prepare_keys64, dim3(cdiv(E, 256)), dim3(256), 0, stream, keys, E, n_keys,
+                     ka, d_invalid);
+  if (int rc = check_launch("k_prepare_keys64")) return rc;
+  const int32_t* sk = nullptr;
+  if (int rc = radix_sort_pairs(ka, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
     return rc;
   hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);

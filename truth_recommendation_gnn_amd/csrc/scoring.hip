@@ -132,8 +132,10 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
       if (lane < n) {
         const int64_t k = base + lane;
         if (a.hpos) a.hpos[a.to_post_pos[k]] = my_hp;
-        a.neg_key[k] = nid;
-        a.neg_u[k] = (int32_t)u;
+        if (a.neg_key) {
+          a.neg_key[k] = nid;
+          a.neg_u[k] = (int32_t)u;
+        }
         if (a.neg_w) a.neg_w[k] = my_hn;
       }
     }
@@ -235,7 +237,7 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   if (d < 1 || n_users < 0 || n_posts < 0 || n_edges < 0)
     return fail(HGNN_E_ARG, "edge_score: bad sizes");
   if (!cscale || !loss || !err ||
-      (n_users > 0 && (!U || !rowptr_u || !dU || !part || !neg_key || !neg_user)))
+      (n_users > 0 && (!U || !rowptr_u || !dU || !part)) || (!neg_key != !neg_user))
     return fail(HGNN_E_ARG, "edge_score: null pointer");
   if (hpos && !to_post_pos) return fail(HGNN_E_ARG, "edge_score: hpos needs to_post_pos");
   (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);

@@ -204,16 +204,17 @@ class _Lanes:
     main stream beforehand or record_stream()'d for it, and the main stream joins the side
     stream before returning, so the caching allocator never hands out memory still in use.
     Off by default: on cfg2 every overlapped pair slowed each other by as much as the overlap
-    saved (10.55 vs 10.51 ms/step; the gathers already saturate the memory system).
-    HGNN_STREAMS=1 turns it on."""
+    saved (layers: 10.55 vs 10.51 ms/step, the gathers already saturate the memory system; loss:
+    the sort beside pass A stretched 0.49 -> 1.66 ms — pass A's workgroups hold every CU, so the
+    sort's only get dispatched as it drains).  HGNN_STREAMS=1 turns it on."""
 
     _side: Dict[torch.device, torch.cuda.Stream] = {}
     enabled = os.environ.get("HGNN_STREAMS", "0") == "1"
 
-    def __init__(self, dev: torch.device, n_chains: int):
+    def __init__(self, dev: torch.device, n_chains: int, force: bool = False):
         self.main = torch.cuda.current_stream(dev)
         self.side = None
-        if self.enabled and n_chains > 1:
+        if (self.enabled or force) and n_chains > 1:
             self.side = _Lanes._side.get(dev)
             if self.side is None:
                 self.side = _Lanes._side[dev] = torch.cuda.Stream(dev)
@@ -362,6 +363,18 @@ def link_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.T
 
 
 # ----------------------------------------------------------------------------- fused link loss
+def _user_of_pos(csr: RelationCSR) -> torch.Tensor:
+    """Static per graph: the user owning each position of the user-grouped CSC (int32)."""
+    m = getattr(csr, "_uop", None)
+    if m is None:
+        rp = csr.bwd.rowptr
+        deg = (rp[1:] - rp[:-1]).long()
+        m = torch.repeat_interleave(torch.arange(csr.n_src, dtype=torch.int32, device=rp.device),
+                                    deg).contiguous()
+        csr._uop = m
+    return m
+
+
 def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tensor:
     """Re-order negatives drawn per COO edge (train_gnn.py:272) to the user-grouped order the
     fused kernel walks."""
@@ -380,39 +393,37 @@ class _EdgeBCELoss(torch.autograd.Function):
             raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
         ub, pf = csr.bwd, csr.fwd
         dU = torch.empty_like(U)
-        neg_key = torch.empty(E, dtype=torch.int32, device=dev)
-        neg_user = torch.empty(E, dtype=torch.int32, device=dev)
         part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         err = torch.zeros(2, dtype=torch.int32, device=dev)
         c = cscale.to(torch.float32).reshape(()).contiguous()
         inv_e = 1.0 / n_total if n_total > 0 else 0.0
-        # pass A: loss + dU; the dP weights are not stored — the two dP gathers recompute them
-        # from <U[u], P[post]> with P[post] held per row (hgnn_score_gather)
-        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2 + 2) + 8 * nu * d):
-            N.check(lib.hgnn_edge_score_fwd(
-                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                N.ptr(neg_u_order), None, n_total, N.ptr(c), N.ptr(dU), None,
-                N.ptr(neg_key), N.ptr(neg_user), None, N.ptr(part), N.ptr(loss),
-                N.ptr(err), s), "hgnn_edge_score_fwd")
-        # dP = positives (post-grouped CSR, side stream) + negatives (fresh draw every step:
-        # (post, user) sorted by post on the main stream, overlapping the HBM-bound gather)
+        uop = _user_of_pos(csr)
+        neg = neg_u_order.to(torch.int64).contiguous()
         rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
         nu_s = torch.empty(E, dtype=torch.int32, device=dev)
         dP = torch.empty_like(P)
+        # dP chain (side stream under HGNN_STREAMS=1): sort the negatives (post, user) by post,
+        # then the two dP gathers, each edge's weight recomputed from <U[u], P[post]>
+        # (hgnn_score_gather); pass A (loss + dU) needs none of it.
         lanes = _Lanes(dev, 2)
         with torch.cuda.stream(lanes.stream(1)):
+            ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
+            with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
+                N.check(lib.hgnn_sort_pairs_i64(
+                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s), None,
+                    N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                    "hgnn_sort_pairs_i64")
             _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
-        ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-        with _timed("sort_negatives", 4 * E * 4 * 2):
-            N.check(lib.hgnn_sort_pairs_i32(
-                N.ptr(neg_key), N.ptr(neg_user), None, E, np_, N.ptr(rowptr_n),
-                N.ptr(nu_s), None, None, N.ptr(ws), ws.numel(),
-                N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
+            from .graph import GroupedEdges, Plan
+            negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
+            _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
+        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
+            N.check(lib.hgnn_edge_score_fwd(
+                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
+                N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
         lanes.join()
-        from .graph import GroupedEdges, Plan
-        negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
-        _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
         if check and int(err[0]):
             raise ValueError("edge_bce_loss: negative post id out of range")
         ctx.save_for_backward(dU, dP)
