@@ -160,6 +160,19 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
                         int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
                         hgnn_stream_t stream);
 
+/* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
+ * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of
+ * user and candidate embeddings, computed by the caller).  Per row:
+ *   top-k, k = min(K, n_cand), ordered by (score desc, candidate index asc)  -> topk_idx (opt.)
+ *   recall[r] = |top-k ∩ true(r)| / true_count[r]   (true_count counts duplicate test edges)
+ *   ndcg[r]   = sklearn ndcg_score(binary relevance, scores, k=K), tie-averaged (ignore_ties=False)
+ * true_rowptr/true_cand: each row's sorted unique relevant candidate indices.  K <= 63.
+ * Scores are assumed finite. */
+int hgnn_topk_metrics(const float* scores, int64_t n_rows, int64_t n_cand, int64_t ld,
+                      const int32_t* true_rowptr, const int32_t* true_cand,
+                      const int32_t* true_count, int32_t K, int32_t* topk_idx, double* recall,
+                      double* ndcg, hgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

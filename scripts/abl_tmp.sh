@@ -1,8 +1,8 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests -m gpu -x -q -k "loss or golden or shard or score or sort or csr" > gpurun_out/t_so.log 2>&1 || { tail -30 gpurun_out/t_so.log; exit 1; }
-tail -1 gpurun_out/t_so.log
-timeout -k 10 300 python scripts/microbench.py > gpurun_out/mb_so.log 2>&1 || exit 1
-grep "loss" gpurun_out/mb_so.log | head -6
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b_so.log 2>&1 || exit 1
-tail -1 gpurun_out/b_so.log | cut -c1-200
+rm -rf gpurun_out/evpmc_*
+for c in "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_BRANCH" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_ANY"; do
+  tag=$(echo $c | cut -d' ' -f1)
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d gpurun_out/evpmc_$tag -o k -- python3 scripts/eval_target.py > gpurun_out/evpmc_$tag.log 2>&1 || exit 1
+  echo "$tag ok"
+done

@@ -105,6 +105,14 @@ def main():
     for k, v in t.summary().items():
         rec("  loss/" + k, v["ms"] / v["launches"] * (v["launches"] / args.reps),
             v["bytes"] / args.reps)
+    # evaluation (train_gnn.py:289-367): 10% of the engages as test edges
+    from truth_recommendation_gnn_amd import metrics
+    te = eng[:, ::10].clone()
+    te[1] += cfg.num_users
+    n_eval_users = int(torch.unique(te[0]).numel())
+    ms = timeit(lambda: metrics.evaluate(te, U, P, K=10), 2, 1)
+    rec("evaluate Recall/NDCG@10 (10% test)", ms)
+    print(f"   test users {n_eval_users}, candidates {int(torch.unique(te[1]).numel())}")
     print(json.dumps(res))
 
 

@@ -46,6 +46,8 @@ _SIGS = {
     "hgnn_score_gather": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _c_i64, _c_i32, _p,
                                    ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p,
                                    _c_i32, _p]),
+    "hgnn_topk_metrics": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _c_i32, _p, _p, _p,
+                                   _p]),
     "hgnn_edge_score_parts": (_c_i64, [_c_i64]),
     "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _p, _c_i64, _p,
                                      _p, _p, _p, _p, _p, _p, _p, _p, _p]),

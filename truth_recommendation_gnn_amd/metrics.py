@@ -1,0 +1,92 @@
+"""Batched Recall@K / NDCG@K — the reference's ``evaluate`` (train_gnn.py:289-367) on device.
+
+The reference loops over test users in Python: one [1,d]x[d,C] product, one ``torch.topk``, one
+``sklearn.metrics.ndcg_score`` and several host syncs per user.  Here the grouping is a handful of
+device sorts, the scores of a batch of users are one GEMM (a plain library GEMM, torch.mm ->
+hipBLASLt), and top-K + both metrics for every user of the batch are one HIP kernel
+(``hgnn_topk_metrics``, csrc/eval.hip).  Same arguments, same return values.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import _native as N
+
+
+class _Grouped:
+    """Test edges grouped per user: candidates, per-user unique relevant candidates, counts."""
+
+    def __init__(self, test_edges: torch.Tensor, num_users: int, num_posts: int):
+        te = test_edges.to(torch.int64)
+        u, p_local = te[0], te[1] - num_users             # train_gnn.py:313-316
+        if p_local.numel() and (int(p_local.min()) < 0 or int(p_local.max()) >= num_posts):
+            raise ValueError("evaluate: test edge post id outside [num_users, num_users+num_posts)")
+        if u.numel() and int(u.min()) < 0:
+            raise ValueError("evaluate: negative user id in test_edges")
+        # candidates: every post of the test set, sorted (train_gnn.py:320-322) — including the
+        # posts of skipped (out-of-range) users, as in the reference
+        self.cand, inv = torch.unique(p_local, sorted=True, return_inverse=True)
+        C = int(self.cand.numel())
+        keep = u < num_users                              # train_gnn.py:328
+        u, c = u[keep], inv[keep]
+        self.users, counts = torch.unique(u, sorted=True, return_counts=True)
+        self.true_count = counts.to(torch.int32)
+        key = torch.unique(u * max(C, 1) + c, sorted=True)     # (user, candidate) pairs, deduped
+        ku = key // max(C, 1)
+        per_user = torch.searchsorted(ku, self.users, right=True)
+        self.rowptr = torch.cat([per_user.new_zeros(1), per_user]).to(torch.int32)
+        self.true_cand = (key % max(C, 1)).to(torch.int32)
+
+
+def evaluate(test_edges: torch.Tensor, user_emb: torch.Tensor, post_emb: torch.Tensor,
+             K: int = 10, num_users: Optional[int] = None,
+             batch_scores: int = 1 << 30) -> Tuple[float, float]:
+    """Mean Recall@K and NDCG@K over the test users (train_gnn.py:289-367).
+
+    ``test_edges``: [2, E] user -> global post id (post ids offset by ``num_users``, as the
+    reference builds them; ``num_users`` defaults to ``user_emb.shape[0]``, the reference's global).
+    ``batch_scores`` bounds the floats of one score matrix (rows x candidates)."""
+    dev = N.require_device(user_emb, post_emb, test_edges)
+    if user_emb.dtype != torch.float32 or post_emb.dtype != torch.float32:
+        raise TypeError("evaluate: fp32 embeddings expected (the reference dtype)")
+    nu = int(user_emb.shape[0]) if num_users is None else int(num_users)
+    g = _Grouped(test_edges, nu, int(post_emb.shape[0]))
+    n_rows, C = int(g.users.numel()), int(g.cand.numel())
+    if n_rows == 0:
+        return math.nan, math.nan                         # np.mean([]) in the reference
+    ld = (C + 3) // 4 * 4                                  # 16-B aligned score rows
+    P_c = post_emb.new_zeros(ld, post_emb.shape[1])        # candidates, zero-padded to ld
+    P_c[:C] = post_emb.index_select(0, g.cand)
+    recall = torch.empty(n_rows, dtype=torch.float64, device=dev)
+    ndcg = torch.empty(n_rows, dtype=torch.float64, device=dev)
+    rows = max(1, min(n_rows, batch_scores // ld))
+    buf = torch.empty(rows, ld, dtype=torch.float32, device=dev)
+    lib = N.lib()
+    for r0 in range(0, n_rows, rows):
+        r1 = min(n_rows, r0 + rows)
+        S = buf[: r1 - r0]                                 # columns >= C (padding) are ignored
+        torch.mm(user_emb.index_select(0, g.users[r0:r1]), P_c.T, out=S)
+        N.check(lib.hgnn_topk_metrics(
+            N.ptr(S), r1 - r0, C, ld, N.ptr(g.rowptr[r0:]), N.ptr(g.true_cand),
+            N.ptr(g.true_count[r0:]), K, None, N.ptr(recall[r0:]), N.ptr(ndcg[r0:]),
+            N.stream_ptr(dev)), "hgnn_topk_metrics")
+    return float(recall.mean()), float(ndcg.mean())
+
+
+def topk_metrics(scores: torch.Tensor, true_rowptr: torch.Tensor, true_cand: torch.Tensor,
+                 true_count: torch.Tensor, K: int = 10):
+    """Raw kernel: per-row (topk_idx, recall, ndcg) of a [rows, C] score matrix."""
+    dev = N.require_device(scores, true_rowptr, true_cand, true_count)
+    n, C = scores.shape
+    k = min(K, C)
+    topk = torch.empty(n, k, dtype=torch.int32, device=dev)
+    recall = torch.empty(n, dtype=torch.float64, device=dev)
+    ndcg = torch.empty(n, dtype=torch.float64, device=dev)
+    N.check(N.lib().hgnn_topk_metrics(
+        N.ptr(scores), n, C, scores.stride(0), N.ptr(true_rowptr), N.ptr(true_cand),
+        N.ptr(true_count), K, N.ptr(topk), N.ptr(recall), N.ptr(ndcg), N.stream_ptr(dev)),
+        "hgnn_topk_metrics")
+    return topk, recall, ndcg
