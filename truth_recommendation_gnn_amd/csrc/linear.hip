@@ -593,11 +593,12 @@ static int fast_grid(int64_t n_tiles) {
 //   * ds_read_b128 where lanes (i, g) read row i, columns 4g..4g+3: stride = 8 (mod 16) dwords
 //     (row i lands on 16-B slot 2i + g: even/odd by g, 8 distinct per b128 lane group);
 //   * ds_read_b32 where lanes (i, g) read row g, column i: stride = 16 (mod 32) dwords.
+constexpr int kMaxChunks = 16;   // K <= 256
 struct ChunkTab {
-  const float* x[8];
-  float* dx[8];
-  int32_t ld[8];
-  int32_t col[8];   // first column of the chunk inside its segment
+  const float* x[kMaxChunks];
+  float* dx[kMaxChunks];
+  int32_t ld[kMaxChunks];
+  int32_t col[kMaxChunks];   // first column of the chunk inside its segment
 };
 
 // Forward: out = act(X @ W^T + b); W [H][K+8] in LDS (b128 fragments), A fragments prefetched.
@@ -667,7 +668,7 @@ __global__ void __launch_bounds__(256) k_linear_fwd_v3(const LinArgs a, const Ch
 // the current tile's MFMAs.  Output tiles are computed transposed (out^T = W X^T) so every lane
 // stores one float4 per 16 output columns.
 template <int H, int K>
-__global__ void __launch_bounds__(512, (H <= 64 ? 4 : 3)) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
+__global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 : 2))) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
                                                        int64_t n_tiles) {
   constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
   __shared__ __attribute__((aligned(16))) float ws[H * LDW];
@@ -1078,6 +1079,16 @@ static size_t v4_bwd_lds(int h, int k, bool dx) {
          4;
 }
 
+// the persistent forward also takes K = 256 (W: H*(K+8)*4 <= 135 KB of LDS, one block per CU)
+static bool fwd4_ok(const LinArgs& a, bool vec) {
+  if (!vec || !(a.h == 64 || a.h == 128) ||
+      !(a.k_total == 64 || a.k_total == 128 || a.k_total == 256))
+    return false;
+  for (int s = 0; s < a.n_seg; ++s)
+    if (a.seg[s].k % 16) return false;
+  return true;
+}
+
 static bool v3_ok(const LinArgs& a, bool vec) {
   if (!vec || !(a.h == 64 || a.h == 128) || !(a.k_total == 64 || a.k_total == 128)) return false;
   for (int s = 0; s < a.n_seg; ++s)
@@ -1096,7 +1107,7 @@ static int v3_bwd_grid(int64_t n_tiles, int h, int k, bool dx) {
 
 static ChunkTab chunk_table(const LinArgs& a) {
   ChunkTab t{};
-  for (int c = 0; c < a.k_total / 16 && c < 8; ++c) {
+  for (int c = 0; c < a.k_total / 16 && c < kMaxChunks; ++c) {
     const int k = c * 16;
     int s = 0;
     while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
@@ -1152,7 +1163,7 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.out = out;
   a.relu = relu;
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
-  if (v3_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
+  if (fwd4_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
     const ChunkTab tab = chunk_table(a);
     const int64_t n_tiles = cdiv(n_rows, 16);
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) /
@@ -1160,14 +1171,17 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
                                                                       256 * per_cu))),
         block(512);
-    if (h == 64 && a.k_total == 128)
-      hipLaunchKernelGGL((k_linear_fwd_v4<64, 128>), grid, block, 0, stream, a, tab, n_tiles);
-    else if (h == 64)
-      hipLaunchKernelGGL((k_linear_fwd_v4<64, 64>), grid, block, 0, stream, a, tab, n_tiles);
-    else if (a.k_total == 128)
-      hipLaunchKernelGGL((k_linear_fwd_v4<128, 128>), grid, block, 0, stream, a, tab, n_tiles);
-    else
-      hipLaunchKernelGGL((k_linear_fwd_v4<128, 64>), grid, block, 0, stream, a, tab, n_tiles);
+#define HGNN_FWD4(HV, KV) \
+  hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV>), grid, block, 0, stream, a, tab, n_tiles)
+    switch (h * 1000 + a.k_total) {
+      case 64064: HGNN_FWD4(64, 64); break;
+      case 64128: HGNN_FWD4(64, 128); break;
+      case 64256: HGNN_FWD4(64, 256); break;
+      case 128064: HGNN_FWD4(128, 64); break;
+      case 128128: HGNN_FWD4(128, 128); break;
+      default: HGNN_FWD4(128, 256); break;
+    }
+#undef HGNN_FWD4
     return check_launch("k_linear_fwd_v4");
   }
   if (v3_ok(a, vec)) {
