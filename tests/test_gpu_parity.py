@@ -165,8 +165,9 @@ def _linear_bwd_ref(segs, w, dout, out_act):
     return list(dx.split([s.shape[1] for s in segs], 1)), dz.T @ x, dz.sum(0)
 
 
-@pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 64), ([64, 64], 128), ([16, 48], 128)])
-@pytest.mark.parametrize("mode", ["no_relu", "dx_subset", "wgrad_only", "db_only"])
+@pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 64), ([64, 64], 128), ([16, 48], 128),
+                                  ([128, 128], 128), ([128, 128], 64), ([64, 64, 128], 128)])
+@pytest.mark.parametrize("mode", ["no_relu", "dx_subset", "wgrad_only", "db_only", "dgrad_only"])
 def test_linear_bwd_variants(ks, h, mode):
     """The compile-time-shape K3 backward (two-role, double-buffered tiles) under every operand
     combination the layers use: no activation mask, dX for a subset of segments, dW/db only."""
@@ -187,9 +188,10 @@ def test_linear_bwd_variants(ks, h, mode):
         dxs = [None] * len(ks)
     elif mode == "dx_subset":
         dxs[0] = None
-    need_w = mode != "db_only"
+    need_w = mode not in ("db_only", "dgrad_only")
+    need_b = mode != "dgrad_only"
     dw, db = ops.linear_bwd(dsegs, w.to(DEV), dout.to(DEV), out if relu else None, dxs,
-                            need_w, True)
+                            need_w, need_b)
     for gx, r in zip(dxs, ref_dx):
         if gx is not None:
             close(gx, r)
@@ -197,7 +199,8 @@ def test_linear_bwd_variants(ks, h, mode):
         close(dw, ref_dw)
     else:
         assert dw is None
-    close(db, ref_db)
+    if need_b:
+        close(db, ref_db)
 
 
 # ----------------------------------------------------------------------------- models

@@ -900,10 +900,15 @@ __global__ void __launch_bounds__(256) k_linear_bwd_v3(const LinArgs a, const Ch
 // tiles are double-buffered, so with one barrier per tile the dgrad of tile t+1 (dz waves) runs
 // beside the wgrad of tile t (X waves) on every SIMD: MFMA issue from one role hides the memory
 // waits of the other.
-template <int H, int K, bool DX>
+// T = 32 (wgrad-only, for K = 256 whose X tiles would not fit twice at T = 64): the two 16-row
+// slices of a tile go to dz waves (w & 1), each loading half of the columns (w >> 1).
+template <int H, int K, bool DX, int T = 64>
 __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const ChunkTab tab,
                                                        int64_t n_tiles) {
-  constexpr int T = 64, HC = H / 16, KC = K / 16;
+  static_assert(T == 64 || (T == 32 && !DX), "dgrad needs one 16-row slice per dz wave");
+  constexpr int HC = H / 16, KC = K / 16;
+  constexpr int ZR = T / 16;                // 16-row slices per tile
+  constexpr int ZC = HC * ZR / 4;           // column chunks loaded per dz wave
   constexpr int JT = H / 64;                // wgrad j tiles per X wave
   constexpr int XQ = T * K / 4 / 256;       // X float4 per X-wave thread per tile
   constexpr int LWT = H + 8, LZ = H + 16, LX = K + 16;
@@ -915,6 +920,7 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
   const int i = lane & 15, g = lane >> 4;
   const bool zrole = wave < 4;
   const int w4 = wave & 3;
+  const int zrow = w4 % ZR, zcol0 = (w4 / ZR) * ZC;   // dz wave: row slice, first column chunk
   if (DX) {
     for (int idx = threadIdx.x; idx < H * K; idx += 512) {
       const int j = idx / K, k = idx % K;
@@ -925,11 +931,11 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
   const int64_t n_my = (n_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
   if (zrole) {
     auto load_dz = [&](int64_t it, float4 (&z)[HC]) {
-      const int64_t row = (blockIdx.x + it * gridDim.x) * T + w4 * 16 + i;
+      const int64_t row = (blockIdx.x + it * gridDim.x) * T + zrow * 16 + i;
 #pragma unroll
       for (int c = 0; c < HC; ++c) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (it < n_my && row < a.n) {
+        if (it < n_my && row < a.n && c >= zcol0 && c < zcol0 + ZC) {
           v = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
           if (a.out_act) {
             const float4 m =
@@ -948,16 +954,16 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
     const float* wt_r = wt + i * LWT + 4 * g;
     for (int64_t it = 0; it <= n_my; ++it) {
       if (it < n_my) {
-        float* dz_w = dzb + (it & 1) * T * LZ + (w4 * 16 + i) * LZ + 4 * g;
+        float* dz_w = dzb + (it & 1) * T * LZ + (zrow * 16 + i) * LZ + 4 * g;
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
-          *reinterpret_cast<float4*>(dz_w + c * 16) = zc[c];
+          if (c >= zcol0 && c < zcol0 + ZC) *reinterpret_cast<float4*>(dz_w + c * 16) = zc[c];
           dbacc[c].x += zc[c].x; dbacc[c].y += zc[c].y;
           dbacc[c].z += zc[c].z; dbacc[c].w += zc[c].w;
         }
         load_dz(it + 1, zn);
         if (DX) {
-          const int64_t row = (blockIdx.x + it * gridDim.x) * T + w4 * 16 + i;
+          const int64_t row = (blockIdx.x + it * gridDim.x) * T + zrow * 16 + i;
 #pragma unroll
           for (int ct = 0; ct < KC; ct += 2) {
             f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
@@ -1074,10 +1080,86 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
   }
 }
 
-static size_t v4_bwd_lds(int h, int k, bool dx) {
-  return ((dx ? (size_t)k * (h + 8) : 0) + (size_t)2 * 64 * (h + 16) + (size_t)2 * 64 * (k + 16)) *
+static size_t v4_bwd_lds(int h, int k, bool dx, int t = 64) {
+  return ((dx ? (size_t)k * (h + 8) : 0) + (size_t)2 * t * (h + 16) + (size_t)2 * t * (k + 16)) *
          4;
 }
+
+// dgrad alone, persistent: dX = (dout * [out > 0]) W with W^T staged in LDS once per block
+// ([K][H+8], conflict-free b128 fragments); each of the 8 waves streams its own 16-row tiles with
+// the next tile's masked dz fragments in flight, and computes dX^T = W^T dz^T so that every lane
+// stores float4 runs of its row.  Used with the wgrad-only kernel when the fused backward's LDS
+// (W^T + two dz and X tiles) does not fit: K = 256, or H = 128 with K = 128.
+template <int H, int K>
+__global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const ChunkTab tab,
+                                                         int64_t n_tiles) {
+  constexpr int HC = H / 16, KC = K / 16, LWT = H + 8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* wt = smem;   // [K][LWT]
+  for (int idx = threadIdx.x; idx < H * K; idx += 512) {
+    const int j = idx / K, k = idx % K;
+    wt[k * LWT + j] = a.w[(int64_t)j * K + k];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  auto load_dz = [&](int64_t t, float4 (&z)[HC]) {
+    const int64_t row = t * 16 + i;
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (row < a.n) {
+        v = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
+        if (a.out_act) {
+          const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * H + c * 16 + 4 * g);
+          v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
+          v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
+        }
+      }
+      z[c] = v;
+    }
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  float4 zc[HC], zn[HC];
+  if (t < n_tiles) load_dz(t, zc);
+  __syncthreads();
+  const int wr0 = i * LWT + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    if (t + nw < n_tiles) load_dz(t + nw, zn);
+    int wo = wr0;
+    asm volatile("" : "+v"(wo));   // keep W^T fragments as per-tile LDS reads (see fwd v4)
+    const float* wt_r = wt + wo;
+    const int64_t row = t * 16 + i;
+#pragma unroll
+    for (int ct = 0; ct < KC; ct += 2) {
+      f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+        const float4 b0 = *reinterpret_cast<const float4*>(wt_r + ct * 16 * LWT + c * 16);
+        const float4 b1 = *reinterpret_cast<const float4*>(wt_r + (ct + 1) * 16 * LWT + c * 16);
+        o0 = mfma4(b0.x, zc[c].x, o0); o1 = mfma4(b1.x, zc[c].x, o1);
+        o0 = mfma4(b0.y, zc[c].y, o0); o1 = mfma4(b1.y, zc[c].y, o1);
+        o0 = mfma4(b0.z, zc[c].z, o0); o1 = mfma4(b1.z, zc[c].z, o1);
+        o0 = mfma4(b0.w, zc[c].w, o0); o1 = mfma4(b1.w, zc[c].w, o1);
+      }
+      if (row < a.n) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          float* dx = tab.dx[ct + h2];
+          if (dx) {
+            const f32x4 o = h2 ? o1 : o0;
+            *reinterpret_cast<float4*>(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] + 4 * g) =
+                make_float4(o[0], o[1], o[2], o[3]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < HC; ++c) zc[c] = zn[c];
+  }
+}
+
+static size_t dgrad4_lds(int h, int k) { return (size_t)k * (h + 8) * 4; }
 
 // the persistent forward also takes K = 256 (W: H*(K+8)*4 <= 135 KB of LDS, one block per CU)
 static bool fwd4_ok(const LinArgs& a, bool vec) {
@@ -1270,30 +1352,63 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   }
   bool any_dx = false;
   for (int s = 0; s < n_seg; ++s) any_dx |= a.seg[s].dx != nullptr;
-  if (v3_ok(a, vec) && (dw || db) && ws && v4_bwd_lds(h, a.k_total, any_dx) <= 160 * 1024 &&
-      !getenv("HGNN_LIN_V3")) {
+  if (fwd4_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
+    // fused two-role backward when W^T and two dz / X tiles fit the LDS; otherwise persistent
+    // dgrad + wgrad-only (T = 32 tiles for K = 256)
     const ChunkTab tab = chunk_table(a);
-    const int64_t n_tiles = cdiv(n_rows, 64);
+    const int K = a.k_total;
+    const bool fused = any_dx && (dw || db) && K <= 128 && v4_bwd_lds(h, K, true) <= 160 * 1024;
+    if (any_dx && !fused) {
+      const int64_t n16 = cdiv(n_rows, 16);
+      const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
+          block(512);
+      const size_t lds = dgrad4_lds(h, K);
+#define HGNN_DG4(HV, KV) \
+  hipLaunchKernelGGL((k_linear_dgrad_v4<HV, KV>), grid, block, lds, stream, a, tab, n16)
+      switch (h * 1000 + K) {
+        case 64064: HGNN_DG4(64, 64); break;
+        case 64128: HGNN_DG4(64, 128); break;
+        case 64256: HGNN_DG4(64, 256); break;
+        case 128064: HGNN_DG4(128, 64); break;
+        case 128128: HGNN_DG4(128, 128); break;
+        default: HGNN_DG4(128, 256); break;
+      }
+#undef HGNN_DG4
+      if (int rc = check_launch("k_linear_dgrad_v4")) return rc;
+    }
+    if (!(dw || db)) return HGNN_OK;
+    if (!ws) return fail(HGNN_E_WS, "linear_bwd: weight gradients need the workspace");
+    const int T = v4_bwd_lds(h, K, fused, 64) <= 160 * 1024 ? 64 : 32;
+    const int64_t n_tiles = cdiv(n_rows, T);
     const int G = (int)std::min<int64_t>(n_tiles, 256);
-    const size_t lds = v4_bwd_lds(h, a.k_total, any_dx);
-    const size_t need = (size_t)G * h * (a.k_total + 1) * 4;
+    const size_t lds = v4_bwd_lds(h, K, fused, T);
+    const size_t need = (size_t)G * h * (K + 1) * 4;
     if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
     a.slab = static_cast<float*>(ws);
     const dim3 grid(G), block(512);
-#define HGNN_BWD4(HV, KV)                                                                      \
-  if (any_dx) hipLaunchKernelGGL((k_linear_bwd_v4<HV, KV, true>), grid, block, lds, stream, a,  \
-                                 tab, n_tiles);                                                \
-  else hipLaunchKernelGGL((k_linear_bwd_v4<HV, KV, false>), grid, block, lds, stream, a, tab,   \
-                          n_tiles);
-    if (h == 64 && a.k_total == 128) { HGNN_BWD4(64, 128) }
-    else if (h == 64) { HGNN_BWD4(64, 64) }
-    else if (a.k_total == 128) { HGNN_BWD4(128, 128) }
-    else { HGNN_BWD4(128, 64) }
+#define HGNN_BWD4(HV, KV, DXV, TV) \
+  hipLaunchKernelGGL((k_linear_bwd_v4<HV, KV, DXV, TV>), grid, block, lds, stream, a, tab, n_tiles)
+    if (fused) {
+      switch (h * 1000 + K) {
+        case 64064: HGNN_BWD4(64, 64, true, 64); break;
+        case 64128: HGNN_BWD4(64, 128, true, 64); break;
+        default: HGNN_BWD4(128, 64, true, 64); break;
+      }
+    } else {
+      switch (h * 1000 + K) {
+        case 64064: HGNN_BWD4(64, 64, false, 64); break;
+        case 64128: HGNN_BWD4(64, 128, false, 64); break;
+        case 64256: HGNN_BWD4(64, 256, false, 32); break;
+        case 128064: HGNN_BWD4(128, 64, false, 64); break;
+        case 128128: HGNN_BWD4(128, 128, false, 64); break;
+        default: HGNN_BWD4(128, 256, false, 32); break;
+      }
+    }
 #undef HGNN_BWD4
     if (int rc = check_launch("k_linear_bwd_v4")) return rc;
-    const int64_t total = (int64_t)h * (a.k_total + 1);
+    const int64_t total = (int64_t)h * (K + 1);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                       a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
+                       a.slab, (int64_t)G, h, K + 1, dw, db);
     return check_launch("k_wgrad_reduce");
   }
   if (v3_ok(a, vec) && (dw || db) && ws) {
