@@ -133,3 +133,24 @@ def test_evaluate_edge_cases():
     assert math.isnan(r)
     with pytest.raises(ValueError):
         evaluate(torch.tensor([[0], [1]], device=DEV), U, P)        # post id < num_users
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,C,K", [(50, 1000, 10), (3, 7, 10), (300, 4097, 25)])
+def test_recommend_matches_topk(n, C, K):
+    """inference.py:427-429: torch.topk over user_emb @ known_post_emb.T, batched over users."""
+    from truth_recommendation_gnn_amd import recommend
+    rng = np.random.default_rng(C)
+    U = torch.from_numpy(rng.integers(-3, 4, size=(n, 16)).astype(np.float32))
+    P = torch.from_numpy(rng.integers(-3, 4, size=(C, 16)).astype(np.float32))
+    S = U @ P.T                                   # exact (integers): CPU == GPU scores
+    s, i = recommend(U.to(DEV), P.to(DEV), K, batch_scores=64 * C)
+    k = min(K, C)
+    assert s.shape == (n, k) and i.shape == (n, k)
+    for r in range(n):
+        order = sorted(range(C), key=lambda j: (-float(S[r, j]), j))[:k]
+        assert i[r].tolist() == order
+        assert torch.equal(s[r].cpu(), S[r, order])
+    # ties aside, the same multiset of scores as torch.topk (what the reference returns)
+    ts, _ = torch.topk(S, k, dim=1)
+    assert torch.equal(s.cpu(), ts)

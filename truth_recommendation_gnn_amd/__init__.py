@@ -5,6 +5,6 @@ reference's PyG-style Python surface (``SAGEConv``, ``HeteroData``, ``WeightedRG
 from .graph import HeteroData, RelationCSR, relation_csr, CSR_CACHE  # noqa: F401
 from .nn import SAGEConv, WeightedRGCN, WeightedRGCNAuthor, HeteroSAGE  # noqa: F401
 from . import ops, synth  # noqa: F401
-from .metrics import evaluate  # noqa: F401
+from .metrics import evaluate, recommend  # noqa: F401
 
 __version__ = "0.1.0"

@@ -90,3 +90,40 @@ def topk_metrics(scores: torch.Tensor, true_rowptr: torch.Tensor, true_cand: tor
         N.ptr(true_count), K, N.ptr(topk), N.ptr(recall), N.ptr(ndcg), N.stream_ptr(dev)),
         "hgnn_topk_metrics")
     return topk, recall, ndcg
+
+
+def recommend(user_emb: torch.Tensor, post_emb: torch.Tensor, K: int = 10,
+              batch_scores: int = 1 << 30) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-K posts for every user row: ``(topk_scores, topk_indices)``, each ``[n_users, k]``,
+    k = min(K, n_posts) — the scoring of ``recommend_for_user_inductive`` (inference.py:427-429:
+    ``torch.topk(user_emb @ known_post_emb.T, min(K, len(scores)))``) for a whole batch of users
+    at once.  Scores descend; equal scores list the lower post index first."""
+    dev = N.require_device(user_emb, post_emb)
+    if user_emb.dtype != torch.float32 or post_emb.dtype != torch.float32:
+        raise TypeError("recommend: fp32 embeddings expected (the reference dtype)")
+    n, C = int(user_emb.shape[0]), int(post_emb.shape[0])
+    if C == 0:
+        raise ValueError("recommend: no posts to rank")
+    k = min(K, C)
+    ld = (C + 3) // 4 * 4
+    P_c = post_emb.new_zeros(ld, post_emb.shape[1])
+    P_c[:C] = post_emb
+    out_s = torch.empty(n, k, dtype=torch.float32, device=dev)
+    out_i = torch.empty(n, k, dtype=torch.int32, device=dev)
+    if n == 0:
+        return out_s, out_i.long()
+    rows = max(1, min(n, batch_scores // ld))
+    buf = torch.empty(rows, ld, dtype=torch.float32, device=dev)
+    no_rel = torch.zeros(rows + 1, dtype=torch.int32, device=dev)   # empty relevance sets
+    scratch = torch.empty(2, rows, dtype=torch.float64, device=dev)
+    lib = N.lib()
+    for r0 in range(0, n, rows):
+        r1 = min(n, r0 + rows)
+        S = buf[: r1 - r0]
+        torch.mm(user_emb[r0:r1], P_c.T, out=S)
+        N.check(lib.hgnn_topk_metrics(
+            N.ptr(S), r1 - r0, C, ld, N.ptr(no_rel), N.ptr(no_rel), N.ptr(no_rel), K,
+            N.ptr(out_i[r0:r1]), N.ptr(scratch[0]), N.ptr(scratch[1]), N.stream_ptr(dev)),
+            "hgnn_topk_metrics")
+        out_s[r0:r1] = S.gather(1, out_i[r0:r1].long())
+    return out_s, out_i.long()
