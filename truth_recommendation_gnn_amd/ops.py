@@ -491,6 +491,25 @@ def mean_gather(x_src: torch.Tensor, csr: RelationCSR) -> torch.Tensor:
     return _GatherMean.apply(x_src, csr)
 
 
+# Gradients still being produced by an in-flight collective (parallel.py issues the adjoint of
+# its post-table all-reduce asynchronously): the consumer below waits on the collective right
+# before its first kernel, so the user-side backward kernels scheduled in between overlap it.
+_PENDING: Dict[int, Tuple[torch.Tensor, object]] = {}
+
+
+def defer_until(t: torch.Tensor, work) -> torch.Tensor:
+    """Register ``t`` as not yet valid until ``work.wait()`` (a torch.distributed Work)."""
+    _PENDING[id(t)] = (t, work)
+    return t
+
+
+def await_pending(t: torch.Tensor) -> torch.Tensor:
+    entry = _PENDING.pop(id(t), None)
+    if entry is not None and entry[0] is t:
+        entry[1].wait()   # NCCL: the current stream waits on the collective (no host sync)
+    return t
+
+
 class _GatherWeighted(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_src, csr: RelationCSR, w_fwd, w_bwd):
@@ -505,6 +524,7 @@ class _GatherWeighted(torch.autograd.Function):
         if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
             return None, None, None, None
         csr = ctx.csr
+        await_pending(g)
         out = torch.empty(csr.n_src, g.shape[1], dtype=torch.float32, device=g.device)
         _gather(g.contiguous(), csr.bwd, None, csr_mean=False, out=out, accumulate=False,
                 edge_w=ctx.w_bwd)

@@ -20,7 +20,9 @@ graph is partitioned by USER (contiguous id ranges, the 10x larger node type):
   per-rank losses add up to the reference loss (``train_gnn.py:259-281``).
 
 Exchanged per step: 3 post-sized all-reduces (layer-1 and layer-2 post aggregates forward, the
-layer-2 post-aggregate gradient backward) + the weight gradients.  The compute ops are injected
+layer-2 post-aggregate gradient backward) + the weight gradients.  All three are asynchronous:
+the forward ones overlap the user-side gather + projection of the same layer, the backward one
+overlaps the user-side backward that autograd runs before its consumer.  The compute ops are injected
 (``HipImpl`` here; the CPU gloo tests inject plain-torch ops to check the partitioning logic).
 """
 from __future__ import annotations
@@ -56,22 +58,66 @@ class DistEnv:
             dist.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_async(self, t: torch.Tensor):
+        """Start an in-place all-reduce; ``.wait()`` on the result before reading ``t`` (with
+        NCCL/RCCL that is a stream wait, so kernels enqueued in between overlap the collective)."""
+        if self.world > 1:
+            return dist.all_reduce(t, group=self.group, async_op=True)
+        return _Done()
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+class Pending:
+    """Handle of an in-flight forward all-reduce (see ``all_reduce_sum``)."""
+    work = None
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+
 
 class _AllReduceSum(torch.autograd.Function):
-    """y = sum over ranks of x (replicated result); adjoint: the same all-reduce of gradients."""
+    """y = sum over ranks of x (replicated result); adjoint: the same all-reduce of gradients.
+
+    Both directions are issued asynchronously.  Forward: the caller gets ``handle`` and waits on
+    it right before consuming y, after enqueueing independent work.  Backward (``defer_grad``):
+    the gradient is handed on with the collective still in flight, registered with
+    ``ops.defer_until``; its consumer (``ops.weighted_gather``'s backward) waits on it, so the
+    autograd nodes that run in between — the user-side backward — overlap it."""
 
     @staticmethod
-    def forward(ctx, x, env: DistEnv):
-        ctx.env = env
-        return env.all_reduce_(x.contiguous().clone())
+    def forward(ctx, x, env: DistEnv, handle: "Pending", defer_grad: bool):
+        ctx.env, ctx.defer = env, defer_grad
+        y = x.contiguous().clone()
+        handle.work = env.all_reduce_async(y)
+        return y
 
     @staticmethod
     def backward(ctx, g):
-        return ctx.env.all_reduce_(g.contiguous().clone()), None
+        g = g.contiguous().clone()
+        work = ctx.env.all_reduce_async(g)
+        if ctx.defer and ctx.env.world > 1:
+            ops.defer_until(g, work)
+        else:
+            work.wait()
+        return g, None, None, None
 
 
-def all_reduce_sum(x: torch.Tensor, env: DistEnv) -> torch.Tensor:
-    return _AllReduceSum.apply(x, env)
+def all_reduce_sum(x: torch.Tensor, env: DistEnv, handle: Optional[Pending] = None,
+                   defer_grad: bool = False) -> torch.Tensor:
+    """Sum over ranks.  Without ``handle`` the result is ready on return; with one, call
+    ``handle.wait()`` before using it."""
+    own = handle is None
+    handle = handle or Pending()
+    y = _AllReduceSum.apply(x, env, handle, defer_grad)
+    if own:
+        handle.wait()
+    return y
 
 
 def user_range(n_users: int, world: int, rank: int) -> Tuple[int, int]:
@@ -82,6 +128,9 @@ def user_range(n_users: int, world: int, rank: int) -> Tuple[int, int]:
 
 class HipImpl:
     """The MI355X kernels behind the partitioned step."""
+
+    # weighted_gather's backward awaits a gradient whose all-reduce is still in flight
+    defer_grad = True
 
     def relation(self, edge_index, n_src, n_dst):
         return relation_csr(edge_index, n_src, n_dst)   # cached: the loss finds the same one
@@ -151,10 +200,13 @@ class UserShard:
             shapes = {"user": h_u, "post": h_p}
             Wu, bu = _fused_weights(convs, [(nu, REV_ENGAGES, wts[REV_ENGAGES])], shapes)
             Wp, bp = _fused_weights(convs, [(np_, ENGAGES, wts[ENGAGES])], shapes)
+            # post partial sums first, their all-reduce in flight during the user-side layer
             s_post = impl.weighted_gather(h_u, self.rel_eng, self.w_eng_fwd, self.w_eng_bwd)
+            pend = Pending()
+            a_post = all_reduce_sum(s_post, env, pend, getattr(impl, "defer_grad", False))
             a_user = impl.mean_gather(h_p, self.rel_rev)
             h_u_next = impl.fused_linear([a_user, h_u], Wu, bu, True)
-            a_post = all_reduce_sum(s_post, env)
+            pend.wait()
             h_p_next = impl.fused_linear([a_post, h_p], Wp, bp, True)
             h_u, h_p = h_u_next, h_p_next
         return h_u, h_p
