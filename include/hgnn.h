@@ -160,6 +160,26 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
                         int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
                         hgnn_stream_t stream);
 
+/* ---- neighbour sampling for mini-batches (BASELINE cfg5; no reference counterpart) -----------
+ * For each destination dst_ids[i] (rows of a destination-grouped CSR rowptr/col over n_rows):
+ * keep all in-neighbours if deg <= fanout (or fanout < 0), else `fanout` distinct neighbour
+ * positions drawn uniformly (Floyd's algorithm, counter-based hash of (seed, dst id, draw)).
+ * out_rowptr[n_dst+1] is written first; with out_col == NULL only the counts are produced (read
+ * out_rowptr[n_dst] to size out_col).  fanout in 1..64 or < 0.  ws: hgnn_sample_ws_bytes(n_dst). */
+size_t hgnn_sample_ws_bytes(int64_t n_dst);
+int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                          const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
+                          int32_t* out_rowptr, int32_t* out_col, void* ws, size_t ws_bytes,
+                          hgnn_stream_t stream);
+/* Next layer's node set of one type: nodes_out = [prefix (order kept), then every item id not in
+ * prefix, once, ascending]; local_out[k] = position of items[k] in nodes_out; *d_count = total.
+ * Ids in [0, n_nodes); prefix ids distinct.  nodes_out holds n_prefix + n_items entries.
+ * ws: hgnn_relabel_ws_bytes(n_nodes) (three dense n_nodes maps). */
+size_t hgnn_relabel_ws_bytes(int64_t n_nodes);
+int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
+                 int64_t n_nodes, int32_t* local_out, int32_t* nodes_out, int32_t* d_count,
+                 void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of
  * user and candidate embeddings, computed by the caller).  Per row:

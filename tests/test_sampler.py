@@ -1,0 +1,170 @@
+"""Neighbour-sampled mini-batches (sampler.py, csrc/sampler.hip; BASELINE cfg5).
+
+No reference counterpart exists (the reference trains full-batch), so parity is anchored on the
+full-graph oracle: with fanouts covering every degree the mini-batch forward must equal the
+full-graph forward on the seeds.  With real fanouts, the blocks are checked against a plain-torch
+forward/backward over the same sampled edges, and the sampler itself by its defining properties.
+"""
+import collections
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sage_ref
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _rand_csr_graph(rng, n_src, n_dst, E):
+    src = rng.integers(0, n_src, size=E)
+    dst = (n_dst * rng.random(E) ** 2).astype(np.int64)      # skewed in-degrees
+    return torch.from_numpy(np.stack([src, dst]).astype(np.int64))
+
+
+def test_sample_neighbors_properties():
+    from truth_recommendation_gnn_amd import graph, sampler
+    rng = np.random.default_rng(0)
+    ei = _rand_csr_graph(rng, 500, 300, 20000)
+    s = sampler.NeighborSampler({"a": 500, "b": 300}, {("a", "r", "b"): ei.to(DEV)},
+                                [("a", "r", "b")], [7])
+    dst = torch.from_numpy(rng.permutation(300)[:200].astype(np.int32)).to(DEV)
+    rp, col = s._sample(("a", "r", "b"), dst, 7, 123)
+    rp2, col2 = s._sample(("a", "r", "b"), dst, 7, 123)
+    assert torch.equal(rp, rp2) and torch.equal(col, col2)          # deterministic
+    _, col3 = s._sample(("a", "r", "b"), dst, 7, 124)
+    assert not torch.equal(col, col3)                                # seed-dependent
+    nbrs = collections.defaultdict(list)
+    for u, v in ei.t().tolist():
+        nbrs[v].append(u)
+    rp, col = rp.cpu().tolist(), col.cpu().tolist()
+    for i, d in enumerate(dst.cpu().tolist()):
+        got = col[rp[i]:rp[i + 1]]
+        assert len(got) == min(len(nbrs[d]), 7)
+        have = collections.Counter(nbrs[d])
+        assert not (collections.Counter(got) - have)                 # a sub-multiset
+        if len(nbrs[d]) <= 7:
+            assert sorted(got) == sorted(nbrs[d])
+
+
+def test_sample_is_uniform_without_replacement():
+    from truth_recommendation_gnn_amd import sampler
+    deg, k, trials = 40, 5, 4000
+    ei = torch.stack([torch.arange(deg), torch.zeros(deg, dtype=torch.int64)])
+    s = sampler.NeighborSampler({"a": deg, "b": 1}, {("a", "r", "b"): ei.to(DEV)},
+                                [("a", "r", "b")], [k])
+    dst = torch.zeros(1, dtype=torch.int32, device=DEV)
+    hits = np.zeros(deg)
+    for t in range(trials):
+        _, col = s._sample(("a", "r", "b"), dst, k, t)
+        c = col.cpu().numpy()
+        assert len(set(c.tolist())) == k                              # no repeats
+        hits[c] += 1
+    expect = trials * k / deg
+    assert np.abs(hits - expect).max() < 5 * np.sqrt(expect)          # ~uniform
+
+
+def test_relabel_prefix_then_new_ids_ascending():
+    from truth_recommendation_gnn_amd import sampler
+    rng = np.random.default_rng(1)
+    n = 1000
+    prefix = rng.permutation(n)[:50].astype(np.int32)
+    items = rng.integers(0, n, size=3000).astype(np.int32)
+    items[:40] = prefix[:40]
+    ei = torch.zeros(2, 1, dtype=torch.int64, device=DEV)
+    s = sampler.NeighborSampler({"a": n}, {("a", "r", "a"): ei}, [("a", "r", "a")], [3])
+    nodes, local = s._relabel("a", torch.from_numpy(prefix).to(DEV), torch.from_numpy(items).to(DEV))
+    nodes, local = nodes.cpu().numpy(), local.cpu().numpy()
+    assert np.array_equal(nodes[:50], prefix)
+    new = sorted(set(items.tolist()) - set(prefix.tolist()))
+    assert nodes[50:].tolist() == new
+    assert np.array_equal(nodes[local], items)
+
+
+def _cfg5_tiny():
+    from truth_recommendation_gnn_amd import synth
+    cfg = synth.scaled("cfg5", 0.00004)           # 360 users, 40 posts, 8k engages, 4 relations
+    cfg = synth.dataclasses.replace(cfg, dim=16, hidden=16)
+    g = synth.make_graph(cfg)
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
+            (synth.POST_POST, 0.5)]
+    return cfg, g, rels
+
+
+def _model(cfg, rels):
+    from truth_recommendation_gnn_amd import HeteroSAGE
+    names = []
+    for l in range(2):
+        for et, _ in rels:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (16, 16)), (f"{p}.lin_l.bias", (16,)),
+                      (f"{p}.lin_r.weight", (16, 16))]
+    params = sage_ref.init_params(names)
+    m = HeteroSAGE(16, rels, num_layers=2).to(DEV)
+    m.load_state_dict(params)
+    return m, params
+
+
+def test_full_fanout_minibatch_equals_full_graph_forward():
+    from truth_recommendation_gnn_amd import sampler
+    cfg, g, rels = _cfg5_tiny()
+    model, params = _model(cfg, rels)
+    num = {"user": cfg.num_users, "post": cfg.num_posts}
+    ei = {et: e.to(DEV) for et, e in g.edge_index_dict.items()}
+    s = sampler.NeighborSampler(num, ei, [et for et, _ in rels], [-1, -1])
+    seeds = {"user": torch.arange(0, cfg.num_users, 7), "post": torch.arange(0, cfg.num_posts, 3)}
+    mb = s.sample(seeds, seed=5)
+    x = {t: v.to(DEV) for t, v in g.x_dict.items()}
+    got = sampler.forward_blocks(model, mb, x)
+    ref = sage_ref.hetero_sage(params, g.x_dict, g.edge_index_dict, rels, 2)
+    for t, ids in seeds.items():
+        r = ref[t][ids]
+        torch.testing.assert_close(got[t].cpu(), r, rtol=1e-4, atol=1e-5 * float(r.abs().max()))
+
+
+def _torch_blocks(params, rels, mb, x):
+    """Plain-torch forward over the same sampled blocks (CPU): the check for fanout < degree."""
+    h = {t: x[t][ids.long().cpu()] for t, ids in mb.nodes[0].items()}
+    for l, blk in enumerate(mb.blocks):
+        out = {}
+        for dst, n_dst in blk.n_dst.items():
+            acc = None
+            for et, w in rels:
+                if et[2] != dst or et not in blk.csr:
+                    continue
+                ei = blk.csr[et]._ei.cpu()
+                wl, bl, wr = sage_ref._conv_params(params, f"layers.{l}.{'__'.join(et)}")
+                m = sage_ref.sage_conv(h[et[0]], h[dst][:n_dst], ei, wl, bl, wr)
+                acc = w * m if acc is None else acc + w * m
+            out[dst] = torch.relu(acc) if acc is not None else h[dst][:n_dst]
+        h = out
+    return h
+
+
+def test_sampled_minibatch_forward_backward_match_torch_on_blocks():
+    from truth_recommendation_gnn_amd import sampler
+    cfg, g, rels = _cfg5_tiny()
+    model, params = _model(cfg, rels)
+    num = {"user": cfg.num_users, "post": cfg.num_posts}
+    ei = {et: e.to(DEV) for et, e in g.edge_index_dict.items()}
+    s = sampler.NeighborSampler(num, ei, [et for et, _ in rels], [5, 3])
+    seeds = {"user": torch.arange(3, cfg.num_users, 11), "post": torch.arange(0, cfg.num_posts, 4)}
+    mb = s.sample(seeds, seed=9)
+    assert all(b.csr[et].num_edges <= 5 * b.n_dst[et[2]] for b in mb.blocks[1:] for et in b.csr)
+    x = {t: v.to(DEV) for t, v in g.x_dict.items()}
+    got = sampler.forward_blocks(model, mb, x)
+    ref_params = {k: v.clone().requires_grad_() for k, v in params.items()}
+    ref = _torch_blocks(ref_params, rels, mb, g.x_dict)
+    gen = torch.Generator().manual_seed(0)
+    wts = {t: torch.randn(ref[t].shape, generator=gen) for t in ref}
+    loss = sum((got[t] * wts[t].to(DEV)).sum() for t in got)
+    loss.backward()
+    ref_loss = sum((ref[t] * wts[t]).sum() for t in ref)
+    ref_loss.backward()
+    for t in ref:
+        torch.testing.assert_close(got[t].detach().cpu(), ref[t].detach(), rtol=1e-4,
+                                   atol=1e-5 * float(ref[t].abs().max()))
+    for name, p in model.named_parameters():
+        r = ref_params[name].grad
+        torch.testing.assert_close(p.grad.cpu(), r, rtol=1e-4, atol=1e-5 * float(r.abs().max()))

@@ -1,0 +1,199 @@
+// Neighbour sampling for mini-batch training (BASELINE cfg5: fanout [15, 10], 4 relations).
+//
+// The reference trains full-batch (train_gnn.py:254) and has no sampler; SURVEY.md §8 f4 asks for
+// one so the 10M-node / 4-relation config runs on mini-batches.  Semantics follow the usual
+// layer-wise scheme (PyG NeighborLoader, replace=False): for every destination node of a layer
+// and every relation into its type, keep all in-neighbours if there are at most `fanout`, else a
+// uniform sample of `fanout` distinct neighbour positions (duplicate edges are distinct positions).
+//
+//   k_sample_count  counts[i] = min(deg(dst_i), fanout)          (fanout < 0: all neighbours)
+//   (exclusive scan -> the block's rowptr)
+//   k_sample_fill   one wave per destination: Floyd's k-of-n without replacement, the chosen
+//                   positions held one per lane ("already taken?" is one ballot); the random
+//                   draws come from a counter-based hash of (seed, global dst id, draw index), so
+//                   a node's sample does not depend on which batch it sits in, and runs repeat
+//   relabel         the next layer's node set: the current destination nodes first (their order
+//                   kept, so the root term is a prefix view), then every newly reached node in
+//                   ascending global id — a dense id->local map and one exclusive scan, no sort,
+//                   no atomics, deterministic.
+#include "hgnn_common.h"
+
+namespace hgnn {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// uniform integer in [0, m) from the draw (seed, node, r); Lemire's multiply-shift
+__device__ __forceinline__ uint32_t draw(uint64_t seed, int32_t node, int r, uint32_t m) {
+  const uint64_t h = splitmix64(seed * 0xD1B54A32D192ED03ull + ((uint64_t)(uint32_t)node << 8) +
+                                (uint64_t)r);
+  return (uint32_t)(((h >> 32) * (uint64_t)m) >> 32);
+}
+
+__global__ void k_sample_count(const int32_t* rowptr, const int32_t* dst_ids, int64_t n,
+                               int32_t fanout, int32_t* counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t d = dst_ids[i];
+  const int32_t deg = rowptr[d + 1] - rowptr[d];
+  counts[i] = (fanout < 0 || deg <= fanout) ? deg : fanout;
+}
+
+__global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, const int32_t* col,
+                                                     const int32_t* dst_ids, int64_t n,
+                                                     int32_t fanout, uint64_t seed,
+                                                     const int32_t* out_rowptr,
+                                                     int32_t* out_col) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n) return;
+  const int32_t d = dst_ids[w];
+  const int32_t beg = rowptr[d], deg = rowptr[d + 1] - beg;
+  int32_t* out = out_col + out_rowptr[w];
+  if (fanout < 0 || deg <= fanout) {   // keep every neighbour, in CSR order
+    for (int32_t j = lane; j < deg; j += 64) out[j] = col[beg + j];
+    return;
+  }
+  // Floyd: for jj = deg-k .. deg-1 draw t in [0, jj]; take t unless already taken, then jj
+  int32_t chosen = -1;
+  for (int r = 0; r < fanout; ++r) {
+    const int32_t jj = deg - fanout + r;
+    const int32_t t = (int32_t)draw(seed, d, r, (uint32_t)jj + 1u);
+    const bool taken = __ballot(lane < r && chosen == t) != 0ull;
+    if (lane == r) chosen = taken ? jj : t;
+  }
+  if (lane < fanout) out[lane] = col[beg + chosen];
+}
+
+__global__ void k_relabel_prefix(const int32_t* prefix, int64_t n_prefix, int32_t* map,
+                                 int32_t* nodes) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_prefix) return;
+  map[prefix[i]] = (int32_t)i;
+  nodes[i] = prefix[i];
+}
+
+__global__ void k_relabel_mark(const int32_t* items, int64_t n_items, const int32_t* map,
+                               int32_t* present) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_items) return;
+  const int32_t id = items[k];
+  if (map[id] < 0) present[id] = 1;   // same value from every writer
+}
+
+__global__ void k_relabel_assign(const int32_t* present, const int32_t* scan, int64_t n_nodes,
+                                 int64_t n_prefix, int32_t* map, int32_t* nodes) {
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n_nodes || !present[id]) return;
+  const int32_t local = (int32_t)(n_prefix + scan[id]);
+  map[id] = local;
+  nodes[local] = (int32_t)id;
+}
+
+__global__ void k_relabel_items(const int32_t* items, int64_t n_items, const int32_t* map,
+                                int32_t* local) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n_items) local[k] = map[items[k]];
+}
+
+__global__ void k_relabel_count(const int32_t* scan, int64_t n_nodes, int64_t n_prefix,
+                                int32_t* d_count) {
+  *d_count = (int32_t)(n_prefix + scan[n_nodes]);
+}
+
+static size_t relabel_ws(int64_t n_nodes) {
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n_nodes, nullptr, &scan_b, 0);
+  return 3 * align_up((size_t)(n_nodes + 1) * 4, 256) + scan_b + 256;
+}
+
+}  // namespace hgnn
+
+using namespace hgnn;
+
+extern "C" {
+
+int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                          const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
+                          int32_t* out_rowptr, int32_t* out_col, void* ws, size_t ws_bytes,
+                          hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (n_rows < 0 || n_dst < 0 || fanout == 0 || fanout > 64)
+    return fail(HGNN_E_ARG, "sample_neighbors: n_rows=%lld n_dst=%lld fanout=%d (1..64 or <0)",
+                (long long)n_rows, (long long)n_dst, fanout);
+  if (!out_rowptr || (n_dst > 0 && (!rowptr || !dst_ids)))
+    return fail(HGNN_E_ARG, "sample_neighbors: null pointer");
+  if (n_dst == 0) {
+    (void)hipMemsetAsync(out_rowptr, 0, sizeof(int32_t), stream);
+    return check_launch("sample_neighbors(empty)");
+  }
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n_dst, nullptr, &scan_b, stream);
+  const size_t need = align_up((size_t)n_dst * 4, 256) + scan_b;
+  if (ws_bytes < need) return fail(HGNN_E_WS, "sample_neighbors: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* counts = w.take<int32_t>(n_dst);
+  void* scan_ws = w.take<char>(scan_b);
+  hipLaunchKernelGGL(k_sample_count, dim3((unsigned)cdiv(n_dst, 256)), dim3(256), 0, stream,
+                     rowptr, dst_ids, n_dst, fanout, counts);
+  if (int rc = check_launch("k_sample_count")) return rc;
+  if (int rc = exclusive_scan_i32(counts, out_rowptr, n_dst, scan_ws, &scan_b, stream)) return rc;
+  if (!out_col) return HGNN_OK;   // count-only call
+  hipLaunchKernelGGL(k_sample_fill, dim3((unsigned)cdiv(n_dst, 4)), dim3(256), 0, stream, rowptr,
+                     col, dst_ids, n_dst, fanout, seed, out_rowptr, out_col);
+  return check_launch("k_sample_fill");
+}
+
+size_t hgnn_sample_ws_bytes(int64_t n_dst) {
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n_dst < 1 ? 1 : n_dst, nullptr, &scan_b, 0);
+  return align_up((size_t)(n_dst < 1 ? 1 : n_dst) * 4, 256) + scan_b + 256;
+}
+
+size_t hgnn_relabel_ws_bytes(int64_t n_nodes) { return relabel_ws(n_nodes < 1 ? 1 : n_nodes); }
+
+int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
+                 int64_t n_nodes, int32_t* local_out, int32_t* nodes_out, int32_t* d_count,
+                 void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (n_prefix < 0 || n_items < 0 || n_nodes < 0 || n_prefix > n_nodes)
+    return fail(HGNN_E_ARG, "relabel: bad sizes");
+  if (!d_count || (n_prefix > 0 && (!prefix || !nodes_out)) ||
+      (n_items > 0 && (!items || !local_out || !nodes_out)))
+    return fail(HGNN_E_ARG, "relabel: null pointer");
+  if (n_nodes == 0) {
+    (void)hipMemsetAsync(d_count, 0, sizeof(int32_t), stream);
+    return check_launch("relabel(empty)");
+  }
+  if (ws_bytes < relabel_ws(n_nodes)) return fail(HGNN_E_WS, "relabel: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* map = w.take<int32_t>(n_nodes + 1);
+  int32_t* present = w.take<int32_t>(n_nodes + 1);
+  int32_t* scan = w.take<int32_t>(n_nodes + 1);
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n_nodes, nullptr, &scan_b, stream);
+  void* scan_ws = w.take<char>(scan_b);
+  (void)hipMemsetAsync(map, 0xFF, (size_t)n_nodes * 4, stream);   // -1
+  (void)hipMemsetAsync(present, 0, (size_t)n_nodes * 4, stream);
+  if (n_prefix > 0)
+    hipLaunchKernelGGL(k_relabel_prefix, dim3((unsigned)cdiv(n_prefix, 256)), dim3(256), 0,
+                       stream, prefix, n_prefix, map, nodes_out);
+  if (n_items > 0)
+    hipLaunchKernelGGL(k_relabel_mark, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, stream,
+                       items, n_items, map, present);
+  if (int rc = exclusive_scan_i32(present, scan, n_nodes, scan_ws, &scan_b, stream)) return rc;
+  hipLaunchKernelGGL(k_relabel_assign, dim3((unsigned)cdiv(n_nodes, 256)), dim3(256), 0, stream,
+                     present, scan, n_nodes, n_prefix, map, nodes_out);
+  if (n_items > 0)
+    hipLaunchKernelGGL(k_relabel_items, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, stream,
+                       items, n_items, map, local_out);
+  hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(1), 0, stream, scan, n_nodes, n_prefix,
+                     d_count);
+  return check_launch("relabel");
+}
+
+}  // extern "C"

@@ -1,0 +1,159 @@
+"""Neighbour-sampled mini-batches for the hetero SAGE stack (BASELINE cfg5).
+
+The reference trains full-batch (``train_gnn.py:254``) and has no sampler.  This adds the usual
+layer-wise scheme so the 4-relation 10M-node config can train on mini-batches:
+
+* ``NeighborSampler(num_nodes, edge_index_dict, relations, fanouts)`` builds, once, the
+  destination-grouped CSR of every relation on the GPU (K5, cached like the full-batch path);
+* ``sample(seeds)`` walks outwards from the seed nodes: hop h keeps, for every frontier node and
+  every relation into its type, all in-neighbours or ``fanouts[h]`` of them drawn uniformly without
+  replacement (``hgnn_sample_neighbors``), then relabels the reached nodes into the next frontier
+  (``hgnn_relabel``: previous frontier first, order kept, then new nodes by ascending id);
+* each hop becomes one ``Block`` per layer: a ``RelationCSR`` per relation over local ids, so the
+  layer runs on the same K1/K2 gathers and K3 projections as the full graph;
+* ``forward_blocks(model, batch, x_dict)`` runs a ``HeteroSAGE`` on the blocks (differentiable).
+
+With fanouts at least the maximum degree, the seeds' embeddings equal the full-graph forward's
+(tested), which is the parity anchor for a component with no reference counterpart.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import torch
+
+from . import _native as N
+from . import ops
+from .graph import RelationCSR, relation_csr
+from .nn import HeteroSAGE, _fused_weights
+
+EdgeType = Tuple[str, str, str]
+
+
+@dataclasses.dataclass
+class Block:
+    """One layer of a mini-batch: ``csr[et]`` maps the layer's source nodes (local ids into
+    ``src_nodes``) to its destination nodes (a prefix of the source nodes of the same type)."""
+    csr: Dict[EdgeType, RelationCSR]
+    n_dst: Dict[str, int]
+    n_src: Dict[str, int]
+
+
+@dataclasses.dataclass
+class MiniBatch:
+    nodes: List[Dict[str, torch.Tensor]]   # nodes[0]: input nodes per type ... nodes[L]: seeds
+    blocks: List[Block]                    # blocks[l]: nodes[l] -> nodes[l+1]
+
+
+def _i32(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.int32).contiguous()
+
+
+class NeighborSampler:
+    def __init__(self, num_nodes: Mapping[str, int],
+                 edge_index_dict: Mapping[EdgeType, torch.Tensor],
+                 relations: Sequence[EdgeType], fanouts: Sequence[int]):
+        if any(f == 0 or f > 64 for f in fanouts):
+            raise ValueError("fanouts must be in 1..64, or < 0 for every neighbour")
+        self.num_nodes = {t: int(n) for t, n in num_nodes.items()}
+        self.relations = [tuple(et) for et in relations]
+        self.fanouts = list(fanouts)
+        # full-graph CSR per relation: rows = destinations, col = global source ids
+        self.csr = {et: relation_csr(edge_index_dict[et], self.num_nodes[et[0]],
+                                     self.num_nodes[et[2]]) for et in self.relations}
+        self.device = next(iter(edge_index_dict.values())).device
+
+    def _sample(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int):
+        g = self.csr[et].fwd
+        lib, dev = N.lib(), self.device
+        n = int(dst.numel())
+        rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+        ws = N.workspace(lib.hgnn_sample_ws_bytes(n), dev)
+        args = (N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst), n, fanout, seed,
+                N.ptr(rowptr))
+        N.check(lib.hgnn_sample_neighbors(*args, None, N.ptr(ws), ws.numel(),
+                                          N.stream_ptr(dev)), "hgnn_sample_neighbors")
+        total = int(rowptr[n])                                  # one host sync per relation
+        col = torch.empty(total, dtype=torch.int32, device=dev)
+        N.check(lib.hgnn_sample_neighbors(*args, N.ptr(col), N.ptr(ws), ws.numel(),
+                                          N.stream_ptr(dev)), "hgnn_sample_neighbors")
+        return rowptr, col
+
+    def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
+        lib, dev = N.lib(), self.device
+        n_nodes = self.num_nodes[t]
+        n_p, n_i = int(prefix.numel()), int(items.numel())
+        nodes = torch.empty(n_p + n_i, dtype=torch.int32, device=dev)
+        local = torch.empty(n_i, dtype=torch.int32, device=dev)
+        count = torch.empty(1, dtype=torch.int32, device=dev)
+        ws = N.workspace(lib.hgnn_relabel_ws_bytes(n_nodes), dev)
+        N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, n_nodes, N.ptr(local),
+                                 N.ptr(nodes), N.ptr(count), N.ptr(ws), ws.numel(),
+                                 N.stream_ptr(dev)), "hgnn_relabel")
+        return nodes[: int(count)], local
+
+    def sample(self, seeds: Mapping[str, torch.Tensor], seed: int = 0) -> MiniBatch:
+        cur: Dict[str, torch.Tensor] = {}
+        for t, s in seeds.items():
+            s = _i32(s.to(self.device))
+            if s.numel() and (int(s.min()) < 0 or int(s.max()) >= self.num_nodes[t]):
+                raise ValueError(f"seed ids of type {t!r} out of range")
+            if torch.unique(s).numel() != s.numel():
+                raise ValueError(f"seed ids of type {t!r} must be distinct")
+            cur[t] = s
+        nodes, blocks = [cur], []
+        for hop, fanout in enumerate(self.fanouts):
+            hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
+            sampled = {}
+            for et in self.relations:
+                if et[2] in cur:
+                    sampled[et] = self._sample(et, cur[et[2]], fanout, hop_seed)
+            nxt: Dict[str, torch.Tensor] = {}
+            local: Dict[EdgeType, torch.Tensor] = {}
+            for t in sorted(set(cur) | {et[0] for et in sampled}):
+                ets = [et for et in sampled if et[0] == t]
+                items = (torch.cat([sampled[et][1] for et in ets]) if ets else
+                         torch.empty(0, dtype=torch.int32, device=self.device))
+                prefix = cur.get(t, torch.empty(0, dtype=torch.int32, device=self.device))
+                nxt[t], loc = self._relabel(t, prefix, items.contiguous())
+                o = 0
+                for et in ets:
+                    n = int(sampled[et][1].numel())
+                    local[et] = loc[o:o + n]
+                    o += n
+            csrs = {}
+            for et, (rowptr, _) in sampled.items():
+                n_dst = int(cur[et[2]].numel())
+                deg = (rowptr[1:] - rowptr[:-1]).long()
+                dst_local = torch.repeat_interleave(
+                    torch.arange(n_dst, dtype=torch.int64, device=self.device), deg)
+                ei = torch.stack([local[et].long(), dst_local])
+                csrs[et] = RelationCSR(ei, int(nxt[et[0]].numel()), n_dst)
+            blocks.append(Block(csrs, {t: int(v.numel()) for t, v in cur.items()},
+                                {t: int(v.numel()) for t, v in nxt.items()}))
+            nodes.append(nxt)
+            cur = nxt
+        return MiniBatch(nodes[::-1], blocks[::-1])
+
+
+def forward_blocks(model: HeteroSAGE, batch: MiniBatch,
+                   x_dict: Mapping[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """``model`` on the sampled blocks; returns the seeds' embeddings per type (seed order)."""
+    if len(batch.blocks) != len(model.layers):
+        raise ValueError(f"{len(batch.blocks)} blocks for a {len(model.layers)}-layer model")
+    h = {t: x_dict[t].index_select(0, ids.long()) for t, ids in batch.nodes[0].items()}
+    for convs, blk in zip(model.layers, batch.blocks):
+        out = {}
+        for dst, n_dst in blk.n_dst.items():
+            msgs = [("__".join(et), et, w) for et, w in model.relations
+                    if et[2] == dst and et in blk.csr]
+            root = h[dst][:n_dst]
+            if not msgs:                      # no relation into this type: kept as is
+                out[dst] = root
+                continue
+            W, b = _fused_weights(convs, msgs, h)
+            aggrs = [ops.mean_gather(h[et[0]], blk.csr[et]) for _, et, _ in msgs]
+            out[dst] = ops.fused_linear(aggrs + [root.contiguous()], W, b, True)
+        h = out
+    return h
