@@ -66,11 +66,14 @@ def _worker(rank, world, port, q):
         res = {"rank": rank,
                "loss_err": abs(float(total) - float(ref_loss)) / abs(float(ref_loss)),
                "user_err": float((h_u.detach() - out["user"][lo:hi]).abs().max()),
-               "post_err": float((h_p.detach() - out["post"]).abs().max()),
+               "post_err": float((h_p.detach()[:cfg.num_posts] - out["post"]).abs().max()),
                "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
                                max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
                "n_local": int(shard.pos_local.shape[1]), "n_total": int(pos.shape[1])}
         q.put(res)
+    except Exception as e:   # report instead of leaving the parent waiting on the queue
+        q.put({"rank": rank, "error": repr(e)})
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -84,6 +87,8 @@ def test_user_sharded_step_matches_single_process_oracle(world):
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
+    errs = [r["error"] for r in res if "error" in r]
+    assert not errs, errs
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

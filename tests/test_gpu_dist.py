@@ -49,7 +49,7 @@ def _worker(rank, world, port, q):
         torch.cuda.synchronize()
         if rank == 0:
             q.put((float(total), {n: p.grad.cpu().numpy() for n, p in model.named_parameters()},
-                   h_p.detach().cpu().numpy()))
+                   h_p.detach()[:xp.shape[0]].cpu().numpy()))
     except Exception as e:   # surface worker failures in the parent
         q.put(repr(e))
         raise

@@ -113,12 +113,13 @@ def _fused_weights(convs: Dict[str, SAGEConv], msgs, x_dict) -> Tuple[torch.Tens
         d_src = x_dict[et[0]].shape[1]
         d_dst = x_dict[et[2]].shape[1]
         conv.materialize(d_src, d_dst)
-        w_ls.append(conv.lin_l.weight * wt)
+        scale = (lambda t: t) if wt == 1.0 else (lambda t: t * wt)   # no kernel for weight 1
+        w_ls.append(scale(conv.lin_l.weight))
         if conv.lin_r is not None:
-            r = conv.lin_r.weight * wt
+            r = scale(conv.lin_r.weight)
             w_root = r if w_root is None else w_root + r
         if conv.lin_l.bias is not None:
-            bb = conv.lin_l.bias * wt
+            bb = scale(conv.lin_l.bias)
             b = bb if b is None else b + bb
     parts = w_ls + ([w_root] if w_root is not None else [])
     return torch.cat(parts, dim=1), b

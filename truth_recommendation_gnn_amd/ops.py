@@ -506,7 +506,8 @@ def defer_until(t: torch.Tensor, work) -> torch.Tensor:
 def await_pending(t: torch.Tensor) -> torch.Tensor:
     entry = _PENDING.pop(id(t), None)
     if entry is not None and entry[0] is t:
-        entry[1].wait()   # NCCL: the current stream waits on the collective (no host sync)
+        with torch.no_grad():
+            entry[1].wait()   # NCCL: the current stream waits on the collective (no host sync)
     return t
 
 
