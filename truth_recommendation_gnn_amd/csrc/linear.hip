@@ -584,9 +584,9 @@ static int fast_grid(int64_t n_tiles) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 512));
 }
 
-// ================================================================ v3: compile-time shapes
-// H (output width) in {64, 128}, K (sum of segments) in {64, 128}, every segment a multiple of 16
-// columns and float4-aligned.  Per 16-column chunk c of the concatenated input, a host-built
+// ================================================================ v4: compile-time shapes
+// H (output width) in {64, 128}, K (sum of segments) in {64, 128, 256}, every segment a multiple
+// of 16 columns and float4-aligned.  Per 16-column chunk c of the concatenated input, a host-built
 // table gives the segment base/stride (no per-element segment search).
 // LDS strides are chosen so that addresses stay affine in the lane id (the compiler keeps one
 // base register + immediates) and the two access kinds are conflict-free:
@@ -600,68 +600,6 @@ struct ChunkTab {
   int32_t ld[kMaxChunks];
   int32_t col[kMaxChunks];   // first column of the chunk inside its segment
 };
-
-// Forward: out = act(X @ W^T + b); W [H][K+8] in LDS (b128 fragments), A fragments prefetched.
-template <int H, int K>
-__global__ void __launch_bounds__(256) k_linear_fwd_v3(const LinArgs a, const ChunkTab tab) {
-  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
-  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
-  for (int idx = threadIdx.x; idx < H * K / 4; idx += 256) {
-    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
-    *reinterpret_cast<float4*>(ws + j * LDW + k) =
-        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock + wave * (RT * 16);
-  float4 av[RT][KC];
-#pragma unroll
-  for (int c = 0; c < KC; ++c)
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int64_t row = r0 + rt * 16 + i;
-      av[rt][c] = row < a.n ? *reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] +
-                                                               tab.col[c] + 4 * g)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  __syncthreads();
-  f32x4 acc[RT][NT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[rt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* wl = ws + i * LDW + 4 * g;
-#pragma unroll
-  for (int c = 0; c < KC; ++c)
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const float4 bv = *reinterpret_cast<const float4*>(wl + t * 16 * LDW + c * 16);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {   // out^T tile = W X^T: lane (i, g) gets row i
-        acc[rt][t] = mfma4(bv.x, av[rt][c].x, acc[rt][t]);
-        acc[rt][t] = mfma4(bv.y, av[rt][c].y, acc[rt][t]);
-        acc[rt][t] = mfma4(bv.z, av[rt][c].z, acc[rt][t]);
-        acc[rt][t] = mfma4(bv.w, av[rt][c].w, acc[rt][t]);
-      }
-    }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {   // lane (i, g): row 16rt+i, columns 16t+4g..+3 -> one float4
-    const float4 b = a.bias ? *reinterpret_cast<const float4*>(a.bias + t * 16 + 4 * g)
-                            : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int64_t row = r0 + rt * 16 + i;
-      if (row < a.n) {
-        float4 v = make_float4(acc[rt][t][0] + b.x, acc[rt][t][1] + b.y, acc[rt][t][2] + b.z,
-                               acc[rt][t][3] + b.w);
-        if (a.relu) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        *reinterpret_cast<float4*>(a.out + row * H + t * 16 + 4 * g) = v;
-      }
-    }
-  }
-}
 
 // Forward v4: persistent.  W is staged into LDS once per block; then each of the 8 waves streams
 // its own 16-row tiles (no further barriers), with the next tile's A fragments in flight during
@@ -732,166 +670,6 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
 #pragma unroll
     for (int c = 0; c < KC; ++c) av[c] = an[c];
   }
-}
-
-// Backward, persistent over 64-row tiles (wave w: rows 16w..16w+15 of the tile).
-//   dgrad: dX = dz @ W      A = dz fragments in registers (masked on load),
-//                           B = W^T image [K][H+8] in LDS (b128)
-//   wgrad: dW += dz^T @ X   A = dz column, B = X column (b32 reads of row-major tiles)
-// The next tile's dz fragments and X tile are prefetched into registers during the MFMAs.
-template <int H, int K, bool DX>
-__global__ void __launch_bounds__(256) k_linear_bwd_v3(const LinArgs a, const ChunkTab tab,
-                                                       int64_t n_tiles) {
-  constexpr int T = 64, HC = H / 16, KC = K / 16;
-  constexpr int JT = H / 64;                // wgrad j tiles per wave
-  constexpr int XQ = T * K / 4 / 256;       // X float4 per thread per tile
-  constexpr int LWT = H + 8, LZ = H + 16, LX = K + 16;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* wt = smem;                         // [K][LWT]  W^T   (DX only)
-  float* dz = wt + (DX ? K * LWT : 0);      // [T][LZ]
-  float* xs = dz + T * LZ;                  // [T][LX]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  if (DX) {
-    for (int idx = threadIdx.x; idx < H * K; idx += 256) {
-      const int j = idx / K, k = idx % K;
-      wt[k * LWT + j] = a.w[(int64_t)j * K + k];
-    }
-  }
-  // this thread's X float4 column (fixed: 256 % (K/4) == 0) and its chunk's segment
-  constexpr int XR = 256 / (K / 4);         // rows covered per pass
-  const int xq_col = (threadIdx.x % (K / 4)) * 4, xq_row0 = threadIdx.x / (K / 4);
-  const int xc = xq_col / 16;
-  const float* xseg = tab.x[xc] + tab.col[xc] + (xq_col % 16);
-  const int xld = tab.ld[xc];
-  auto load_dz = [&](int64_t r0, float4 (&z)[HC]) {
-    const int64_t row = r0 + wave * 16 + i;
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (row < a.n) {
-        v = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
-        if (a.out_act) {
-          const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * H + c * 16 + 4 * g);
-          v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
-          v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
-        }
-      }
-      z[c] = v;
-    }
-  };
-  auto load_x = [&](int64_t r0, float4 (&x)[XQ]) {
-#pragma unroll
-    for (int q = 0; q < XQ; ++q) {
-      const int64_t row = r0 + xq_row0 + q * XR;
-      x[q] = row < a.n ? *reinterpret_cast<const float4*>(xseg + row * xld)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  f32x4 wacc[JT][KC];
-#pragma unroll
-  for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-    for (int kt = 0; kt < KC; ++kt) wacc[jt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float4 dbacc[HC];
-#pragma unroll
-  for (int c = 0; c < HC; ++c) dbacc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 zc[HC], zn[HC], xp[XQ];
-  load_dz((int64_t)blockIdx.x * T, zc);
-  load_x((int64_t)blockIdx.x * T, xp);
-  float* dz_w = dz + (wave * 16 + i) * LZ + 4 * g;          // b128 store of my fragments
-  float* xs_w = xs + xq_row0 * LX + xq_col;
-  const float* wt_r = wt + i * LWT + 4 * g;                 // b128 dgrad B fragments
-  const float* dz_r = dz + g * LZ + (wave * JT) * 16 + i;   // b32 wgrad A column
-  const float* xs_r = xs + g * LX + i;                      // b32 wgrad B column
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int64_t r0 = tile * T;
-    __syncthreads();   // previous tile's LDS reads are done
-#pragma unroll
-    for (int c = 0; c < HC; ++c) {
-      *reinterpret_cast<float4*>(dz_w + c * 16) = zc[c];
-      dbacc[c].x += zc[c].x; dbacc[c].y += zc[c].y; dbacc[c].z += zc[c].z; dbacc[c].w += zc[c].w;
-    }
-#pragma unroll
-    for (int q = 0; q < XQ; ++q) *reinterpret_cast<float4*>(xs_w + q * XR * LX) = xp[q];
-    const bool more = tile + gridDim.x < n_tiles;
-    if (more) {   // next tile in flight during this tile's MFMAs
-      load_dz((tile + gridDim.x) * T, zn);
-      load_x((tile + gridDim.x) * T, xp);
-    }
-    if (DX) {   // dgrad computed transposed, dX^T = W^T dz^T, so that lane (i, g) ends up with
-                // dX[row 16w+i][cols 16ct+4g..+3] and stores one float4; two tiles interleaved
-      const int64_t row = r0 + wave * 16 + i;
-#pragma unroll
-      for (int ct = 0; ct < KC; ct += 2) {
-        f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
-#pragma unroll
-        for (int c = 0; c < HC; ++c) {
-          const float4 b0 = *reinterpret_cast<const float4*>(wt_r + ct * 16 * LWT + c * 16);
-          const float4 b1 = *reinterpret_cast<const float4*>(wt_r + (ct + 1) * 16 * LWT + c * 16);
-          o0 = mfma4(b0.x, zc[c].x, o0); o1 = mfma4(b1.x, zc[c].x, o1);
-          o0 = mfma4(b0.y, zc[c].y, o0); o1 = mfma4(b1.y, zc[c].y, o1);
-          o0 = mfma4(b0.z, zc[c].z, o0); o1 = mfma4(b1.z, zc[c].z, o1);
-          o0 = mfma4(b0.w, zc[c].w, o0); o1 = mfma4(b1.w, zc[c].w, o1);
-        }
-        if (row < a.n) {
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            float* dx = tab.dx[ct + h2];
-            if (dx) {
-              const f32x4 o = h2 ? o1 : o0;
-              *reinterpret_cast<float4*>(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] + 4 * g) =
-                  make_float4(o[0], o[1], o[2], o[3]);
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();   // dz / X tiles complete
-#pragma unroll 4
-    for (int s4 = 0; s4 < T / 4; ++s4) {   // rows 4*s4 + g
-      float az[JT];
-#pragma unroll
-      for (int jt = 0; jt < JT; ++jt) az[jt] = dz_r[s4 * 4 * LZ + jt * 16];
-#pragma unroll
-      for (int kt = 0; kt < KC; ++kt) {
-        const float bx = xs_r[s4 * 4 * LX + kt * 16];
-#pragma unroll
-        for (int jt = 0; jt < JT; ++jt) wacc[jt][kt] = mfma4(az[jt], bx, wacc[jt][kt]);
-      }
-    }
-    if (more) {
-#pragma unroll
-      for (int c = 0; c < HC; ++c) zc[c] = zn[c];
-    }
-  }
-  // partial slab [blockIdx.x][H][K+1]: dW tiles, then db in column K
-  constexpr int KEXT = K + 1;
-  float* slab = a.slab + (int64_t)blockIdx.x * H * KEXT;
-#pragma unroll
-  for (int jt = 0; jt < JT; ++jt)
-#pragma unroll
-    for (int kt = 0; kt < KC; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        slab[(int64_t)((wave * JT + jt) * 16 + 4 * g + r) * KEXT + kt * 16 + i] = wacc[jt][kt][r];
-  // db: lanes (i, g) of every wave hold column sums of cols c*16+4g..+3 over their rows; reduce
-  // over i (16 lanes) with xor shuffles, then over the 4 waves through LDS, in a fixed order
-  __syncthreads();
-  float* red = xs;   // [4 waves][H]
-#pragma unroll
-  for (int c = 0; c < HC; ++c) {
-    float4 v = dbacc[c];
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) {
-      v.x += __shfl_xor(v.x, m, 64); v.y += __shfl_xor(v.y, m, 64);
-      v.z += __shfl_xor(v.z, m, 64); v.w += __shfl_xor(v.w, m, 64);
-    }
-    if (i == 0) *reinterpret_cast<float4*>(red + wave * H + c * 16 + 4 * g) = v;
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < H; j += 256)
-    slab[(int64_t)j * KEXT + K] = ((red[j] + red[H + j]) + red[2 * H + j]) + red[3 * H + j];
 }
 
 // Backward v4: two roles per SIMD.  512 threads; waves 0-3 ("dz waves") load the masked dz
@@ -1171,22 +949,6 @@ static bool fwd4_ok(const LinArgs& a, bool vec) {
   return true;
 }
 
-static bool v3_ok(const LinArgs& a, bool vec) {
-  if (!vec || !(a.h == 64 || a.h == 128) || !(a.k_total == 64 || a.k_total == 128)) return false;
-  for (int s = 0; s < a.n_seg; ++s)
-    if (a.seg[s].k % 16) return false;
-  return true;
-}
-
-static size_t v3_bwd_lds(int h, int k, bool dx) {
-  return ((dx ? (size_t)k * (h + 8) : 0) + (size_t)64 * (h + 16) + (size_t)64 * (k + 16)) * 4;
-}
-
-static int v3_bwd_grid(int64_t n_tiles, int h, int k, bool dx) {
-  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / v3_bwd_lds(h, k, dx)));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 256 * per_cu));
-}
-
 static ChunkTab chunk_table(const LinArgs& a) {
   ChunkTab t{};
   for (int c = 0; c < a.k_total / 16 && c < kMaxChunks; ++c) {
@@ -1245,7 +1007,7 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.out = out;
   a.relu = relu;
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
-  if (fwd4_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
+  if (fwd4_ok(a, vec)) {
     const ChunkTab tab = chunk_table(a);
     const int64_t n_tiles = cdiv(n_rows, 16);
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) /
@@ -1265,19 +1027,6 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     }
 #undef HGNN_FWD4
     return check_launch("k_linear_fwd_v4");
-  }
-  if (v3_ok(a, vec)) {
-    const ChunkTab tab = chunk_table(a);
-    const dim3 grid(gx), block(256);
-    if (h == 64 && a.k_total == 128)
-      hipLaunchKernelGGL((k_linear_fwd_v3<64, 128>), grid, block, 0, stream, a, tab);
-    else if (h == 64)
-      hipLaunchKernelGGL((k_linear_fwd_v3<64, 64>), grid, block, 0, stream, a, tab);
-    else if (a.k_total == 128)
-      hipLaunchKernelGGL((k_linear_fwd_v3<128, 128>), grid, block, 0, stream, a, tab);
-    else
-      hipLaunchKernelGGL((k_linear_fwd_v3<128, 64>), grid, block, 0, stream, a, tab);
-    return check_launch("k_linear_fwd_v3");
   }
   // v2 (W in LDS, A prefetched): 279 vs 321 us at N=1M, K=128, h=64 — the default when it fits
   bool seg16 = vec && a.k_total <= 128 && (h == 64 || h == 128);
@@ -1326,7 +1075,7 @@ size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h) {
   int64_t gx, rpb;
   wgrad_grid(n_rows < 1 ? 1 : n_rows, k_total, h, &gx, &rpb);
   gx = std::max<int64_t>(gx, fast_grid(cdiv(n_rows < 1 ? 1 : n_rows, FT)));
-  gx = std::max<int64_t>(gx, v3_bwd_grid(cdiv(n_rows < 1 ? 1 : n_rows, 64), h, k_total, false));
+  gx = std::max<int64_t>(gx, 256);   // persistent v4 backward: at most 256 blocks
   return align_up((size_t)gx * h * (k_total + 1) * 4, 256) + 256;
 }
 
@@ -1352,7 +1101,7 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   }
   bool any_dx = false;
   for (int s = 0; s < n_seg; ++s) any_dx |= a.seg[s].dx != nullptr;
-  if (fwd4_ok(a, vec) && !getenv("HGNN_LIN_V3")) {
+  if (fwd4_ok(a, vec)) {
     // fused two-role backward when W^T and two dz / X tiles fit the LDS; otherwise persistent
     // dgrad + wgrad-only (T = 32 tiles for K = 256)
     const ChunkTab tab = chunk_table(a);
@@ -1409,31 +1158,6 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     const int64_t total = (int64_t)h * (K + 1);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
                        a.slab, (int64_t)G, h, K + 1, dw, db);
-    return check_launch("k_wgrad_reduce");
-  }
-  if (v3_ok(a, vec) && (dw || db) && ws) {
-    const ChunkTab tab = chunk_table(a);
-    const int64_t n_tiles = cdiv(n_rows, 64);
-    const int G = v3_bwd_grid(n_tiles, h, a.k_total, any_dx);
-    const size_t lds = v3_bwd_lds(h, a.k_total, any_dx);
-    const size_t need = (size_t)G * h * (a.k_total + 1) * 4;
-    if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
-    a.slab = static_cast<float*>(ws);
-    const dim3 grid(G), block(256);
-#define HGNN_BWD3(HV, KV)                                                                      \
-  if (any_dx) hipLaunchKernelGGL((k_linear_bwd_v3<HV, KV, true>), grid, block, lds, stream, a,  \
-                                 tab, n_tiles);                                                \
-  else hipLaunchKernelGGL((k_linear_bwd_v3<HV, KV, false>), grid, block, lds, stream, a, tab,   \
-                          n_tiles);
-    if (h == 64 && a.k_total == 128) { HGNN_BWD3(64, 128) }
-    else if (h == 64) { HGNN_BWD3(64, 64) }
-    else if (a.k_total == 128) { HGNN_BWD3(128, 128) }
-    else { HGNN_BWD3(128, 64) }
-#undef HGNN_BWD3
-    if (int rc = check_launch("k_linear_bwd_v3")) return rc;
-    const int64_t total = (int64_t)h * (a.k_total + 1);
-    hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                       a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
     return check_launch("k_wgrad_reduce");
   }
   if (fast_path_ok(a, vec) && (dw || db) && ws) {
