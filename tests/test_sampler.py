@@ -74,8 +74,9 @@ def test_relabel_prefix_then_new_ids_ascending():
     items[:40] = prefix[:40]
     ei = torch.zeros(2, 1, dtype=torch.int64, device=DEV)
     s = sampler.NeighborSampler({"a": n}, {("a", "r", "a"): ei}, [("a", "r", "a")], [3])
-    nodes, local = s._relabel("a", torch.from_numpy(prefix).to(DEV), torch.from_numpy(items).to(DEV))
-    nodes, local = nodes.cpu().numpy(), local.cpu().numpy()
+    nodes, local, count = s._relabel("a", torch.from_numpy(prefix).to(DEV),
+                                     torch.from_numpy(items).to(DEV))
+    nodes, local = nodes[:int(count)].cpu().numpy(), local.cpu().numpy()
     assert np.array_equal(nodes[:50], prefix)
     new = sorted(set(items.tolist()) - set(prefix.tolist()))
     assert nodes[50:].tolist() == new
@@ -133,7 +134,7 @@ def _torch_blocks(params, rels, mb, x):
             for et, w in rels:
                 if et[2] != dst or et not in blk.csr:
                     continue
-                ei = blk.csr[et]._ei.cpu()
+                ei = blk.csr[et].edge_index.cpu()
                 wl, bl, wr = sage_ref._conv_params(params, f"layers.{l}.{'__'.join(et)}")
                 m = sage_ref.sage_conv(h[et[0]], h[dst][:n_dst], ei, wl, bl, wr)
                 acc = w * m if acc is None else acc + w * m

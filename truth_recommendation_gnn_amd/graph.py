@@ -189,11 +189,45 @@ class RelationCSR:
                                         N.stream_ptr(edge_index.device)), "hgnn_inv_degree")
         self._bwd: Optional[GroupedEdges] = None
 
+    @classmethod
+    def from_csr(cls, rowptr: torch.Tensor, col: torch.Tensor, n_src: int, n_dst: int,
+                 may_have_heavy_rows: bool = True) -> "RelationCSR":
+        """A relation whose edges already come grouped by destination (``rowptr`` over n_dst
+        rows, ``col`` = source ids): no sort and no validation sync.  The edge ids are the CSR
+        positions; the COO and the transposed grouping are derived on first use.  Rows are
+        short (e.g. sampled blocks) unless ``may_have_heavy_rows``, which builds the skew plan."""
+        self = cls.__new__(cls)
+        self.n_src, self.n_dst = int(n_src), int(n_dst)
+        self.num_edges = int(col.numel())
+        self.chunk = None
+        dev = col.device
+        perm = torch.arange(self.num_edges, dtype=torch.int32, device=dev)
+        c = default_chunk(self.num_edges)
+        plan = _plan(rowptr, self.n_dst, c) if may_have_heavy_rows else Plan(c, 0, 0, None, None)
+        self.fwd = GroupedEdges(rowptr, col, perm, plan, self.n_dst)
+        self.inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=dev)
+        N.check(N.lib().hgnn_inv_degree(N.ptr(rowptr), self.n_dst, N.ptr(self.inv_deg),
+                                        N.stream_ptr(dev)), "hgnn_inv_degree")
+        self._ei = None
+        self._bwd = None
+        return self
+
+    @property
+    def edge_index(self) -> torch.Tensor:
+        """[2, E] COO (source, destination) in CSR order for a relation built ``from_csr``."""
+        if self._ei is None:
+            g = self.fwd
+            deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
+            dst = torch.repeat_interleave(torch.arange(self.n_dst, device=g.col.device), deg)
+            self._ei = torch.stack([g.col.long(), dst])
+        return self._ei
+
     @property
     def bwd(self) -> GroupedEdges:
         """Transposed grouping (by source), built on first backward that needs it."""
         if self._bwd is None:
-            self._bwd = group_edges(self._ei[0], self._ei[1], self.n_src, self.n_dst, self.chunk)
+            ei = self.edge_index
+            self._bwd = group_edges(ei[0], ei[1], self.n_src, self.n_dst, self.chunk)
         return self._bwd
 
     @property

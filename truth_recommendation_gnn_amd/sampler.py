@@ -64,21 +64,33 @@ class NeighborSampler:
                                      self.num_nodes[et[2]]) for et in self.relations}
         self.device = next(iter(edge_index_dict.values())).device
 
-    def _sample(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int):
+    def _count(self, et: EdgeType, dst: torch.Tensor, fanout: int):
+        """Phase 1 (no sync): the block rowptr of relation ``et`` for destinations ``dst``."""
         g = self.csr[et].fwd
         lib, dev = N.lib(), self.device
         n = int(dst.numel())
         rowptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
         ws = N.workspace(lib.hgnn_sample_ws_bytes(n), dev)
-        args = (N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst), n, fanout, seed,
-                N.ptr(rowptr))
-        N.check(lib.hgnn_sample_neighbors(*args, None, N.ptr(ws), ws.numel(),
+        N.check(lib.hgnn_sample_neighbors(N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst), n,
+                                          fanout, 0, N.ptr(rowptr), None, N.ptr(ws), ws.numel(),
                                           N.stream_ptr(dev)), "hgnn_sample_neighbors")
-        total = int(rowptr[n])                                  # one host sync per relation
+        return rowptr, ws
+
+    def _fill(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int, rowptr, ws,
+              total: int):
+        """Phase 2: the sampled source ids (global) into a ``total``-long column array."""
+        g = self.csr[et].fwd
+        lib, dev = N.lib(), self.device
         col = torch.empty(total, dtype=torch.int32, device=dev)
-        N.check(lib.hgnn_sample_neighbors(*args, N.ptr(col), N.ptr(ws), ws.numel(),
-                                          N.stream_ptr(dev)), "hgnn_sample_neighbors")
-        return rowptr, col
+        N.check(lib.hgnn_sample_neighbors(N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst),
+                                          int(dst.numel()), fanout, seed, N.ptr(rowptr),
+                                          N.ptr(col), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                "hgnn_sample_neighbors")
+        return col
+
+    def _sample(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int):
+        rowptr, ws = self._count(et, dst, fanout)
+        return rowptr, self._fill(et, dst, fanout, seed, rowptr, ws, int(rowptr[-1]))
 
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
         lib, dev = N.lib(), self.device
@@ -91,7 +103,7 @@ class NeighborSampler:
         N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, n_nodes, N.ptr(local),
                                  N.ptr(nodes), N.ptr(count), N.ptr(ws), ws.numel(),
                                  N.stream_ptr(dev)), "hgnn_relabel")
-        return nodes[: int(count)], local
+        return nodes, local, count      # nodes[:count] is the node set (count read by the caller)
 
     def sample(self, seeds: Mapping[str, torch.Tensor], seed: int = 0) -> MiniBatch:
         cur: Dict[str, torch.Tensor] = {}
@@ -105,31 +117,35 @@ class NeighborSampler:
         nodes, blocks = [cur], []
         for hop, fanout in enumerate(self.fanouts):
             hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
-            sampled = {}
-            for et in self.relations:
-                if et[2] in cur:
-                    sampled[et] = self._sample(et, cur[et[2]], fanout, hop_seed)
-            nxt: Dict[str, torch.Tensor] = {}
-            local: Dict[EdgeType, torch.Tensor] = {}
-            for t in sorted(set(cur) | {et[0] for et in sampled}):
-                ets = [et for et in sampled if et[0] == t]
-                items = (torch.cat([sampled[et][1] for et in ets]) if ets else
+            ets = [et for et in self.relations if et[2] in cur]
+            counted = {et: self._count(et, cur[et[2]], fanout) for et in ets}
+            totals = (torch.stack([counted[et][0][-1] for et in ets]).tolist() if ets else [])
+            sampled = {et: (counted[et][0], self._fill(et, cur[et[2]], fanout, hop_seed,
+                                                       counted[et][0], counted[et][1], tot))
+                       for et, tot in zip(ets, totals)}          # one sync for every relation
+            types = sorted(set(cur) | {et[0] for et in sampled})
+            relabeled = {}
+            for t in types:
+                src_ets = [et for et in sampled if et[0] == t]
+                items = (torch.cat([sampled[et][1] for et in src_ets]) if src_ets else
                          torch.empty(0, dtype=torch.int32, device=self.device))
                 prefix = cur.get(t, torch.empty(0, dtype=torch.int32, device=self.device))
-                nxt[t], loc = self._relabel(t, prefix, items.contiguous())
+                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items.contiguous())
+            sizes = torch.cat([relabeled[t][3] for t in types]).tolist()   # one sync per hop
+            nxt: Dict[str, torch.Tensor] = {}
+            local: Dict[EdgeType, torch.Tensor] = {}
+            for t, size in zip(types, sizes):
+                src_ets, nodes_buf, loc, _ = relabeled[t]
+                nxt[t] = nodes_buf[:size]
                 o = 0
-                for et in ets:
+                for et in src_ets:
                     n = int(sampled[et][1].numel())
                     local[et] = loc[o:o + n]
                     o += n
-            csrs = {}
-            for et, (rowptr, _) in sampled.items():
-                n_dst = int(cur[et[2]].numel())
-                deg = (rowptr[1:] - rowptr[:-1]).long()
-                dst_local = torch.repeat_interleave(
-                    torch.arange(n_dst, dtype=torch.int64, device=self.device), deg)
-                ei = torch.stack([local[et].long(), dst_local])
-                csrs[et] = RelationCSR(ei, int(nxt[et[0]].numel()), n_dst)
+            csrs = {et: RelationCSR.from_csr(rowptr, local[et], int(nxt[et[0]].numel()),
+                                             int(cur[et[2]].numel()),
+                                             may_have_heavy_rows=fanout < 0)
+                    for et, (rowptr, _) in sampled.items()}
             blocks.append(Block(csrs, {t: int(v.numel()) for t, v in cur.items()},
                                 {t: int(v.numel()) for t, v in nxt.items()}))
             nodes.append(nxt)
