@@ -603,7 +603,9 @@ struct ChunkTab {
 
 // Forward v4: persistent.  W is staged into LDS once per block; then each of the 8 waves streams
 // its own 16-row tiles (no further barriers), with the next tile's A fragments in flight during
-// the current tile's MFMAs.  Output tiles are computed transposed (out^T = W X^T) so every lane
+// the current tile's MFMAs.  (Measured and rejected: MFMAs interleaved across accumulators —
+// the 4-deep dependent chains are already covered by 4 waves per SIMD — and a two-stage register
+// ping-pong instead of the copy, which spills: 193-200 us vs 202-205 and 227 at N=1M, K=128.)  Output tiles are computed transposed (out^T = W X^T) so every lane
 // stores one float4 per 16 output columns.
 template <int H, int K>
 __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 : 2))) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
