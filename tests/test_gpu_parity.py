@@ -37,7 +37,8 @@ def rand_coo(rng, n_src, n_dst, E, skew=False):
 
 # ----------------------------------------------------------------------------- K5
 @pytest.mark.parametrize("n_keys,E,skew", [(1, 10, False), (7, 0, False), (300, 5000, True),
-                                           (70000, 200000, True), (1 << 17, 300000, False)])
+                                           (70000, 200000, True), (1 << 17, 300000, False),
+                                           (800000, 400000, True), (1000, 30000, True)])
 def test_coo_to_csr_bit_exact(n_keys, E, skew):
     rng = np.random.default_rng(n_keys + E)
     ei = rand_coo(rng, 1000, n_keys, E, skew)
@@ -363,9 +364,13 @@ def test_weighted_rgcn_fused_loss_step_matches_golden():
         close(p.grad, z["grad:" + name])
 
 
-def test_sort_pairs_matches_numpy():
-    rng = np.random.default_rng(9)
-    E, nk = 100000, 70000
+@pytest.mark.parametrize("E,nk", [(100000, 70000),       # 17 bits: 2 passes of 9
+                                  (300000, 800000),      # 20 bits: 3 passes of 8
+                                  (200000, 300000),      # 19 bits: 3 passes of 8
+                                  (5000, 900),           # 10 bits: 2 passes of 8
+                                  (50000, 3_000_000)])   # 22 bits: 3 passes of 8
+def test_sort_pairs_matches_numpy(E, nk):
+    rng = np.random.default_rng(9 + nk)
     keys = torch.from_numpy(rng.integers(0, nk, E).astype(np.int32))
     a = torch.arange(E, dtype=torch.int32)
     b = torch.from_numpy(rng.integers(-5, 5, E).astype(np.int32))
