@@ -8,7 +8,6 @@
 // oracle/csr_ref.py.
 #include "hgnn_common.h"
 
-
 #include <string.h>
 
 namespace hgnn {
