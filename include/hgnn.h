@@ -193,6 +193,36 @@ int hgnn_topk_metrics(const float* scores, int64_t n_rows, int64_t n_cand, int64
                       const int32_t* true_count, int32_t K, int32_t* topk_idx, double* recall,
                       double* ndcg, hgnn_stream_t stream);
 
+/* ---- edge construction from raw ids -------------------------------------------
+ * Replaces the host loops that map entity ids to node indices row by row:
+ * build_edge_index_safe (train_gnn.py:40-73), build_test_edges (test_gnn.py:34-55) and the
+ * Series.map(dict) + dropna of build_graph.py:383-402.
+ *
+ * An id map is a dict {key: value} as an open-addressing table of 16-B slots in device memory.
+ * Keys are integers (key_ints[n]) or strings in the Arrow layout (key_offsets[n+1] int64 byte
+ * offsets into key_bytes, UTF-8); keys distinct.  capacity: hgnn_idmap_capacity(n_keys) (a power
+ * of two >= 2 n_keys, >= 16); slots: 16·capacity bytes.  The key arrays (and vals) must stay alive
+ * for lookups: the table stores key rows, and string matches are confirmed byte by byte. */
+int64_t hgnn_idmap_capacity(int64_t n_keys);
+int hgnn_idmap_build(const int64_t* key_ints, const int64_t* key_offsets, const uint8_t* key_bytes,
+                     int64_t n_keys, void* slots, int64_t capacity, hgnn_stream_t stream);
+/* dict.get for n_q queries: out[q] = vals[row of the key equal to query q], or -1 when absent or
+ * q_valid[q] == 0 (q_valid may be NULL).  vals == NULL returns the key row.  Integer queries
+ * (q_ints) need an integer-keyed map; string queries (q_offsets + q_bytes) a string-keyed one. */
+int hgnn_idmap_lookup(const void* slots, int64_t capacity, const int64_t* key_ints,
+                      const int64_t* key_offsets, const uint8_t* key_bytes, const int64_t* vals,
+                      const int64_t* q_ints, const int64_t* q_offsets, const uint8_t* q_bytes,
+                      const uint8_t* q_valid, int64_t n_q, int64_t* out, hgnn_stream_t stream);
+/* Keep the rows i in [0,n) whose every column cols[c][i] >= 0 (c < n_cols <= 4), in order:
+ * outs[o][k] = cols[out_col[o]][i] for the k-th kept row (n_outs <= 4; one column may feed several
+ * outputs, e.g. the post column of both the engage and the author edge list).  *d_count (device)
+ * = kept rows; with n_outs == 0 only the count is produced.  n < 2^31.
+ * ws: hgnn_compact_rows_ws_bytes(n).  cols/outs/out_col are HOST arrays of device pointers. */
+size_t hgnn_compact_rows_ws_bytes(int64_t n);
+int hgnn_compact_rows(const int64_t* const* cols, int32_t n_cols, int64_t n,
+                      int64_t* const* outs, const int32_t* out_col, int32_t n_outs,
+                      int32_t* d_count, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

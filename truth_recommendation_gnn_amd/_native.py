@@ -56,6 +56,11 @@ _SIGS = {
     "hgnn_edge_score_parts": (_c_i64, [_c_i64]),
     "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _p, _c_i64, _p,
                                      _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "hgnn_idmap_capacity": (_c_i64, [_c_i64]),
+    "hgnn_idmap_build": (_c_i32, [_p, _p, _p, _c_i64, _p, _c_i64, _p]),
+    "hgnn_idmap_lookup": (_c_i32, [_p, _c_i64, _p, _p, _p, _p, _p, _p, _p, _p, _c_i64, _p, _p]),
+    "hgnn_compact_rows_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_compact_rows": (_c_i32, [_p, _c_i32, _c_i64, _p, _p, _c_i32, _p, _p, _c_sz, _p]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
