@@ -72,6 +72,8 @@ def test_query_encoding_follows_python_equality():
     q = edges._encode(pd.Series(["7", 7, 7.0, True, None, 2.5], dtype=object))
     assert q.ints[1].tolist() == [0, 1, 1, 1, 0, 0] and q.ints[0][1:4].tolist() == [7, 7, 1]
     assert q.strs[2].tolist() == [1, 0, 0, 0, 0, 0]
+    q = edges._encode(pd.Series(["a", None, "bc"], dtype="string[pyarrow]"))
+    assert q.strs[0].tolist() == [0, 1, 1, 3] and q.strs[2].tolist() == [1, 0, 1]
     q = edges._encode(np.array([1, 2 ** 63 + 1], dtype=np.uint64))
     assert q.ints[1].tolist() == [1, 0]
 
@@ -93,6 +95,10 @@ def test_build_edge_index_safe_matches_reference_loop(seed, n_rows, id_style):
     got_e, got_a = edges.build_edge_index_safe(df, um, pm, device=DEV)
     assert got_e.dtype == torch.int64 and got_e.device.type == "cuda"
     assert torch.equal(got_e.cpu(), ref_e) and torch.equal(got_a.cpu(), ref_a)
+    if id_style == "str":                               # Arrow-backed string columns
+        dfa = df.astype({"engager": "string[pyarrow]", "target_user": "string[pyarrow]"})
+        got_e, got_a = edges.build_edge_index_safe(dfa, um, pm, device=DEV)
+        assert torch.equal(got_e.cpu(), ref_e) and torch.equal(got_a.cpu(), ref_a)
 
 
 @pytest.mark.gpu
