@@ -52,6 +52,9 @@ def parse():
                    help="no per-kernel events (for rocprofv3 runs)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
+    p.add_argument("--dist", action="store_true",
+                   help="take the sharded path (process group + collectives) even at world size 1: "
+                        "runs the RCCL calls on a 1-GPU box")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
@@ -100,23 +103,34 @@ def cpu_baseline(cfg, threads):
                       f"bwd+Adam, mean of {n} steps after 1 warmup (oracle/sage_ref.py, torch CPU)"}
 
 
+def _barrier(args, local):
+    if args.dist_backend == "nccl":
+        dist.barrier(device_ids=[local])
+    else:
+        dist.barrier()
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(args.dist_backend)
+    sharded = world > 1 or args.dist
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)
+    if sharded:
+        if "MASTER_ADDR" not in os.environ:          # plain `python bench.py --dist`
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0",
+                              WORLD_SIZE="1")
+        dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", local)
     cfg = synth.CONFIGS[args.config]
     if args.scale != 1.0:
         cfg = synth.scaled(args.config, args.scale)
     torch.manual_seed(synth.WEIGHT_SEED)
     gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED + rank)
-    if world == 1:
+    if not sharded:
         g = synth.make_graph(cfg, device=dev)
         pos = g.edge_index_dict[synth.ENGAGES]
         pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
@@ -163,7 +177,7 @@ def main():
         opt.zero_grad(set_to_none=True)
         loss = forward_loss()
         loss.backward()
-        if world > 1:
+        if sharded:
             parallel.sync_grads(model, parallel.DistEnv.from_torch())
         opt.step()
         return loss
@@ -172,19 +186,19 @@ def main():
         step()
     timer = None if args.profile_steps else ops.KernelTimer()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if sharded:
+        _barrier(args, local)
     ops.set_timer(timer)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if sharded:
+        _barrier(args, local)
     t1 = time.perf_counter()
     ops.set_timer(None)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
+    if sharded:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed)
     value = edges_step * args.steps / elapsed     # edges_step is already the global count
@@ -228,16 +242,17 @@ def main():
                                    f"E_engage={cfg.num_engages} (+reverse), d=h={cfg.dim}, "
                                    f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
                        "edges_per_step": edges_step, "global_batch": edges_step,
-                       "parallelism": (f"user-shard x{world} (posts replicated, RCCL all-reduce)"
-                                       if world > 1 else "single")},
+                       "parallelism": (f"user-shard x{world} (post-table slices: RCCL "
+                                       "reduce-scatter / all-gather per layer)"
+                                       if sharded else "single")},
             "roofline": roof, "cpu_baseline": cpu,
             "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
                             "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
                         for k, v in sorted(kern.items())},
-            "loss": float(loss),
+            "loss": float(loss.detach()),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 
