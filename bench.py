@@ -247,7 +247,9 @@ def main():
                                        if sharded else "single")},
             "roofline": roof, "cpu_baseline": cpu,
             "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
-                            "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+                            "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
+                            "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
+                                                if v["ms"] else None)}
                         for k, v in sorted(kern.items())},
             "loss": float(loss.detach()),
         }

@@ -160,6 +160,29 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
                         int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
                         hgnn_stream_t stream);
 
+/* Single-input forms, one PyG Linear at a time (SURVEY §8b names; same kernels as above):
+ *   hgnn_linear_fwd_f32:   out[n,h] = x[n,k] @ w[h,k]^T (+ bias[h] when non-NULL)
+ *   hgnn_linear_dgrad_f32: dx[n,k]  = dy[n,h] @ w
+ *   hgnn_linear_wgrad_f32: dw[h,k]  = dy^T @ x, db[h] = colsum(dy) (db may be NULL);
+ *                          ws: hgnn_linear_bwd_ws_bytes(n, k, h) */
+int hgnn_linear_fwd_f32(const float* x, int64_t n_rows, int32_t k, const float* w, int32_t h,
+                        const float* bias, float* out, hgnn_stream_t stream);
+int hgnn_linear_dgrad_f32(const float* dy, int64_t n_rows, int32_t h, const float* w, int32_t k,
+                          float* dx, hgnn_stream_t stream);
+int hgnn_linear_wgrad_f32(const float* x, const float* dy, int64_t n_rows, int32_t k, int32_t h,
+                          float* dw, float* db, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
+/* ---- K4 standalone: WeightedRGCN's weighted relation sum + ReLU (train_gnn.py:187-198) -------
+ *   out[e] = act( sum_r weights[r] * ins[r][e] ),  e < n elements, n_in <= HGNN_MAX_SEG
+ * (weights: HOST array; ins: HOST array of device pointers).  The model path folds this into K3;
+ * these are for callers that combine per-relation SAGEConv outputs themselves.
+ * Backward: dins[r][e] = weights[r] * dout[e] * (relu ? out[e] > 0 : 1)  (NULL dins[r] skipped). */
+int hgnn_hetero_epilogue(int32_t n_in, const float* const* ins, const float* weights, int64_t n,
+                         int32_t relu, float* out, hgnn_stream_t stream);
+int hgnn_hetero_epilogue_bwd(int32_t n_in, const float* weights, int64_t n, int32_t relu,
+                             const float* out, const float* dout, float* const* dins,
+                             hgnn_stream_t stream);
+
 /* ---- neighbour sampling for mini-batches (BASELINE cfg5; no reference counterpart) -----------
  * For each destination dst_ids[i] (rows of a destination-grouped CSR rowptr/col over n_rows):
  * keep all in-neighbours if deg <= fanout (or fanout < 0), else `fanout` distinct neighbour

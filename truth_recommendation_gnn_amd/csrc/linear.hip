@@ -1214,4 +1214,30 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   return HGNN_OK;
 }
 
+// ---- single-input forms (the PyG Linear calls one at a time; SURVEY §8b names) ----------------
+// lin(x) = x @ w^T (+ bias): PyG Linear inside SAGEConv (lin_l with bias, lin_r without).
+int hgnn_linear_fwd_f32(const float* x, int64_t n_rows, int32_t k, const float* w, int32_t h,
+                        const float* bias, float* out, hgnn_stream_t stream) {
+  return hgnn_linear_fwd(1, &x, &k, n_rows, w, h, bias, 0, out, stream);
+}
+
+// dx = dy @ w (autograd of lin).  The dx-only backward never reads x, so dx stands in for it.
+int hgnn_linear_dgrad_f32(const float* dy, int64_t n_rows, int32_t h, const float* w, int32_t k,
+                          float* dx, hgnn_stream_t stream) {
+  if (n_rows > 0 && !dx) return fail(HGNN_E_ARG, "linear_dgrad: dx is null");
+  const float* x = dx;
+  return hgnn_linear_bwd(1, &x, &k, n_rows, w, h, dy, nullptr, &dx, nullptr, nullptr, nullptr, 0,
+                         stream);
+}
+
+// dw = dy^T @ x, db = colsum(dy) (db may be NULL).  ws: hgnn_linear_bwd_ws_bytes(n_rows, k, h).
+// The weight-only backward never reads w (every W load sits behind the dx template flag), so dw
+// stands in for it.
+int hgnn_linear_wgrad_f32(const float* x, const float* dy, int64_t n_rows, int32_t k, int32_t h,
+                          float* dw, float* db, void* ws, size_t ws_bytes, hgnn_stream_t stream) {
+  if (!dw) return fail(HGNN_E_ARG, "linear_wgrad: dw is null");
+  return hgnn_linear_bwd(1, &x, &k, n_rows, dw, h, dy, nullptr, nullptr, dw, db, ws, ws_bytes,
+                         stream);
+}
+
 }  // extern "C"

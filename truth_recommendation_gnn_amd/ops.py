@@ -37,17 +37,18 @@ class KernelTimer:
     bench.py inside its timed region; ``None`` when off (zero overhead)."""
 
     def __init__(self):
-        self.records = []   # (name, algorithmic bytes, start event, end event)
+        self.records = []   # (name, algorithmic bytes, start event, end event, compulsory bytes)
 
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for name, nbytes, s, e in self.records:
+        for name, nbytes, s, e, cbytes in self.records:
             ms = s.elapsed_time(e)
-            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0})
+            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0, "cbytes": 0})
             a["launches"] += 1
             a["ms"] += ms
             a["bytes"] += nbytes
+            a["cbytes"] += cbytes
         return agg
 
 
@@ -60,8 +61,12 @@ def set_timer(t: Optional[KernelTimer]) -> None:
 
 
 class _timed:
-    def __init__(self, name, nbytes):
+    """``cbytes``: compulsory bytes (every table row counted once), when it differs from the
+    algorithmic figure — the honest number for a gather whose source table is cache-resident."""
+
+    def __init__(self, name, nbytes, cbytes=None):
         self.name, self.nbytes = name, nbytes
+        self.cbytes = nbytes if cbytes is None else cbytes
 
     def __enter__(self):
         if _timer is not None:
@@ -73,13 +78,19 @@ class _timed:
         if _timer is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            _timer.records.append((self.name, int(self.nbytes), self.s, e))
+            _timer.records.append((self.name, int(self.nbytes), self.s, e, int(self.cbytes)))
 
 
 def gather_bytes(n_edges: int, n_rows: int, d: int, weighted: bool) -> int:
     """Algorithmic HBM bytes of one K1/K2 launch: per edge a 4-B index and one
     4*d-B source row (+4 B weight for K2), rowptr, and the output rows."""
     return 4 * n_edges * (1 + d + (1 if weighted else 0)) + 4 * (n_rows + 1) + 4 * n_rows * d
+
+
+def gather_compulsory_bytes(n_edges: int, n_rows: int, n_src: int, d: int, weighted: bool) -> int:
+    """As gather_bytes with each source row read once: min(E, N_src) rows instead of E."""
+    return (4 * n_edges * (1 + (1 if weighted else 0)) + 4 * min(n_edges, n_src) * d
+            + 4 * (n_rows + 1) + 4 * n_rows * d)
 
 
 # ----------------------------------------------------------------------------- raw kernel calls
@@ -106,7 +117,9 @@ def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
     weighted = edge_w is not None or col_w is not None
     kind = "fwd" if csr_mean else "bwd"
     name = f"gather_{kind}[{grouped.n_rows}<-{x.shape[0]}]x{d}"   # [dst rows <- src rows] x d
-    with _timed(name, gather_bytes(int(grouped.col.numel()), grouped.n_rows, d, weighted)):
+    E = int(grouped.col.numel())
+    with _timed(name, gather_bytes(E, grouped.n_rows, d, weighted),
+                gather_compulsory_bytes(E, grouped.n_rows, int(x.shape[0]), d, weighted)):
         N.check(N.lib().hgnn_gather_reduce(
             N.ptr(x), x.shape[0], d, N.ptr(grouped.rowptr), N.ptr(grouped.col),
             grouped.n_rows, N.ptr(edge_w), N.ptr(col_w), flags, N.ptr(p.heavy_rows),
@@ -123,8 +136,10 @@ def _score_gather(U, P, grouped, mode, cscale, inv_e, out, accumulate, tag):
     slab = None
     if p.n_heavy:
         slab = torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
-    nb = gather_bytes(int(grouped.col.numel()), grouped.n_rows, d, False) + 4 * grouped.n_rows * d
-    with _timed(f"score_gather_{tag}[{grouped.n_rows}<-{U.shape[0]}]x{d}", nb):
+    E = int(grouped.col.numel())
+    nb = gather_bytes(E, grouped.n_rows, d, False) + 4 * grouped.n_rows * d
+    cb = gather_compulsory_bytes(E, grouped.n_rows, int(U.shape[0]), d, False) + 4 * grouped.n_rows * d
+    with _timed(f"score_gather_{tag}[{grouped.n_rows}<-{U.shape[0]}]x{d}", nb, cb):
         N.check(N.lib().hgnn_score_gather(
             N.ptr(U), U.shape[0], N.ptr(P), d, N.ptr(grouped.rowptr), N.ptr(grouped.col),
             grouped.n_rows, mode, N.ptr(cscale), inv_e, N.ptr(p.heavy_rows), N.ptr(p.heavy_first),
