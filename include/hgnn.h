@@ -195,13 +195,14 @@ int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_r
                           int32_t* out_rowptr, int32_t* out_col, void* ws, size_t ws_bytes,
                           hgnn_stream_t stream);
 /* Next layer's node set of one type: nodes_out = [prefix (order kept), then every item id not in
- * prefix, once, ascending]; local_out[k] = position of items[k] in nodes_out; *d_count = total.
- * Ids in [0, n_nodes); prefix ids distinct.  nodes_out holds n_prefix + n_items entries.
- * ws: hgnn_relabel_ws_bytes(n_nodes) (three dense n_nodes maps). */
-size_t hgnn_relabel_ws_bytes(int64_t n_nodes);
+ * prefix, once, in order of first appearance in items]; local_out[k] = position of items[k] in
+ * nodes_out; *d_count = total.  Prefix ids distinct; ids are non-negative int32.  nodes_out holds
+ * n_prefix + n_items entries.  O(n_prefix + n_items) work (a hash set over this call's ids),
+ * deterministic.  ws: hgnn_relabel_ws_bytes(n_prefix, n_items). */
+size_t hgnn_relabel_ws_bytes(int64_t n_prefix, int64_t n_items);
 int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
-                 int64_t n_nodes, int32_t* local_out, int32_t* nodes_out, int32_t* d_count,
-                 void* ws, size_t ws_bytes, hgnn_stream_t stream);
+                 int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
+                 size_t ws_bytes, hgnn_stream_t stream);
 
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of

@@ -35,11 +35,13 @@ def main():
     opt = None
     gen = torch.Generator(device=dev).manual_seed(0)
     stats = {"sample_ms": [], "step_ms": [], "edges": []}
+    # one shuffle per epoch, as a loader over the seed nodes does; batches are slices of it
+    order = {"user": torch.randperm(cfg.num_users, device=dev, generator=gen),
+             "post": torch.randperm(cfg.num_posts, device=dev, generator=gen)}
     for b in range(args.batches + 2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        seeds = {"user": torch.randperm(cfg.num_users, device=dev, generator=gen)[:args.seeds],
-                 "post": torch.randperm(cfg.num_posts, device=dev, generator=gen)[:args.seeds]}
+        seeds = {t: o[b * args.seeds:(b + 1) * args.seeds] for t, o in order.items()}
         mb = s.sample(seeds, seed=b)
         torch.cuda.synchronize()
         t1 = time.perf_counter()

@@ -65,7 +65,7 @@ def test_sample_is_uniform_without_replacement():
     assert np.abs(hits - expect).max() < 5 * np.sqrt(expect)          # ~uniform
 
 
-def test_relabel_prefix_then_new_ids_ascending():
+def test_relabel_prefix_then_new_ids_in_first_appearance_order():
     from truth_recommendation_gnn_amd import sampler
     rng = np.random.default_rng(1)
     n = 1000
@@ -78,7 +78,8 @@ def test_relabel_prefix_then_new_ids_ascending():
                                      torch.from_numpy(items).to(DEV))
     nodes, local = nodes[:int(count)].cpu().numpy(), local.cpu().numpy()
     assert np.array_equal(nodes[:50], prefix)
-    new = sorted(set(items.tolist()) - set(prefix.tolist()))
+    pre = set(prefix.tolist())
+    new = list(dict.fromkeys(i for i in items.tolist() if i not in pre))
     assert nodes[50:].tolist() == new
     assert np.array_equal(nodes[local], items)
 
@@ -165,7 +166,26 @@ def test_sampled_minibatch_forward_backward_match_torch_on_blocks():
     ref_loss.backward()
     for t in ref:
         torch.testing.assert_close(got[t].detach().cpu(), ref[t].detach(), rtol=1e-4,
-                                   atol=1e-5 * float(ref[t].abs().max()))
+                                   atol=1e-5 * float(ref[t].detach().abs().max()))
     for name, p in model.named_parameters():
         r = ref_params[name].grad
         torch.testing.assert_close(p.grad.cpu(), r, rtol=1e-4, atol=1e-5 * float(r.abs().max()))
+
+
+def test_relabel_edge_cases_and_seed_checks():
+    from truth_recommendation_gnn_amd import sampler
+    ei = torch.tensor([[0, 1, 2], [1, 2, 0]], device=DEV)
+    s = sampler.NeighborSampler({"a": 3}, {("a", "r", "a"): ei}, [("a", "r", "a")], [2])
+    pre = torch.tensor([2, 0], dtype=torch.int32, device=DEV)
+    none = torch.empty(0, dtype=torch.int32, device=DEV)
+    nodes, local, count = s._relabel("a", pre, none)                  # no items
+    assert int(count) == 2 and nodes[:2].tolist() == [2, 0] and local.numel() == 0
+    nodes, local, count = s._relabel("a", none, torch.tensor([5, 5, 3, 9, 3], dtype=torch.int32,
+                                                               device=DEV))   # no prefix
+    assert int(count) == 3 and nodes[:3].tolist() == [5, 3, 9] and local.tolist() == [0, 0, 1, 2, 1]
+    with pytest.raises(ValueError):
+        s.sample({"a": torch.tensor([0, 0])})
+    with pytest.raises(ValueError):
+        s.sample({"a": torch.tensor([3])})
+    mb = s.sample({"a": torch.tensor([1])}, seed=1)
+    assert mb.nodes[-1]["a"].tolist() == [1]

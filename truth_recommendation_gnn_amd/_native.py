@@ -49,8 +49,8 @@ _SIGS = {
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_neighbors": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p,
                                        _p, _p, _c_sz, _p]),
-    "hgnn_relabel_ws_bytes": (_c_sz, [_c_i64]),
-    "hgnn_relabel": (_c_i32, [_p, _c_i64, _p, _c_i64, _c_i64, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_relabel_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_relabel": (_c_i32, [_p, _c_i64, _p, _c_i64, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_topk_metrics": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _c_i32, _p, _p, _p,
                                    _p]),
     "hgnn_edge_score_parts": (_c_i64, [_c_i64]),

@@ -309,16 +309,22 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
 }
 
 // rowptr[r] = #sorted keys < r for r in [0, n_keys] (keys == n_keys are dropped sentinels).
+// rowptr[r] = lower_bound(skey, r) for r in [0, n_keys]: one thread per row, a binary search over
+// the sorted keys (the sentinel n_keys of dropped edges sorts last, so rowptr[n_keys] = valid
+// edges).  Every thread does ~log2(E) cached reads; no thread ever fills a run of empty rows
+// serially, which the per-edge boundary scheme did (a graph whose keys leave a long tail of
+// empty rows made one thread write them all).
 __global__ void __launch_bounds__(256) k_rowptr_from_sorted(const int32_t* skey, int64_t E,
                                                             int64_t n_keys, int32_t* rowptr) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= E) return;
-  int32_t k = skey[i];
-  int64_t prev = i > 0 ? skey[i - 1] : -1;
-  int64_t hi = k < n_keys ? k : n_keys;
-  for (int64_t r = prev + 1; r <= hi; ++r) rowptr[r] = (int32_t)i;
-  if (i == E - 1)
-    for (int64_t r = (int64_t)k + 1; r <= n_keys; ++r) rowptr[r] = (int32_t)E;
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > n_keys) return;
+  int64_t lo = 0, hi = E;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (skey[mid] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  rowptr[r] = (int32_t)lo;
 }
 
 __global__ void __launch_bounds__(256) k_gather_other(const int32_t* perm, const int32_t* skey,
@@ -481,7 +487,7 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
   if (int rc = radix_sort_pairs(ka, ka, E, n_keys, nullptr, nullptr, perm, nullptr, w, stream,
                                 &sk))
     return rc;
-  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);
   if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
   hipLaunchKernelGGL(k_gather_other, dim3(cdiv(E, 256)), dim3(256), 0, stream, perm, sk, other,
@@ -522,7 +528,7 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   const int32_t* sk = nullptr;
   if (int rc = radix_sort_pairs(kin, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
     return rc;
-  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);
   return check_launch("k_rowptr_from_sorted");
 }
@@ -554,7 +560,7 @@ int hgnn_sort_pairs_i64(const int64_t* keys, const int32_t* a, const int32_t* b,
   const int32_t* sk = nullptr;
   if (int rc = radix_sort_pairs(ka, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
     return rc;
-  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(E, 256)), dim3(256), 0, stream, sk, E,
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);
   return check_launch("k_rowptr_from_sorted");
 }

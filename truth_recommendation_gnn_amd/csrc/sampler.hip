@@ -14,8 +14,10 @@
 //                   a node's sample does not depend on which batch it sits in, and runs repeat
 //   relabel         the next layer's node set: the current destination nodes first (their order
 //                   kept, so the root term is a prefix view), then every newly reached node in
-//                   ascending global id — a dense id->local map and one exclusive scan, no sort,
-//                   no atomics, deterministic.
+//                   order of first appearance among the sampled items (PyG's order) — a hash set
+//                   over the ids of this call (O(items) work, independent of the graph's node
+//                   count), atomicMin for the first appearance and one exclusive scan, so the
+//                   result is deterministic.
 #include "hgnn_common.h"
 
 namespace hgnn {
@@ -69,46 +71,90 @@ __global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, cons
   if (lane < fanout) out[lane] = col[beg + chosen];
 }
 
-__global__ void k_relabel_prefix(const int32_t* prefix, int64_t n_prefix, int32_t* map,
+// ---- relabel: a hash set over the ids this call sees, O(n_prefix + n_items) work --------------
+// slot arrays (capacity a power of two >= 2·(n_prefix + n_items)): key (-1 empty), ppos (prefix
+// position or -1), first (smallest item position of a non-prefix id; atomicMin, so deterministic)
+struct RelabelTab {
+  int32_t* key;
+  int32_t* ppos;
+  int32_t* first;
+  uint32_t mask;
+  int shift;   // 64 - log2(capacity)
+};
+
+__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t id) {
+  uint32_t s = (uint32_t)(((uint64_t)(uint32_t)id * 0x9E3779B97F4A7C15ull) >> t.shift);
+  for (uint32_t probe = 0; probe <= t.mask; ++probe) {   // ends: load factor <= 1/2
+    const int32_t k = __atomic_load_n(&t.key[s], __ATOMIC_RELAXED);
+    if (k == id) return s;
+    if (k == -1) {
+      const int32_t old = atomicCAS(&t.key[s], -1, id);
+      if (old == -1 || old == id) return s;
+    }
+    s = (s + 1) & t.mask;
+  }
+  return 0;   // unreachable with the capacity the host sizes
+}
+
+__global__ void k_relabel_prefix(RelabelTab t, const int32_t* prefix, int64_t n_prefix,
                                  int32_t* nodes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_prefix) return;
-  map[prefix[i]] = (int32_t)i;
+  const uint32_t s = rl_find_or_insert(t, prefix[i]);
+  t.ppos[s] = (int32_t)i;   // prefix ids are distinct: one writer per slot
   nodes[i] = prefix[i];
 }
 
-__global__ void k_relabel_mark(const int32_t* items, int64_t n_items, const int32_t* map,
-                               int32_t* present) {
+__global__ void k_relabel_insert(RelabelTab t, const int32_t* items, int64_t n_items,
+                                 int32_t* slot_of) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n_items) return;
-  const int32_t id = items[k];
-  if (map[id] < 0) present[id] = 1;   // same value from every writer
+  const uint32_t s = rl_find_or_insert(t, items[k]);
+  slot_of[k] = (int32_t)s;
+  if (t.ppos[s] < 0) atomicMin(&t.first[s], (int32_t)k);
 }
 
-__global__ void k_relabel_assign(const int32_t* present, const int32_t* scan, int64_t n_nodes,
-                                 int64_t n_prefix, int32_t* map, int32_t* nodes) {
-  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (id >= n_nodes || !present[id]) return;
-  const int32_t local = (int32_t)(n_prefix + scan[id]);
-  map[id] = local;
-  nodes[local] = (int32_t)id;
-}
-
-__global__ void k_relabel_items(const int32_t* items, int64_t n_items, const int32_t* map,
-                                int32_t* local) {
+__global__ void k_relabel_flags(RelabelTab t, const int32_t* slot_of, int64_t n_items,
+                                int32_t* flags) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n_items) local[k] = map[items[k]];
+  if (k >= n_items) return;
+  const int32_t s = slot_of[k];
+  flags[k] = t.ppos[s] < 0 && t.first[s] == (int32_t)k;
 }
 
-__global__ void k_relabel_count(const int32_t* scan, int64_t n_nodes, int64_t n_prefix,
+__global__ void k_relabel_assign(RelabelTab t, const int32_t* items, const int32_t* slot_of,
+                                 const int32_t* rank, int64_t n_items, int64_t n_prefix,
+                                 int32_t* local, int32_t* nodes) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_items) return;
+  const int32_t s = slot_of[k];
+  const int32_t pp = t.ppos[s];
+  if (pp >= 0) {
+    local[k] = pp;
+    return;
+  }
+  const int32_t f = t.first[s];
+  const int32_t l = (int32_t)(n_prefix + rank[f]);
+  local[k] = l;
+  if (f == (int32_t)k) nodes[l] = items[k];
+}
+
+__global__ void k_relabel_count(const int32_t* rank, int64_t n_items, int64_t n_prefix,
                                 int32_t* d_count) {
-  *d_count = (int32_t)(n_prefix + scan[n_nodes]);
+  *d_count = (int32_t)(n_prefix + (n_items > 0 ? rank[n_items] : 0));
 }
 
-static size_t relabel_ws(int64_t n_nodes) {
-  size_t scan_b = 0;
-  exclusive_scan_i32(nullptr, nullptr, n_nodes, nullptr, &scan_b, 0);
-  return 3 * align_up((size_t)(n_nodes + 1) * 4, 256) + scan_b + 256;
+static int64_t relabel_cap(int64_t n) {
+  int64_t c = 64;
+  while (c < 2 * n) c <<= 1;
+  return c;
+}
+
+static size_t relabel_ws(int64_t n_prefix, int64_t n_items, size_t* scan_b) {
+  const int64_t cap = relabel_cap(n_prefix + n_items);
+  exclusive_scan_i32(nullptr, nullptr, n_items < 1 ? 1 : n_items, nullptr, scan_b, 0);
+  return 3 * align_up((size_t)cap * 4, 256) + 3 * align_up((size_t)(n_items + 1) * 4, 256) +
+         *scan_b + 256;
 }
 
 }  // namespace hgnn
@@ -154,44 +200,54 @@ size_t hgnn_sample_ws_bytes(int64_t n_dst) {
   return align_up((size_t)(n_dst < 1 ? 1 : n_dst) * 4, 256) + scan_b + 256;
 }
 
-size_t hgnn_relabel_ws_bytes(int64_t n_nodes) { return relabel_ws(n_nodes < 1 ? 1 : n_nodes); }
+size_t hgnn_relabel_ws_bytes(int64_t n_prefix, int64_t n_items) {
+  size_t scan_b = 0;
+  return relabel_ws(n_prefix < 0 ? 0 : n_prefix, n_items < 0 ? 0 : n_items, &scan_b);
+}
 
 int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
-                 int64_t n_nodes, int32_t* local_out, int32_t* nodes_out, int32_t* d_count,
-                 void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+                 int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
+                 size_t ws_bytes, hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
-  if (n_prefix < 0 || n_items < 0 || n_nodes < 0 || n_prefix > n_nodes)
+  if (n_prefix < 0 || n_items < 0 || n_prefix + n_items >= (int64_t)INT32_MAX / 2)
     return fail(HGNN_E_ARG, "relabel: bad sizes");
   if (!d_count || (n_prefix > 0 && (!prefix || !nodes_out)) ||
       (n_items > 0 && (!items || !local_out || !nodes_out)))
     return fail(HGNN_E_ARG, "relabel: null pointer");
-  if (n_nodes == 0) {
-    (void)hipMemsetAsync(d_count, 0, sizeof(int32_t), stream);
-    return check_launch("relabel(empty)");
-  }
-  if (ws_bytes < relabel_ws(n_nodes)) return fail(HGNN_E_WS, "relabel: workspace too small");
-  Workspace w(ws, ws_bytes);
-  int32_t* map = w.take<int32_t>(n_nodes + 1);
-  int32_t* present = w.take<int32_t>(n_nodes + 1);
-  int32_t* scan = w.take<int32_t>(n_nodes + 1);
   size_t scan_b = 0;
-  exclusive_scan_i32(nullptr, nullptr, n_nodes, nullptr, &scan_b, stream);
+  if (ws_bytes < relabel_ws(n_prefix, n_items, &scan_b))
+    return fail(HGNN_E_WS, "relabel: workspace too small");
+  const int64_t cap = relabel_cap(n_prefix + n_items);
+  int log2cap = 0;
+  while ((int64_t(1) << log2cap) < cap) ++log2cap;
+  Workspace w(ws, ws_bytes);
+  RelabelTab t;
+  t.key = w.take<int32_t>(2 * cap);     // key and ppos adjacent: one 0xFF memset
+  t.ppos = t.key + cap;
+  t.first = w.take<int32_t>(cap);
+  t.mask = (uint32_t)(cap - 1);
+  t.shift = 64 - log2cap;
+  int32_t* slot_of = w.take<int32_t>(n_items + 1);
+  int32_t* flags = w.take<int32_t>(n_items + 1);
+  int32_t* rank = w.take<int32_t>(n_items + 1);
   void* scan_ws = w.take<char>(scan_b);
-  (void)hipMemsetAsync(map, 0xFF, (size_t)n_nodes * 4, stream);   // -1
-  (void)hipMemsetAsync(present, 0, (size_t)n_nodes * 4, stream);
+  (void)hipMemsetAsync(t.key, 0xFF, (size_t)cap * 8, stream);       // key = ppos = -1
+  (void)hipMemsetAsync(t.first, 0x7F, (size_t)cap * 4, stream);     // "infinity"
   if (n_prefix > 0)
     hipLaunchKernelGGL(k_relabel_prefix, dim3((unsigned)cdiv(n_prefix, 256)), dim3(256), 0,
-                       stream, prefix, n_prefix, map, nodes_out);
-  if (n_items > 0)
-    hipLaunchKernelGGL(k_relabel_mark, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, stream,
-                       items, n_items, map, present);
-  if (int rc = exclusive_scan_i32(present, scan, n_nodes, scan_ws, &scan_b, stream)) return rc;
-  hipLaunchKernelGGL(k_relabel_assign, dim3((unsigned)cdiv(n_nodes, 256)), dim3(256), 0, stream,
-                     present, scan, n_nodes, n_prefix, map, nodes_out);
-  if (n_items > 0)
-    hipLaunchKernelGGL(k_relabel_items, dim3((unsigned)cdiv(n_items, 256)), dim3(256), 0, stream,
-                       items, n_items, map, local_out);
-  hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(1), 0, stream, scan, n_nodes, n_prefix,
+                       stream, t, prefix, n_prefix, nodes_out);
+  if (n_items > 0) {
+    const unsigned g = (unsigned)cdiv(n_items, 256);
+    hipLaunchKernelGGL(k_relabel_insert, dim3(g), dim3(256), 0, stream, t, items, n_items,
+                       slot_of);
+    hipLaunchKernelGGL(k_relabel_flags, dim3(g), dim3(256), 0, stream, t, slot_of, n_items,
+                       flags);
+    if (int rc = check_launch("k_relabel_flags")) return rc;
+    if (int rc = exclusive_scan_i32(flags, rank, n_items, scan_ws, &scan_b, stream)) return rc;
+    hipLaunchKernelGGL(k_relabel_assign, dim3(g), dim3(256), 0, stream, t, items, slot_of, rank,
+                       n_items, n_prefix, local_out, nodes_out);
+  }
+  hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(1), 0, stream, rank, n_items, n_prefix,
                      d_count);
   return check_launch("relabel");
 }

@@ -210,25 +210,50 @@ class RelationCSR:
                                         N.stream_ptr(dev)), "hgnn_inv_degree")
         self._ei = None
         self._bwd = None
+        self._from_csr = True
         return self
+
+    def _dst_of_positions(self, dtype) -> torch.Tensor:
+        g = self.fwd
+        deg = g.rowptr[1:] - g.rowptr[:-1]
+        return torch.repeat_interleave(torch.arange(self.n_dst, dtype=dtype, device=g.col.device),
+                                       deg, output_size=self.num_edges)   # no host sync
 
     @property
     def edge_index(self) -> torch.Tensor:
         """[2, E] COO (source, destination) in CSR order for a relation built ``from_csr``."""
         if self._ei is None:
-            g = self.fwd
-            deg = (g.rowptr[1:] - g.rowptr[:-1]).long()
-            dst = torch.repeat_interleave(torch.arange(self.n_dst, device=g.col.device), deg)
-            self._ei = torch.stack([g.col.long(), dst])
+            self._ei = torch.stack([self.fwd.col.long(), self._dst_of_positions(torch.int64)])
         return self._ei
 
     @property
     def bwd(self) -> GroupedEdges:
         """Transposed grouping (by source), built on first backward that needs it."""
         if self._bwd is None:
-            ei = self.edge_index
-            self._bwd = group_edges(ei[0], ei[1], self.n_src, self.n_dst, self.chunk)
+            if getattr(self, "_from_csr", False):
+                self._bwd = self._bwd_from_csr()
+            else:
+                ei = self.edge_index
+                self._bwd = group_edges(ei[0], ei[1], self.n_src, self.n_dst, self.chunk)
         return self._bwd
+
+    def _bwd_from_csr(self) -> GroupedEdges:
+        """CSC of a relation built ``from_csr`` (sampled blocks): its ids were produced on the
+        device and are valid by construction, so the sort runs on the int32 CSR directly with no
+        validation pass and no host sync; no skew plan (block rows are short)."""
+        g, E = self.fwd, self.num_edges
+        dev = g.col.device
+        rowptr = torch.empty(self.n_src + 1, dtype=torch.int32, device=dev)
+        col = torch.empty(E, dtype=torch.int32, device=dev)
+        perm = torch.empty(E, dtype=torch.int32, device=dev)
+        lib = N.lib()
+        ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, self.n_src), dev)
+        N.check(lib.hgnn_sort_pairs_i32(N.ptr(g.col), N.ptr(self._dst_of_positions(torch.int32)),
+                                        N.ptr(g.perm), E, self.n_src, N.ptr(rowptr), N.ptr(col),
+                                        N.ptr(perm), None, N.ptr(ws), ws.numel(),
+                                        N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
+        return GroupedEdges(rowptr, col, perm, Plan(default_chunk(E), 0, 0, None, None),
+                            self.n_src)
 
     @property
     def bwd_weights(self) -> torch.Tensor:

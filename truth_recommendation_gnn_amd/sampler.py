@@ -8,7 +8,8 @@ layer-wise scheme so the 4-relation 10M-node config can train on mini-batches:
 * ``sample(seeds)`` walks outwards from the seed nodes: hop h keeps, for every frontier node and
   every relation into its type, all in-neighbours or ``fanouts[h]`` of them drawn uniformly without
   replacement (``hgnn_sample_neighbors``), then relabels the reached nodes into the next frontier
-  (``hgnn_relabel``: previous frontier first, order kept, then new nodes by ascending id);
+  (``hgnn_relabel``: previous frontier first, order kept, then new nodes in order of first
+  appearance, as PyG's sampler orders them);
 * each hop becomes one ``Block`` per layer: a ``RelationCSR`` per relation over local ids, so the
   layer runs on the same K1/K2 gathers and K3 projections as the full graph;
 * ``forward_blocks(model, batch, x_dict)`` runs a ``HeteroSAGE`` on the blocks (differentiable).
@@ -94,26 +95,33 @@ class NeighborSampler:
 
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
         lib, dev = N.lib(), self.device
-        n_nodes = self.num_nodes[t]
         n_p, n_i = int(prefix.numel()), int(items.numel())
         nodes = torch.empty(n_p + n_i, dtype=torch.int32, device=dev)
         local = torch.empty(n_i, dtype=torch.int32, device=dev)
         count = torch.empty(1, dtype=torch.int32, device=dev)
-        ws = N.workspace(lib.hgnn_relabel_ws_bytes(n_nodes), dev)
-        N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, n_nodes, N.ptr(local),
+        ws = N.workspace(lib.hgnn_relabel_ws_bytes(n_p, n_i), dev)
+        N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, N.ptr(local),
                                  N.ptr(nodes), N.ptr(count), N.ptr(ws), ws.numel(),
                                  N.stream_ptr(dev)), "hgnn_relabel")
         return nodes, local, count      # nodes[:count] is the node set (count read by the caller)
 
     def sample(self, seeds: Mapping[str, torch.Tensor], seed: int = 0) -> MiniBatch:
         cur: Dict[str, torch.Tensor] = {}
+        checks = []
         for t, s in seeds.items():
             s = _i32(s.to(self.device))
-            if s.numel() and (int(s.min()) < 0 or int(s.max()) >= self.num_nodes[t]):
-                raise ValueError(f"seed ids of type {t!r} out of range")
-            if torch.unique(s).numel() != s.numel():
-                raise ValueError(f"seed ids of type {t!r} must be distinct")
+            if s.numel():    # [min, max, any duplicate]: read back for all types in one sync
+                ss = torch.sort(s).values
+                dup = (ss[1:] == ss[:-1]).any().to(s.dtype)
+                checks.append((t, torch.stack([ss[0], ss[-1], dup])))
             cur[t] = s
+        if checks:
+            vals = torch.stack([c for _, c in checks]).tolist()
+            for (t, _), (lo, hi, dup) in zip(checks, vals):
+                if lo < 0 or hi >= self.num_nodes[t]:
+                    raise ValueError(f"seed ids of type {t!r} out of range")
+                if dup:
+                    raise ValueError(f"seed ids of type {t!r} must be distinct")
         nodes, blocks = [cur], []
         for hop, fanout in enumerate(self.fanouts):
             hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
