@@ -224,7 +224,8 @@ int hgnn_topk_metrics(const float* scores, int64_t n_rows, int64_t n_cand, int64
  *
  * An id map is a dict {key: value} as an open-addressing table of 16-B slots in device memory.
  * Keys are integers (key_ints[n]) or strings in the Arrow layout (key_offsets[n+1] int64 byte
- * offsets into key_bytes, UTF-8); keys distinct.  capacity: hgnn_idmap_capacity(n_keys) (a power
+ * offsets into key_bytes, UTF-8; key_bytes and q_bytes must be readable 16 bytes past their last
+ * string, as Arrow's 64-B buffer padding guarantees); keys distinct.  capacity: hgnn_idmap_capacity(n_keys) (a power
  * of two >= 2 n_keys, >= 16); slots: 16·capacity bytes.  The key arrays (and vals) must stay alive
  * for lookups: the table stores key rows, and string matches are confirmed byte by byte. */
 int64_t hgnn_idmap_capacity(int64_t n_keys);

@@ -78,8 +78,8 @@ def main():
     dq = {}
     for name, q in (("engager", qe), ("target_user", qt)):
         offs, data, valid = q.strs
-        dq[name] = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (offs, data,
-                                                                                   valid))
+        dq[name] = (edges._h2d(offs, dev), edges.bytes_to_device(data, dev),
+                    edges._h2d(valid, dev))
     pq = torch.from_numpy(qp.ints[0]).to(dev)
     outs = {k: torch.empty(a.rows, dtype=torch.int64, device=dev)
             for k in ("engager", "target_user", "post_id")}

@@ -167,3 +167,19 @@ def test_edge_cases():
         edges.IdMap({"a": -1}, DEV)
     with pytest.raises(TypeError):
         edges.IdMap({("a", 1): 0}, DEV)
+
+
+@pytest.mark.gpu
+def test_string_lengths_and_alignments():
+    """Word-wide loads: every length 0..40 at every byte alignment, prefixes of each other, and
+    the last string of the buffer (the kernels read into the 16-B tail padding)."""
+    from truth_recommendation_gnn_amd import edges
+    keys = ["x" * n for n in range(0, 41, 2)] + ["ab" * n + "c" for n in range(12)]
+    m = {k: i for i, k in enumerate(keys)}
+    queries = []
+    for pad in range(4):                       # shifts every following string's alignment
+        queries += ["p" * pad] + ["x" * n for n in range(41)] + ["ab" * n for n in range(12)]
+        queries += ["ab" * n + "c" for n in range(12)] + ["ab" * n + "d" for n in range(12)]
+    queries.append(keys[-1])                   # ends the buffer
+    got = edges.IdMap(m, DEV).lookup(pd.Series(queries)).cpu().tolist()
+    assert got == [m.get(q, -1) for q in queries]

@@ -24,6 +24,7 @@ one host sync that sizes the output.
 from __future__ import annotations
 
 import numbers
+import warnings
 from typing import Mapping, Optional, Sequence, Tuple, Union
 
 import numpy as np
@@ -58,9 +59,27 @@ def _arrow_strings(values) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     bufs = arr.buffers()
     offs = np.frombuffer(bufs[1], dtype=np.int64)[arr.offset: arr.offset + n + 1]
     data = (np.frombuffer(bufs[2], dtype=np.uint8) if bufs[2] is not None and bufs[2].size
-            else np.zeros(1, dtype=np.uint8))
+            else np.zeros(0, dtype=np.uint8))
     valid = (~arr.is_null().to_numpy(zero_copy_only=False)).astype(np.uint8)
     return offs, data, valid
+
+
+def _h2d(a: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """Host array -> device tensor.  Arrow-backed arrays are read-only views; they are only read
+    here, so torch's non-writable warning does not apply."""
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def bytes_to_device(data: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """A string byte buffer on the device with the 16 B of tail padding the kernels read into."""
+    out = torch.zeros(data.size + 16, dtype=torch.uint8, device=dev)
+    if data.size:
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            out[:data.size].copy_(torch.from_numpy(data))
+    return out
 
 
 def _int_like(v) -> Optional[int]:
@@ -206,13 +225,13 @@ class IdMap:
         if ikeys:
             keys = torch.tensor(ikeys, dtype=torch.int64, device=dev)
             self._int = self._table(lib, keys, None, None, len(ikeys),
-                                    torch.from_numpy(np.ascontiguousarray(ivals)).to(dev))
+                                    _h2d(ivals, dev))
         if skeys:
             offs, data, _ = _arrow_strings(skeys)
-            offs_d = torch.from_numpy(np.ascontiguousarray(offs)).to(dev)
-            data_d = torch.from_numpy(data.copy()).to(dev)
+            offs_d = _h2d(offs, dev)
+            data_d = bytes_to_device(data, dev)
             self._str = self._table(lib, None, offs_d, data_d, len(skeys),
-                                    torch.from_numpy(np.ascontiguousarray(svals)).to(dev))
+                                    _h2d(svals, dev))
 
     def _table(self, lib, ints, offs, data, n, vals):
         cap = int(lib.hgnn_idmap_capacity(n))
@@ -241,14 +260,14 @@ class IdMap:
                              out)
             return out
         if q.ints is not None and self._int is not None:
-            iv, ivalid = (torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in q.ints)
+            iv, ivalid = (_h2d(a, dev) for a in q.ints)
             self._lookup(self._int, iv, None, None, ivalid, q.n, out)
         if q.strs is not None and self._str is not None:
             offs, data, valid = q.strs
             res = out if q.ints is None or self._int is None else torch.empty_like(out)
-            self._lookup(self._str, None, torch.from_numpy(np.ascontiguousarray(offs)).to(dev),
-                         torch.from_numpy(np.ascontiguousarray(data)).to(dev),
-                         torch.from_numpy(valid).to(dev), q.n, res)
+            self._lookup(self._str, None, _h2d(offs, dev),
+                         bytes_to_device(data, dev),
+                         _h2d(valid, dev), q.n, res)
             if res is not out:
                 torch.maximum(out, res, out=out)   # each element is valid in one kind at most
         return out
