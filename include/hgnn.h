@@ -248,6 +248,31 @@ int hgnn_compact_rows(const int64_t* const* cols, int32_t n_cols, int64_t n,
                       int64_t* const* outs, const int32_t* out_col, int32_t n_outs,
                       int32_t* d_count, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* As hgnn_topk_metrics for a subset of rows: score row r belongs to row row_map[r] of the true
+ * sets and of recall / ndcg (topk_idx stays indexed by r). */
+int hgnn_topk_metrics_rows(const float* scores, int64_t n_rows, int64_t n_cand, int64_t ld,
+                           const int32_t* row_map, const int32_t* true_rowptr,
+                           const int32_t* true_cand, const int32_t* true_count, int32_t K,
+                           int32_t* topk_idx, double* recall, double* ndcg, hgnn_stream_t stream);
+
+/* Fused scoring + top-L (the evaluation's GEMM and torch.topk, train_gnn.py:330-340, and
+ * inference.py:427-429): for each output row r (user U[rows ? rows[r] : r], d floats) the L best
+ * of the n_cand candidates P[c] by <U, P[c]> (fp32 MFMA), score desc then index asc, written to
+ * topv / topi [n_rows][L].  The [rows, n_cand] score matrix is never materialised.
+ * d in {64, 128}; U and P row-major, 16-B aligned; 1 <= L <= min(64, n_cand). */
+size_t hgnn_score_topk_lds_bytes(int32_t d, int32_t L);
+int hgnn_score_topk(const float* U, const int32_t* rows, int64_t n_rows, const float* P,
+                    int64_t n_cand, int32_t d, int32_t L, float* topv, int32_t* topi,
+                    hgnn_stream_t stream);
+/* Recall / NDCG (as hgnn_topk_metrics) from hgnn_score_topk lists with L = min(K, n_cand) + 1
+ * (or min(K, n_cand) when n_cand <= K).  A row whose K-th value ties the (K+1)-th needs the whole
+ * row for sklearn's tie groups: it gets tie_flag = 1 and no outputs; redo those rows with
+ * materialised scores (hgnn_topk_metrics_rows). */
+int hgnn_topk_finish(const float* topv, const int32_t* topi, int64_t n_rows, int32_t L,
+                     int64_t n_cand, int32_t K, const int32_t* true_rowptr,
+                     const int32_t* true_cand, const int32_t* true_count, double* recall,
+                     double* ndcg, int32_t* tie_flag, hgnn_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

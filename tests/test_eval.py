@@ -69,13 +69,30 @@ def _int_case(seed, n_users, n_posts, E, d, lo=-2, hi=3, extra_users=0):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("d,fused", [(8, False), (64, True), (64, False), (128, True)])
 @pytest.mark.parametrize("n_users,n_posts,E,K", [(300, 257, 3000, 10), (64, 7, 200, 10),
-                                                 (500, 1000, 2500, 1), (200, 90, 800, 33)])
-def test_evaluate_matches_reference_loop_exact_scores(n_users, n_posts, E, K):
+                                                 (500, 1000, 2500, 1), (200, 90, 800, 33),
+                                                 (150, 700, 1500, 63)])
+def test_evaluate_matches_reference_loop_exact_scores(n_users, n_posts, E, K, d, fused):
+    """Integer embeddings: exact scores, full of ties — on the fused path most rows are redone
+    on the materialised one (tie across the cut), the rest finish from the fused lists."""
     from truth_recommendation_gnn_amd import evaluate
-    U, P, te = _int_case(n_users + K, n_users, n_posts, E, 8, extra_users=5)
+    U, P, te = _int_case(n_users + K, n_users, n_posts, E, d, extra_users=5)
     users, rec, nd = eval_ref.evaluate(te, U, P, n_users, K=K, tie_break="index", per_user=True)
-    r, n = evaluate(te.to(DEV), U.to(DEV), P.to(DEV), K=K)
+    r, n = evaluate(te.to(DEV), U.to(DEV), P.to(DEV), K=K, fused=fused)
+    assert abs(r - float(np.mean(rec))) < 1e-12
+    assert abs(n - float(np.mean(nd))) < 1e-12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [64, 128])
+def test_fused_evaluate_without_ties_matches_reference(d):
+    """Distinct scores (integer embeddings from a wide range): no row needs the tie pass, every
+    metric comes from the fused lists."""
+    from truth_recommendation_gnn_amd import evaluate
+    U, P, te = _int_case(d, 400, 3000, 6000, d, lo=-60, hi=61)
+    users, rec, nd = eval_ref.evaluate(te, U, P, 400, K=10, tie_break="index", per_user=True)
+    r, n = evaluate(te.to(DEV), U.to(DEV), P.to(DEV), K=10, fused=True)
     assert abs(r - float(np.mean(rec))) < 1e-12
     assert abs(n - float(np.mean(nd))) < 1e-12
 
@@ -136,13 +153,15 @@ def test_evaluate_edge_cases():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,C,K", [(50, 1000, 10), (3, 7, 10), (300, 4097, 25)])
-def test_recommend_matches_topk(n, C, K):
-    """inference.py:427-429: torch.topk over user_emb @ known_post_emb.T, batched over users."""
+@pytest.mark.parametrize("d", [16, 64, 128])
+@pytest.mark.parametrize("n,C,K", [(50, 1000, 10), (3, 7, 10), (300, 4097, 25), (129, 65, 63)])
+def test_recommend_matches_topk(n, C, K, d):
+    """inference.py:427-429: torch.topk over user_emb @ known_post_emb.T, batched over users
+    (d 64/128: the fused kernel; 16: the materialised path)."""
     from truth_recommendation_gnn_amd import recommend
     rng = np.random.default_rng(C)
-    U = torch.from_numpy(rng.integers(-3, 4, size=(n, 16)).astype(np.float32))
-    P = torch.from_numpy(rng.integers(-3, 4, size=(C, 16)).astype(np.float32))
+    U = torch.from_numpy(rng.integers(-3, 4, size=(n, d)).astype(np.float32))
+    P = torch.from_numpy(rng.integers(-3, 4, size=(C, d)).astype(np.float32))
     S = U @ P.T                                   # exact (integers): CPU == GPU scores
     s, i = recommend(U.to(DEV), P.to(DEV), K, batch_scores=64 * C)
     k = min(K, C)

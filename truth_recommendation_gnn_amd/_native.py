@@ -53,6 +53,12 @@ _SIGS = {
     "hgnn_relabel": (_c_i32, [_p, _c_i64, _p, _c_i64, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_topk_metrics": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _c_i32, _p, _p, _p,
                                    _p]),
+    "hgnn_topk_metrics_rows": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _c_i32, _p,
+                                        _p, _p, _p]),
+    "hgnn_score_topk_lds_bytes": (_c_sz, [_c_i32, _c_i32]),
+    "hgnn_score_topk": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, _c_i32, _p, _p, _p]),
+    "hgnn_topk_finish": (_c_i32, [_p, _p, _c_i64, _c_i32, _c_i64, _c_i32, _p, _p, _p, _p, _p, _p,
+                                  _p]),
     "hgnn_edge_score_parts": (_c_i64, [_c_i64]),
     "hgnn_edge_score_fwd": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _p, _c_i64, _p,
                                      _p, _p, _p, _p, _p, _p, _p, _p, _p]),
