@@ -268,6 +268,7 @@ __global__ void __launch_bounds__(256) k_topk_metrics(const TopkArgs a) {
 // of scores costs D/4 MFMAs; the rejection test costs one max3 + one compare per lane.
 constexpr int kStUsersPerWave = 32;
 constexpr int kStWaves = 4;
+constexpr int kStThreads = kStWaves * 64;
 
 struct ScoreTopkArgs {
   const float* U;         // [n_u_rows][d] user embeddings
@@ -285,7 +286,7 @@ struct StCfg {
   static constexpr int TC = 64;              // candidates per chunk
   static constexpr int S = D + 8;            // LDS row stride (dwords): b128 fragment reads
   static constexpr int KC = D / 16;          // float4 fragments per row per lane
-  static constexpr int LOADS = TC * D / 4 / 256;   // float4 per thread per chunk
+  static constexpr int LOADS = TC * D / 4 / kStThreads;   // float4 per thread per chunk
 };
 
 __device__ __forceinline__ void st_insert(float* lvs, int* lis, int L, int lane, float cs, int ci,
@@ -304,7 +305,7 @@ __device__ __forceinline__ void st_insert(float* lvs, int* lis, int L, int lane,
 }
 
 template <int D>
-__global__ void __launch_bounds__(256) k_score_topk(const ScoreTopkArgs a) {
+__global__ void __launch_bounds__(kStThreads) k_score_topk(const ScoreTopkArgs a) {
   using Cfg = StCfg<D>;
   constexpr int TC = Cfg::TC, S = Cfg::S, KC = Cfg::KC, LOADS = Cfg::LOADS;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -335,12 +336,12 @@ __global__ void __launch_bounds__(256) k_score_topk(const ScoreTopkArgs a) {
   }
   const int64_t C = a.n_cand;
   const int64_t n_chunks = (C + TC - 1) / TC;
-  // chunk staging: thread t loads float4 number t + 256 q of the chunk (row-major TC x D)
+  // chunk staging: thread t loads float4 number t + kStThreads q of the chunk (row-major TC x D)
   float4 nxt[LOADS];
   auto load_chunk = [&](int64_t ch) {
 #pragma unroll
     for (int q = 0; q < LOADS; ++q) {
-      const int f = threadIdx.x + 256 * q;
+      const int f = threadIdx.x + kStThreads * q;
       const int rr = f / (D / 4), cc = (f % (D / 4)) * 4;
       const int64_t cand = ch * TC + rr;
       nxt[q] = cand < C ? *reinterpret_cast<const float4*>(a.P + cand * D + cc)
@@ -350,7 +351,7 @@ __global__ void __launch_bounds__(256) k_score_topk(const ScoreTopkArgs a) {
   auto store_chunk = [&](int buf) {
 #pragma unroll
     for (int q = 0; q < LOADS; ++q) {
-      const int f = threadIdx.x + 256 * q;
+      const int f = threadIdx.x + kStThreads * q;
       const int rr = f / (D / 4), cc = (f % (D / 4)) * 4;
       *reinterpret_cast<float4*>(cbuf + buf * TC * S + rr * S + cc) = nxt[q];
     }
@@ -515,7 +516,7 @@ int hgnn_score_topk(const float* U, const int32_t* rows, int64_t n_rows, const f
     return fail(HGNN_E_ARG, "score_topk: U and P must be 16-B aligned");
   ScoreTopkArgs a{U, rows, n_rows, P, n_cand, L, topv, topi};
   const size_t lds = hgnn_score_topk_lds_bytes(d, L);
-  const dim3 grid((unsigned)cdiv(n_rows, kStWaves * kStUsersPerWave)), block(256);
+  const dim3 grid((unsigned)cdiv(n_rows, kStWaves * kStUsersPerWave)), block(kStThreads);
   if (d == 64) hipLaunchKernelGGL(k_score_topk<64>, grid, block, lds, stream, a);
   else hipLaunchKernelGGL(k_score_topk<128>, grid, block, lds, stream, a);
   return check_launch("k_score_topk");
