@@ -21,7 +21,7 @@ RTOL = 1e-4
 
 def close(got, ref, rtol=RTOL, atol_scale=1e-5):
     got = got.detach().double().cpu()
-    ref = torch.as_tensor(ref).double().cpu()
+    ref = torch.as_tensor(ref).detach().double().cpu()
     scale = max(float(ref.abs().max()) if ref.numel() else 0.0, 1e-6)
     torch.testing.assert_close(got, ref, rtol=rtol, atol=atol_scale * scale)
 

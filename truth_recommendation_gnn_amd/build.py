@@ -33,7 +33,9 @@ def _digest() -> str:
     for p in _sources() + sorted(CSRC.glob("*.h")) + [INCLUDE / "hgnn.h"]:
         h.update(p.name.encode())
         h.update(p.read_bytes())
-    h.update(" ".join(FLAGS).encode())
+    # flags without the absolute include path: the same tree built elsewhere (the GPU box's copy)
+    # must hash the same, or the shipped library would be rebuilt there
+    h.update(" ".join(f for f in FLAGS if not f.startswith("-I")).encode())
     return h.hexdigest()[:16]
 
 
