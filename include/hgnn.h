@@ -183,6 +183,18 @@ int hgnn_hetero_epilogue_bwd(int32_t n_in, const float* weights, int64_t n, int3
                              const float* out, const float* dout, float* const* dins,
                              hgnn_stream_t stream);
 
+/* hgnn_edge_score_fwd with int32 negatives (as hgnn_uniform_i32 draws them) and without the
+ * optional per-position outputs (the dP side is formed by hgnn_score_gather). */
+int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n_users,
+                            int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                            const int32_t* neg_u_order, int64_t n_edges, const float* cscale,
+                            float* dU, float* part, float* loss, int32_t* err,
+                            hgnn_stream_t stream);
+/* n uniform int32 draws in [0, hi) (the negatives of train_gnn.py:272), counter-based from the
+ * 64-bit seed at d_seed (device memory: a torch Generator draws it without a host sync). */
+int hgnn_uniform_i32(const uint64_t* d_seed, int64_t n, int32_t hi, int32_t* out,
+                     hgnn_stream_t stream);
+
 /* ---- neighbour sampling for mini-batches (BASELINE cfg5; no reference counterpart) -----------
  * For each destination dst_ids[i] (rows of a destination-grouped CSR rowptr/col over n_rows):
  * keep all in-neighbours if deg <= fanout (or fanout < 0), else `fanout` distinct neighbour

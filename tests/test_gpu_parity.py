@@ -348,6 +348,46 @@ def test_edge_bce_loss_rejects_bad_negatives():
     U, P = torch.randn(2, 8, device=DEV), torch.randn(2, 8, device=DEV)
     with pytest.raises(ValueError, match="out of range"):
         ops.edge_bce_loss(U, P, pos, torch.tensor([0, 7], device=DEV), torch.ones(2, device=DEV))
+    with pytest.raises(ValueError, match="out of range"):       # int32 path: no pre-sort check
+        ops.edge_bce_loss(U, P, pos, torch.tensor([7, 0], dtype=torch.int32, device=DEV),
+                          torch.ones(2, device=DEV))
+
+
+@pytest.mark.parametrize("d", [64, 16])
+def test_edge_bce_loss_int32_negatives_bitwise_equal(d):
+    """int32 negatives (sample_negatives) take the validation-free sort and the int32 scoring
+    entry; the same draws as int64 give bitwise the same loss and gradients."""
+    rng = np.random.default_rng(7 + d)
+    nu, npost, E = 400, 150, 8000
+    pos = torch.from_numpy(np.stack([rng.integers(0, nu, E),
+                                     synth._zipf_sample_np(rng, npost, E, 0.9)]).astype(np.int64))
+    neg = torch.from_numpy(rng.integers(0, npost, E).astype(np.int64)).to(DEV)
+    pw = torch.ones(E, device=DEV)
+    U = torch.from_numpy(rng.standard_normal((nu, d)).astype(np.float32)).to(DEV)
+    P = torch.from_numpy(rng.standard_normal((npost, d)).astype(np.float32)).to(DEV)
+    res = []
+    for n in (neg, neg.to(torch.int32)):
+        Ud, Pd = U.clone().requires_grad_(), P.clone().requires_grad_()
+        loss = ops.edge_bce_loss(Ud, Pd, pos.to(DEV), n, pw)
+        loss.backward()
+        res.append((loss.detach(), Ud.grad, Pd.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+def test_sample_negatives_uniform_and_seeded():
+    pos = torch.zeros(2, 400_000, dtype=torch.int64, device=DEV)
+    g1 = torch.Generator(device=DEV).manual_seed(3)
+    a = ops.sample_negatives(pos, 1000, generator=g1)
+    b = ops.sample_negatives(pos, 1000, generator=torch.Generator(device=DEV).manual_seed(3))
+    c = ops.sample_negatives(pos, 1000, generator=g1)              # the generator advanced
+    assert a.dtype == torch.int32 and torch.equal(a, b) and not torch.equal(a, c)
+    assert int(a.min()) >= 0 and int(a.max()) < 1000
+    counts = torch.bincount(a.long(), minlength=1000).double()
+    chi2 = float(((counts - 400.0) ** 2 / 400.0).sum())             # 999 dof: mean 999, sd ~45
+    assert 800 < chi2 < 1200
+    lag = (a[1:].double() - 499.5) * (a[:-1].double() - 499.5)      # no serial correlation
+    assert abs(float(lag.mean())) / (1000 ** 2 / 12) < 0.01
 
 
 def test_weighted_rgcn_fused_loss_step_matches_golden():

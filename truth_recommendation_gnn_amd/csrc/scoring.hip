@@ -24,7 +24,8 @@ struct ScoreArgs {
   const float* P;
   const int32_t* rowptr;       // user-grouped CSR of the positive edges
   const int32_t* col;          // post id per position
-  const int64_t* neg;          // negative post id per position (user-grouped order)
+  const int64_t* neg;          // negative post id per position (user-grouped order) ...
+  const int32_t* neg32;        // ... or as int32 (exactly one of the two is set)
   const int32_t* to_post_pos;  // position -> post-grouped position (for hpos)
   const float* cscale;         // device scalar mean(pos_weights)
   float* dU;
@@ -81,7 +82,7 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
       int pid = 0, nid = 0;
       if (lane < n) {
         pid = a.col[base + lane];
-        const int64_t nn = a.neg[base + lane];
+        const int64_t nn = a.neg32 ? (int64_t)a.neg32[base + lane] : a.neg[base + lane];
         if (nn < 0 || nn >= a.n_posts) atomicAdd(a.err, 1);
         else nid = (int)nn;
       }
@@ -227,12 +228,13 @@ int64_t hgnn_edge_score_parts(int64_t n_users) {
   return (int64_t)align_up((size_t)(2 * cdiv(n_users, 4)), 4) + 4 * kRedBlocks;
 }
 
-int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
-                        int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
-                        const int64_t* neg_u_order, const int32_t* to_post_pos, int64_t n_edges,
-                        const float* cscale, float* dU, float* hpos, int32_t* neg_key,
-                        int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
-                        hgnn_stream_t stream_) {
+static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
+                          int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                          const int64_t* neg_u_order, const int32_t* neg32,
+                          const int32_t* to_post_pos, int64_t n_edges, const float* cscale,
+                          float* dU, float* hpos, int32_t* neg_key, int32_t* neg_user,
+                          float* neg_w, float* part, float* loss, int32_t* err,
+                          hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   if (d < 1 || n_users < 0 || n_posts < 0 || n_edges < 0)
     return fail(HGNN_E_ARG, "edge_score: bad sizes");
@@ -242,7 +244,7 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   if (hpos && !to_post_pos) return fail(HGNN_E_ARG, "edge_score: hpos needs to_post_pos");
   (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);
   ScoreArgs a{};
-  a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order;
+  a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order; a.neg32 = neg32;
   a.to_post_pos = to_post_pos; a.cscale = cscale; a.dU = dU; a.hpos = hpos; a.neg_key = neg_key;
   a.neg_u = neg_user; a.neg_w = neg_w; a.part = part; a.err = err; a.n_users = n_users;
   a.n_posts = n_posts; a.inv_e = n_edges > 0 ? 1.f / (float)n_edges : 0.f; a.d = d;
@@ -265,6 +267,54 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
   if (int rc2 = check_launch("k_loss_partial")) return rc2;
   hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, stream, red, cscale, a.inv_e, loss);
   return check_launch("k_loss_final");
+}
+
+int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
+                        int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                        const int64_t* neg_u_order, const int32_t* to_post_pos, int64_t n_edges,
+                        const float* cscale, float* dU, float* hpos, int32_t* neg_key,
+                        int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
+                        hgnn_stream_t stream) {
+  if (n_edges > 0 && !neg_u_order) return fail(HGNN_E_ARG, "edge_score: negatives are null");
+  return edge_score_fwd(U, P, d, n_users, n_posts, rowptr_u, col_u, neg_u_order, nullptr,
+                        to_post_pos, n_edges, cscale, dU, hpos, neg_key, neg_user, neg_w, part,
+                        loss, err, stream);
+}
+
+int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n_users,
+                            int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                            const int32_t* neg_u_order, int64_t n_edges, const float* cscale,
+                            float* dU, float* part, float* loss, int32_t* err,
+                            hgnn_stream_t stream) {
+  if (n_edges > 0 && !neg_u_order) return fail(HGNN_E_ARG, "edge_score: negatives are null");
+  return edge_score_fwd(U, P, d, n_users, n_posts, rowptr_u, col_u, nullptr, neg_u_order,
+                        nullptr, n_edges, cscale, dU, nullptr, nullptr, nullptr, nullptr, part,
+                        loss, err, stream);
+}
+
+// Uniform draws in [0, hi): out[i] = hi * (splitmix64(seed + i * golden) >> 32) >> 32 (Lemire's
+// multiply-shift), the seed read from device memory so the caller draws it from a torch
+// Generator without a host sync.  The loss's negatives (train_gnn.py:272's torch.randint) drawn
+// as int32 in range by construction: no int64 array, no validation pass before the sort.
+__global__ void k_uniform_i32(const uint64_t* seed, int64_t n, uint32_t hi, int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t x = *seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  out[i] = (int32_t)(((x >> 32) * (uint64_t)hi) >> 32);
+}
+
+int hgnn_uniform_i32(const uint64_t* d_seed, int64_t n, int32_t hi, int32_t* out,
+                     hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (n < 0 || hi < 1) return fail(HGNN_E_ARG, "uniform_i32: n=%lld hi=%d", (long long)n, hi);
+  if (n == 0) return HGNN_OK;
+  if (!d_seed || !out) return fail(HGNN_E_ARG, "uniform_i32: null pointer");
+  hipLaunchKernelGGL(k_uniform_i32, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, d_seed,
+                     n, (uint32_t)hi, out);
+  return check_launch("k_uniform_i32");
 }
 
 }  // extern "C"

@@ -414,7 +414,8 @@ class _EdgeBCELoss(torch.autograd.Function):
         c = cscale.to(torch.float32).reshape(()).contiguous()
         inv_e = 1.0 / n_total if n_total > 0 else 0.0
         uop = _user_of_pos(csr)
-        neg = neg_u_order.to(torch.int64).contiguous()
+        neg32 = neg_u_order.dtype == torch.int32          # sample_negatives' draws
+        neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
         rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
         nu_s = torch.empty(E, dtype=torch.int32, device=dev)
         dP = torch.empty_like(P)
@@ -424,20 +425,35 @@ class _EdgeBCELoss(torch.autograd.Function):
         lanes = _Lanes(dev, 2)
         with torch.cuda.stream(lanes.stream(1)):
             ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-            with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
-                N.check(lib.hgnn_sort_pairs_i64(
-                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s), None,
-                    N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                    "hgnn_sort_pairs_i64")
+            if neg32:
+                # int32 keys: no validation pass (the scoring pass below counts out-of-range
+                # negatives; the sort only misplaces such a key, never dereferences it)
+                with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
+                    N.check(lib.hgnn_sort_pairs_i32(
+                        N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                        None, None, N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                        "hgnn_sort_pairs_i32")
+            else:
+                with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
+                    N.check(lib.hgnn_sort_pairs_i64(
+                        N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                        None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                        "hgnn_sort_pairs_i64")
             _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
             from .graph import GroupedEdges, Plan
             negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
             _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
         with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
-            N.check(lib.hgnn_edge_score_fwd(
-                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
-                N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
+            if neg32:
+                N.check(lib.hgnn_edge_score_fwd_i32(
+                    N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                    N.ptr(neg), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
+                    N.ptr(err), s), "hgnn_edge_score_fwd_i32")
+            else:
+                N.check(lib.hgnn_edge_score_fwd(
+                    N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                    N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
+                    N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
         lanes.join()
         if check and int(err[0]):
             raise ValueError("edge_bce_loss: negative post id out of range")
@@ -480,9 +496,23 @@ def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:
 def sample_negatives(pos_edges: torch.Tensor, num_posts: int,
                      generator: Optional[torch.Generator] = None) -> torch.Tensor:
     """One uniform negative post per positive edge (train_gnn.py:272's ``torch.randint``), drawn
-    directly in the user-grouped order: the draws are iid, so only their labels move."""
-    return torch.randint(0, num_posts, (pos_edges.shape[1],), device=pos_edges.device,
+    directly in the user-grouped order: the draws are iid, so only their labels move.
+
+    int32 draws from ``hgnn_uniform_i32`` (a counter-based generator seeded from ``generator``
+    on the device, no host sync): in range by construction, so the loss sorts them without the
+    int64 validation pass.  ``edge_bce_loss`` also takes int64 ``torch.randint`` negatives."""
+    dev = N.require_device(pos_edges)
+    E = int(pos_edges.shape[1])
+    out = torch.empty(E, dtype=torch.int32, device=dev)
+    if E == 0:
+        return out
+    if num_posts < 1 or num_posts >= 2**31:
+        raise ValueError(f"num_posts={num_posts} out of range")
+    seed = torch.randint(0, 2**62, (1,), device=dev, dtype=torch.int64,
                          generator=generator)
+    N.check(N.lib().hgnn_uniform_i32(N.ptr(seed), E, int(num_posts), N.ptr(out),
+                                     N.stream_ptr(dev)), "hgnn_uniform_i32")
+    return out
 
 
 # ----------------------------------------------------------------------------- composable ops
