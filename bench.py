@@ -9,9 +9,11 @@ with fresh ``torch.randint`` negatives, full backward, Adam.  Inputs resident in
 timed region.  Metric numerator = sum over layers and relations of E_r = 80M edges/step.
 
 N>1 (``torch.distributed.run``): weak scaling — one global graph N times the cfg2 size (N·1M
-users, N·100k posts, N·20M engages), users sharded across ranks (each rank owns a cfg2-sized
-user range and its edges), posts replicated; the post aggregates and their gradients are
-all-reduced over RCCL every layer, weight gradients once per step (parallel.py).
+users, N·100k posts, N·20M engages), destination-partitioned (parallel.py): each rank owns a
+cfg2-sized user range and a 1/N row slice of the post table.  Per layer one RCCL reduce-scatter
+of the post partial sums and one all-gather of the projected slices (their adjoints in the
+backward), a halo all-to-all for user->user relations when the config has them (cfg5), weight
+gradients all-reduced once per step.
 value = all ranks' edges / max-over-ranks time.
 
 Prints ONE JSON line (rank 0) with ``roofline`` for the dominant kernel (the K1 forward gather:
@@ -36,7 +38,20 @@ from truth_recommendation_gnn_amd import HeteroSAGE, ops, synth  # noqa: E402
 from truth_recommendation_gnn_amd import parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
-RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+# every relation a config may hold, with the reference's weights (train_gnn.py:163-164:
+# w_direct 1.0, w_social 0.75); cfg5's post-post relation takes 1.0
+ALL_RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
+                 (synth.POST_POST, 1.0)]
+
+
+def relations_of(cfg):
+    """The relations ``cfg``'s graph holds: cfg2-4 the two engage directions, cfg5 all four."""
+    have = {synth.REV_ENGAGES, synth.ENGAGES}
+    if cfg.num_social:
+        have.add(synth.SOCIAL)
+    if cfg.num_post_post:
+        have.add(synth.POST_POST)
+    return [(et, w) for et, w in ALL_RELATIONS if et in have]
 
 
 def parse():
@@ -64,12 +79,13 @@ def cpu_baseline(cfg, threads):
     """Oracle (plain torch CPU, PyG's op pattern) on a bounded cfg sample; edges/s."""
     from oracle import sage_ref
     torch.set_num_threads(threads)
+    rels = relations_of(cfg)
     sample = synth.scaled(cfg.name, 0.05) if cfg.num_engages > 1_000_000 else cfg
     g = synth.make_graph(sample)
     names = []
     for l in range(sample.layers):
         cin = sample.dim if l == 0 else sample.hidden
-        for et, _ in RELATIONS:
+        for et, _ in rels:
             p = f"layers.{l}.{'__'.join(et)}"
             names += [(f"{p}.lin_l.weight", (sample.hidden, cin)), (f"{p}.lin_l.bias", (sample.hidden,)),
                       (f"{p}.lin_r.weight", (sample.hidden, cin))]
@@ -80,7 +96,7 @@ def cpu_baseline(cfg, threads):
 
     def step():
         opt.zero_grad()
-        out = sage_ref.hetero_sage(params, g.x_dict, g.edge_index_dict, RELATIONS, sample.layers)
+        out = sage_ref.hetero_sage(params, g.x_dict, g.edge_index_dict, rels, sample.layers)
         neg = torch.randint(0, sample.num_posts, (pos.shape[1],))
         loss = sage_ref.link_loss(out["user"], out["post"], pos, neg, pw)
         loss.backward()
@@ -95,7 +111,7 @@ def cpu_baseline(cfg, threads):
         if time.perf_counter() - t0 > 10.0 or n >= 5:
             break
     dt = (time.perf_counter() - t0) / n
-    edges = sample.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
+    edges = sample.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
     return {"value": edges / dt, "unit": "edges/s", "cores": torch.get_num_threads(),
             "kind": "port",
             "sample": f"{sample.name}: U={sample.num_users} P={sample.num_posts} "
@@ -137,10 +153,11 @@ def main():
         # BCEWithLogitsLoss() collapses the per-edge interaction weights to their mean
         # (train_gnn.py:276-281); the weights are static graph data, so the mean is taken once
         cscale = pw.mean()
-        model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers).to(dev)
+        rels = relations_of(cfg)
+        model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers).to(dev)
         with torch.no_grad():
             model(g.x_dict, g.edge_index_dict)  # materialise lazy weights, build + cache CSR/CSC
-        edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in RELATIONS)
+        edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
 
         def forward_loss():
             out = model(g.x_dict, g.edge_index_dict)
@@ -153,13 +170,16 @@ def main():
         g = synth.make_graph(gcfg, device=dev, device_gen=True)   # identical on every rank
         pos_g = g.edge_index_dict[synth.ENGAGES]
         pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
-        shard = parallel.UserShard(pos_g, gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g)
+        rels = relations_of(gcfg)
+        shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in rels}, gcfg.num_users,
+                                   gcfg.num_posts, env, pos_weights=pw_g)
         x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
         x_post = g.x_dict["post"]
-        edges_step = gcfg.layers * 2 * int(pos_g.shape[1])   # global, both relations
+        # global count over all relations
+        edges_step = gcfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
         del g, pos_g, pw_g
         torch.cuda.empty_cache()
-        model = HeteroSAGE(gcfg.hidden, RELATIONS, num_layers=gcfg.layers).to(dev)
+        model = HeteroSAGE(gcfg.hidden, rels, num_layers=gcfg.layers).to(dev)
         with torch.no_grad():
             shard.forward(model, x_user, x_post)
         for p in model.parameters():
@@ -239,7 +259,9 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded numpy PCG64 graph, Zipf post degrees; random-init weights)",
             "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
-                                   f"E_engage={cfg.num_engages} (+reverse), d=h={cfg.dim}, "
+                                   f"E_engage={cfg.num_engages} (+reverse), "
+                                   f"relations={'+'.join(et[1] for et, _ in relations_of(cfg))}, "
+                                   f"d=h={cfg.dim}, "
                                    f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
                        "edges_per_step": edges_step, "global_batch": edges_step,
                        "parallelism": (f"user-shard x{world} (post-table slices: RCCL "

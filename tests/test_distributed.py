@@ -1,18 +1,19 @@
-"""CPU, world_size 2 (gloo): the user-sharded / post-replicated step of parallel.py reproduces
-the single-process oracle — outputs, loss and every parameter gradient."""
+"""CPU, world_size 2 and 3 (gloo): the destination-partitioned step of parallel.py reproduces the
+single-process oracle — outputs, loss and every parameter gradient — for the two-relation
+training graph, the reference ``WeightedRGCN`` (with the social user->user relation, whose
+remote sources come through the halo all-to-all) and the 4-relation cfg5 graph (user-user and
+post-post added)."""
 import os
 import socket
 
-import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import sage_ref
-from truth_recommendation_gnn_amd import HeteroSAGE, synth
-from truth_recommendation_gnn_amd.parallel import (RELATIONS, DistEnv, UserShard, sync_grads,
-                                                    user_range)
+from truth_recommendation_gnn_amd import synth
+from truth_recommendation_gnn_amd.parallel import DistEnv, UserShard, sync_grads, user_range
 
 
 def _free_port():
@@ -21,36 +22,22 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _param_shapes(cfg):
-    out = []
-    for l in range(cfg.layers):
-        cin = cfg.dim if l == 0 else cfg.hidden
-        for et, _ in RELATIONS:
-            p = f"layers.{l}.{'__'.join(et)}"
-            out += [(f"{p}.lin_l.weight", (cfg.hidden, cin)), (f"{p}.lin_l.bias", (cfg.hidden,)),
-                    (f"{p}.lin_r.weight", (cfg.hidden, cin))]
-    return out
-
-
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, kind="engage2"):
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
     from dist_torch_impl import TorchImpl
+    from dist_cases import setup as _setup
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.set_num_threads(1)
         env = DistEnv.from_torch()
-        cfg = synth.scaled("cfg2", 0.0005)
-        cfg = synth.dataclasses.replace(cfg, dim=16, hidden=16)
-        g = synth.make_graph(cfg)
+        cfg, g, model, params, fwd, edges = _setup(kind)
         pos = g.edge_index_dict[synth.ENGAGES]
         neg = synth.negative_posts(cfg.num_posts, pos.shape[1])
         pw = synth.interaction_weights(cfg.num_posts)[pos[1]]
-        params = sage_ref.init_params(_param_shapes(cfg))
-        model = HeteroSAGE(cfg.hidden, RELATIONS, num_layers=cfg.layers)
         model.load_state_dict(params)
-        shard = UserShard(pos, cfg.num_users, cfg.num_posts, env, impl=TorchImpl(),
+        shard = UserShard(edges, cfg.num_users, cfg.num_posts, env, impl=TorchImpl(),
                           pos_weights=pw)
         lo, hi = user_range(cfg.num_users, world, rank)
         h_u, h_p = shard.forward(model, g.x_dict["user"][lo:hi], g.x_dict["post"])
@@ -60,16 +47,15 @@ def _worker(rank, world, port, q):
         total = env.all_reduce_(loss.detach().clone())
         grads = {n: p.grad.clone() for n, p in model.named_parameters()}
         # reference on the whole graph, one process
-        out, ref_loss, ref_grads = sage_ref.train_step_grads(
-            params, lambda P: sage_ref.hetero_sage(P, g.x_dict, g.edge_index_dict, RELATIONS,
-                                                   cfg.layers), pos, neg, pw)
+        out, ref_loss, ref_grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
         res = {"rank": rank,
                "loss_err": abs(float(total) - float(ref_loss)) / abs(float(ref_loss)),
                "user_err": float((h_u.detach() - out["user"][lo:hi]).abs().max()),
                "post_err": float((h_p.detach()[:cfg.num_posts] - out["post"]).abs().max()),
                "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
                                max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
-               "n_local": int(shard.pos_local.shape[1]), "n_total": int(pos.shape[1])}
+               "n_local": int(shard.pos_local.shape[1]), "n_total": int(pos.shape[1]),
+               "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
         q.put(res)
     except Exception as e:   # report instead of leaving the parent waiting on the queue
         q.put({"rank": rank, "error": repr(e)})
@@ -78,12 +64,13 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_user_sharded_step_matches_single_process_oracle(world):
+@pytest.mark.parametrize("world,kind", [(2, "engage2"), (3, "engage2"), (2, "rgcn"),
+                                        (3, "rgcn"), (2, "rel4"), (3, "rel4")])
+def test_user_sharded_step_matches_single_process_oracle(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
@@ -93,6 +80,8 @@ def test_user_sharded_step_matches_single_process_oracle(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert sum(r["n_local"] for r in res) == res[0]["n_total"]
+    if kind != "engage2":     # the social relation really crosses ranks
+        assert all(r["n_halo"] > 0 for r in res), res
     for r in res:
         assert r["loss_err"] < 1e-5, r
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r

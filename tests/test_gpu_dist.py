@@ -75,3 +75,75 @@ def test_user_shard_world2_async_collectives_match_golden():
     for name, g in grads.items():
         ref = z["grad:" + name]
         np.testing.assert_allclose(g, ref, rtol=1e-4, atol=1e-5 * max(np.abs(ref).max(), 1e-6))
+
+
+def _case_worker(rank, world, port, q, kind):
+    """The HIP kernels under the destination-partitioned step for a case of tests/dist_cases.py;
+    rank 0 also runs the CPU oracle on the whole graph."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dist_cases import setup
+        from oracle import sage_ref
+        from truth_recommendation_gnn_amd import parallel, synth
+        dev = torch.device("cuda:0")
+        cfg, g, model, params, fwd, edges = setup(kind)
+        pos = g.edge_index_dict[synth.ENGAGES]
+        neg = synth.negative_posts(cfg.num_posts, pos.shape[1])
+        pw = synth.interaction_weights(cfg.num_posts)[pos[1]]
+        model.load_state_dict(params)
+        model = model.to(dev)
+        env = parallel.DistEnv.from_torch()
+        ed = {k: v.to(dev) for k, v in edges.items()}
+        shard = parallel.UserShard(ed, cfg.num_users, cfg.num_posts, env,
+                                   pos_weights=pw.to(dev))
+        xu = g.x_dict["user"].to(dev)[shard.lo:shard.hi].contiguous()
+        h_u, h_p = shard.forward(model, xu, g.x_dict["post"].to(dev))
+        loss = shard.loss(h_u, h_p, shard.local_edges_of(neg.to(dev)))
+        loss.backward()
+        parallel.sync_grads(model, env)
+        total = env.all_reduce_(loss.detach().clone())
+        torch.cuda.synchronize()
+        out, ref_loss, ref_grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
+        res = {"rank": rank,
+               "loss_err": abs(float(total) - float(ref_loss)) / abs(float(ref_loss)),
+               "user_err": float((h_u.detach().cpu() - out["user"][shard.lo:shard.hi]).abs().max()
+                                 / out["user"].abs().max()),
+               "post_err": float((h_p.detach().cpu()[:cfg.num_posts] - out["post"]).abs().max()
+                                 / out["post"].abs().max()),
+               "grad_err": max(float((p.grad.cpu() - ref_grads[n]).abs().max()) /
+                               max(float(ref_grads[n].abs().max()), 1e-12)
+                               for n, p in model.named_parameters()),
+               "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
+        q.put(res)
+    except Exception as e:   # surface worker failures in the parent
+        q.put({"rank": rank, "error": repr(e)})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, "rgcn"), (3, "rel4")])
+def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind):
+    """The reference WeightedRGCN (social relation through the halo all-to-all) and the
+    4-relation cfg5 graph on the HIP kernels, world 2/3 on one device (gloo over device
+    tensors, the exchange via host memory), against the CPU oracle of the whole graph."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_case_worker, args=(r, world, port, q, kind))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    errs = [r["error"] for r in res if "error" in r]
+    assert not errs, errs
+    for r in res:
+        assert r["n_halo"] > 0, r
+        assert r["loss_err"] < 1e-4, r
+        assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
+        assert r["grad_err"] < 1e-4, r

@@ -528,6 +528,7 @@ class _GatherMean(torch.autograd.Function):
     def backward(ctx, g):
         if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
             return None, None
+        await_pending(g)     # the halo exchange's adjoint may still be in flight (parallel.py)
         return scatter_mean_bwd(g.contiguous(), ctx.csr), None
 
 

@@ -32,15 +32,17 @@ user-side backward autograd runs before it overlaps it.  The compute ops are inj
 from __future__ import annotations
 
 import dataclasses
-from typing import Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 from . import ops
 from .graph import RelationCSR, relation_csr
-from .nn import HeteroSAGE, _fused_weights
+from .nn import HeteroSAGE, Layout, _fused_weights, _LayoutModel
 from .synth import ENGAGES, REV_ENGAGES
+
+EdgeType = Tuple[str, str, str]
 
 RELATIONS = [(REV_ENGAGES, 1.0), (ENGAGES, 1.0)]
 
@@ -92,6 +94,21 @@ class DistEnv:
             return full, _Held(work, own, full)
         dist.all_gather(list(full.chunk(self.world)), own, group=self.group)
         return full, _Done()
+
+    def all_to_all_async(self, inp: torch.Tensor, send_splits, recv_splits):
+        """Rows ``inp[sum(send_splits[:q]) : ...]`` go to rank q; returns (received rows, in rank
+        order, work).  Split lists are host ints (static per graph: no size exchange per call)."""
+        out = inp.new_empty((int(sum(recv_splits)),) + tuple(inp.shape[1:]))
+        if self._direct(inp):
+            work = dist.all_to_all_single(out, inp, list(recv_splits), list(send_splits),
+                                          group=self.group, async_op=True)
+            return out, _Held(work, inp, out)
+        # gloo over device tensors (one-GPU rehearsal): the exchange goes through host memory
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(host, inp.cpu(), list(recv_splits), list(send_splits),
+                               group=self.group)
+        out.copy_(host)
+        return out, _Done()
 
     def all_reduce_async(self, t: torch.Tensor):
         """Start an in-place all-reduce; ``.wait()`` on the result before reading ``t`` (with
@@ -209,6 +226,29 @@ class _AllGather(torch.autograd.Function):
         return out, None, None
 
 
+class _AllToAll(torch.autograd.Function):
+    """Halo exchange: rows to each peer -> rows from each peer; adjoint: the reverse exchange of
+    the gradients (issued asynchronously; with ``defer_grad`` awaited by its single consumer, the
+    backward of the gather that picked the sent rows)."""
+
+    @staticmethod
+    def forward(ctx, x, env: DistEnv, send_splits, recv_splits, handle: "Pending",
+                defer_grad: bool):
+        ctx.env, ctx.splits, ctx.defer = env, (send_splits, recv_splits), defer_grad
+        out, handle.work = env.all_to_all_async(x.contiguous(), send_splits, recv_splits)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        send_splits, recv_splits = ctx.splits
+        gx, work = ctx.env.all_to_all_async(g.contiguous(), recv_splits, send_splits)
+        if ctx.defer:
+            ops.defer_until(gx, work)
+        else:
+            work.wait()
+        return gx, None, None, None, None, None
+
+
 def user_range(n_users: int, world: int, rank: int) -> Tuple[int, int]:
     m = -(-n_users // world)
     lo = min(n_users, rank * m)
@@ -243,46 +283,180 @@ class HipImpl:
                                  n_edges_total=n_total, cscale=cscale)
 
 
-class UserShard:
-    """Static per-rank structures for the engages relation (and its reverse)."""
+def model_layers(model) -> List[Tuple[Dict[str, torch.nn.Module], Layout]]:
+    """[(convs, layout)] per layer: ``HeteroSAGE`` (relation list, L layers) or a
+    ``WeightedRGCN``-style layout model (one layer, ``train_gnn.py:155-200``)."""
+    if isinstance(model, HeteroSAGE):
+        layout: Layout = {}
+        for et, w in model.relations:
+            layout.setdefault(et[2], []).append(("__".join(et), et, w))
+        return [(convs, layout) for convs in model.layers]
+    if isinstance(model, _LayoutModel):
+        lay = model.layout
+        return [({n: getattr(model, n) for msgs in lay.values() for n, _, _ in msgs}, lay)]
+    raise TypeError(f"no partitioned forward for {type(model).__name__}")
 
-    def __init__(self, engage_edges: torch.Tensor, n_users: int, n_posts: int, env: DistEnv,
-                 impl=None, pos_weights: Optional[torch.Tensor] = None):
+
+@dataclasses.dataclass
+class _Rel:
+    """One relation's share on this rank: its kind ((src type, dst type)), local CSR and (for
+    user->post partial sums) the per-position 1/deg_global weights."""
+    kind: Tuple[str, str]
+    csr: object
+    w_fwd: Optional[torch.Tensor] = None
+    w_bwd: Optional[torch.Tensor] = None
+
+
+@dataclasses.dataclass
+class _Halo:
+    """Remote source users of this rank's user->user edges.  ``rel_send`` picks the owned rows
+    every peer asked for (grouped by peer; a K1 gather of degree-1 rows whose K2 adjoint sums the
+    returned gradients per row, deterministically); received rows follow in rank order, so halo
+    row k is ``remote[k]``."""
+    rel_send: object
+    send_splits: List[int]
+    recv_splits: List[int]
+    n_halo: int
+
+
+class UserShard:
+    """Static per-rank structures of a destination-partitioned user<->post graph.
+
+    ``edges``: the global ``edge_index_dict`` (any of ``post->user``, ``user->user``,
+    ``user->post``, ``post->post`` relations; ``engages`` is also the loss's positive edges) or,
+    for the two-relation training graph, the global ``engages`` tensor alone (its flip is the
+    ``rev_engages`` relation, ``train_gnn.py:142``).  Rank r owns users [lo, hi) and post rows
+    [p_lo, p_hi) of the table padded to world * S rows:
+
+    * post->user  (rev_engages, followed_by): edges into owned users; sources from the full
+      (all-gathered) post table — complete locally;
+    * user->user  (social): edges into owned users; remote sources arrive by one all-to-all
+      halo exchange per layer (the rows each peer asked for at setup), gradients return by the
+      reverse exchange;
+    * user->post  (engages): edges out of owned users, each pre-scaled by 1/deg_global(post);
+      partial sums over the padded table, one reduce-scatter per relation gives the exact
+      mean of the owned slice;
+    * post->post: edges into owned post rows, sources from the full post table.
+    """
+
+    def __init__(self, edges, n_users: int, n_posts: int, env: DistEnv, impl=None,
+                 pos_weights: Optional[torch.Tensor] = None):
         impl = impl or HipImpl()
         self.env, self.impl = env, impl
+        if torch.is_tensor(edges):
+            edges = {ENGAGES: edges, REV_ENGAGES: edges.flip(0)}
         self.n_users, self.n_posts = n_users, n_posts
         self.lo, self.hi = user_range(n_users, env.world, env.rank)
-        u, p = engage_edges[0], engage_edges[1]
-        self.mask = (u >= self.lo) & (u < self.hi)
-        self.pos_local = torch.stack([u[self.mask] - self.lo, p[self.mask]]).contiguous()
-        self.rev_local = self.pos_local.flip(0).contiguous()
         self.n_own = self.hi - self.lo
-        self.num_edges_global = int(engage_edges.shape[1])
         # post table padded to world * S rows; rank r owns rows [r*S, r*S+S)
         self.post_rows, self.p_lo, self.p_hi = env.post_slice(n_posts)
         self.n_posts_pad = self.post_rows * env.world
-        deg = torch.bincount(self.pos_local[1], minlength=self.n_posts_pad).to(torch.float32)
-        env.all_reduce_(deg)
-        self.inv_deg_post = torch.where(deg > 0, 1.0 / deg.clamp(min=1.0), torch.zeros_like(deg))
-        self.rel_eng = impl.relation(self.pos_local, self.n_own, self.n_posts_pad)
-        self.rel_rev = impl.relation(self.rev_local, self.n_posts_pad, self.n_own)
-        self.w_eng_fwd = impl.edge_weights_fwd(self.rel_eng, self.inv_deg_post)
-        self.w_eng_bwd = impl.edge_weights_bwd(self.rel_eng, self.inv_deg_post)
+        n_of = {"user": n_users, "post": n_posts}
+        for et, ei in edges.items():
+            if et[0] not in n_of or et[2] not in n_of:
+                raise ValueError(f"relation {et}: node types must be 'user' / 'post'")
+        # the loss's positive edges: engages out of owned users (same tensor as the relation's
+        # local edges, so the loss finds the cached CSR)
+        self.mask = None
+        self.pos_local = None
+        self.num_edges_global = 0
+        self.rels: Dict[EdgeType, _Rel] = {}
+        uu = [et for et in edges if (et[0], et[2]) == ("user", "user")]
+        remote = None
+        if uu:
+            src_all = torch.cat([edges[et][0][self._owned_users(edges[et][1])] for et in uu])
+            remote = torch.unique(src_all[~self._owned_users(src_all)])   # sorted
+        self.halo = self._setup_halo(remote) if remote is not None else None
+        for et, ei in edges.items():
+            self.rels[et] = self._local_relation(et, ei, remote)
+        if ENGAGES in edges:
+            self.num_edges_global = int(edges[ENGAGES].shape[1])
         self.cscale = None
         if pos_weights is not None:   # global mean of the interaction weights (static)
+            if self.mask is None:
+                raise ValueError("pos_weights given but the graph has no engages relation")
             s = torch.stack([pos_weights[self.mask].to(torch.float64).sum(),
                              torch.tensor(float(self.mask.sum()), dtype=torch.float64,
                                           device=pos_weights.device)])
             env.all_reduce_(s)
             self.cscale = (s[0] / s[1]).to(torch.float32)
 
+    # ------------------------------------------------------------------ setup
+    def _owned_users(self, ids: torch.Tensor) -> torch.Tensor:
+        return (ids >= self.lo) & (ids < self.hi)
+
+    def _local_relation(self, et, ei: torch.Tensor, remote) -> _Rel:
+        impl, kind = self.impl, (et[0], et[2])
+        src, dst = ei[0], ei[1]
+        if kind == ("post", "user"):
+            m = self._owned_users(dst)
+            local = torch.stack([src[m], dst[m] - self.lo]).contiguous()
+            return _Rel(kind, impl.relation(local, self.n_posts_pad, self.n_own))
+        if kind == ("user", "user"):
+            m = self._owned_users(dst)
+            s = src[m]
+            own = self._owned_users(s)
+            if remote is not None and remote.numel():
+                pos = torch.searchsorted(remote, s).clamp_(max=remote.numel() - 1)
+                ext = torch.where(own, s - self.lo, self.n_own + pos)
+            else:
+                ext = s - self.lo
+            local = torch.stack([ext, dst[m] - self.lo]).contiguous()
+            n_halo = self.halo.n_halo if self.halo is not None else 0
+            return _Rel(kind, impl.relation(local, self.n_own + n_halo, self.n_own))
+        if kind == ("user", "post"):
+            m = self._owned_users(src)
+            local = torch.stack([src[m] - self.lo, dst[m]]).contiguous()
+            deg = torch.bincount(local[1], minlength=self.n_posts_pad).to(torch.float32)
+            self.env.all_reduce_(deg)
+            inv = torch.where(deg > 0, 1.0 / deg.clamp(min=1.0), torch.zeros_like(deg))
+            rel = impl.relation(local, self.n_own, self.n_posts_pad)
+            if et == ENGAGES:
+                self.mask, self.pos_local = m, local
+                self.rev_local = local.flip(0).contiguous()
+            return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv))
+        # post -> post: edges into the owned slice of the post table
+        m = (dst >= self.p_lo) & (dst < self.p_hi)
+        local = torch.stack([src[m], dst[m] - self.p_lo]).contiguous()
+        return _Rel(kind, impl.relation(local, self.n_posts_pad, self.post_rows))
+
+    def _setup_halo(self, remote: torch.Tensor) -> _Halo:
+        """Tell every owner which of its rows this rank needs (two all-to-alls, once)."""
+        env, world = self.env, self.env.world
+        m = -(-self.n_users // world)
+        owner = torch.div(remote, m, rounding_mode="floor")
+        recv = torch.bincount(owner, minlength=world).to(torch.int64)
+        ones = [1] * world
+        send, work = env.all_to_all_async(recv, ones, ones)
+        work.wait()
+        recv_splits, send_splits = recv.tolist(), send.tolist()
+        ids, work = env.all_to_all_async(remote.contiguous(), recv_splits, send_splits)
+        work.wait()
+        n_send = int(sum(send_splits))
+        dev = remote.device
+        pick = torch.stack([ids - self.lo, torch.arange(n_send, dtype=torch.int64, device=dev)])
+        rel_send = self.impl.relation(pick.contiguous(), self.n_own, n_send)
+        self._halo_pick = pick          # keeps the cached CSR's key alive
+        return _Halo(rel_send, send_splits, recv_splits, int(sum(recv_splits)))
+
     def local_edges_of(self, per_edge: torch.Tensor) -> torch.Tensor:
         """Slice a per-global-edge tensor (e.g. injected negatives) to this rank's edges."""
         return per_edge[self.mask]
 
-    def forward(self, model: HeteroSAGE, x_user_own: torch.Tensor, x_post: torch.Tensor):
-        """Partitioned forward of ``model``; returns (owned user embeddings, post embeddings of
-        the whole padded table — rows >= n_posts are padding)."""
+    # ---------------------------------------------------------------- forward
+    def _halo_start(self, h_u: torch.Tensor, defer: bool):
+        if self.halo is None or self.env.world == 1:
+            return None, Pending()
+        hl = self.halo
+        x_send = self.impl.mean_gather(h_u, hl.rel_send)
+        pend = Pending()
+        recv = _AllToAll.apply(x_send, self.env, hl.send_splits, hl.recv_splits, pend, defer)
+        return recv, pend
+
+    def forward(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor):
+        """Partitioned forward of ``model`` (``HeteroSAGE`` or a ``WeightedRGCN`` layout);
+        returns (owned user embeddings, post embeddings of the whole padded table — rows >=
+        n_posts are padding)."""
         impl, env = self.impl, self.env
         if x_post.shape[0] != self.n_posts_pad:
             x_post = torch.nn.functional.pad(x_post, (0, 0, 0, self.n_posts_pad - x_post.shape[0]))
@@ -290,33 +464,59 @@ class UserShard:
         h_p_own = x_post[self.p_lo:self.p_hi]
         gathered = None                       # in-flight all-gather of h_p
         defer = getattr(impl, "defer_grad", False)
-        nu = "__".join(REV_ENGAGES)
-        np_ = "__".join(ENGAGES)
-        wts = dict(model.relations)
-        for convs in model.layers:
+        for convs, layout in model_layers(model):
             shapes = {"user": h_u, "post": h_p}
-            Wu, bu = _fused_weights(convs, [(nu, REV_ENGAGES, wts[REV_ENGAGES])], shapes)
-            Wp, bp = _fused_weights(convs, [(np_, ENGAGES, wts[ENGAGES])], shapes)
-            # post partial sums first; their reduce-scatter is in flight during the user side
-            s_post = impl.weighted_gather(h_u, self.rel_eng, self.w_eng_fwd, self.w_eng_bwd)
-            if env.world == 1:
-                a_post, pend = s_post, Pending()
-            else:
-                pend = Pending()
-                a_post = _ReduceScatter.apply(s_post, env, pend, defer)
+            umsgs, pmsgs = layout.get("user", []), layout.get("post", [])
+            for _, et, _ in umsgs + pmsgs:
+                if et not in self.rels:
+                    raise KeyError(f"relation {et} is not in the sharded graph")
+            # 1. halo rows out, 2. post partial sums out: both collectives in flight while the
+            # local gathers below run
+            halo, halo_pend = (self._halo_start(h_u, defer) if any(
+                et[0] == "user" for _, et, _ in umsgs) else (None, Pending()))
+            a_post = {}
+            for _, et, _ in pmsgs:
+                r = self.rels[et]
+                if r.kind[0] == "user":
+                    s = impl.weighted_gather(h_u, r.csr, r.w_fwd, r.w_bwd)
+                    pend = Pending()
+                    a_post[et] = ((_ReduceScatter.apply(s, env, pend, defer), pend)
+                                  if env.world > 1 else (s, pend))
             if gathered is not None:          # the previous layer's all-gather of h_p
                 gathered.wait()
                 gathered = None
-            a_user = impl.mean_gather(h_p, self.rel_rev)
-            h_u_next = impl.fused_linear([a_user, h_u], Wu, bu, True)
-            pend.wait()
-            # the post projection runs on this rank's slice only
-            h_p_own = impl.fused_linear([a_post, h_p_own], Wp, bp, True)
-            if env.world == 1:
-                h_p = h_p_own
-            else:
-                gathered = Pending()
-                h_p = _AllGather.apply(h_p_own, env, gathered)
+            h_u_next = h_u
+            if umsgs:
+                Wu, bu = _fused_weights(convs, umsgs, shapes)
+                segs, x_ext = [], None
+                for _, et, _ in umsgs:
+                    r = self.rels[et]
+                    if r.kind[0] == "post":
+                        segs.append(impl.mean_gather(h_p, r.csr))
+                    else:
+                        if x_ext is None:
+                            halo_pend.wait()
+                            x_ext = h_u if halo is None else torch.cat([h_u, halo])
+                        segs.append(impl.mean_gather(x_ext, r.csr))
+                h_u_next = impl.fused_linear(segs + [h_u], Wu, bu, True)
+            if pmsgs:
+                Wp, bp = _fused_weights(convs, pmsgs, shapes)
+                segs = []
+                for _, et, _ in pmsgs:
+                    r = self.rels[et]
+                    if r.kind[0] == "post":
+                        segs.append(impl.mean_gather(h_p, r.csr))
+                    else:
+                        a, pend = a_post[et]
+                        pend.wait()
+                        segs.append(a)
+                # the post projection runs on this rank's slice only
+                h_p_own = impl.fused_linear(segs + [h_p_own], Wp, bp, True)
+                if env.world == 1:
+                    h_p = h_p_own
+                else:
+                    gathered = Pending()
+                    h_p = _AllGather.apply(h_p_own, env, gathered)
             h_u = h_u_next
         if gathered is not None:
             gathered.wait()
