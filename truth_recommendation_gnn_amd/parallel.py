@@ -1,33 +1,32 @@
-"""Multi-GPU hetero-SAGE: users sharded across ranks, posts replicated, RCCL all-reduce.
+"""Multi-GPU hetero-SAGE: destination-partitioned, one process per GPU over RCCL.
 
 One process per GPU (``torch.distributed``, backend ``nccl`` = RCCL over xGMI).  The user <-> post
 graph is partitioned by USER (contiguous id ranges, the 10x larger node type), and the post
-TABLE by row slices:
+TABLE by row slices (``UserShard`` has the per-relation placement):
 
-* rank r owns users [lo_r, hi_r) and every engages edge whose user it owns, so
-  - the user-destination aggregation (``rev_engages``: post -> user, mean over the user's
-    in-edges) is complete on the owner — no exchange (it reads the all-gathered post table);
-  - the post-destination aggregation (``engages``: user -> post) is a per-rank PARTIAL sum over
-    the rank's edges, each edge pre-scaled by 1/deg_global(post) (K1 with per-edge weights);
-* rank r also owns a slice of post rows: one reduce-scatter gives it the exact mean for its
-  slice, the post projection (K3) runs on that slice only, and one all-gather rebuilds the full
-  post table for the next layer's user side and for the loss.  A reduce-scatter + all-gather
-  moves what one all-reduce does, and the post-side compute is divided by the world size instead
-  of replicated;
-* backward: the all-gather's adjoint is a reduce-scatter of the post-table gradient (the loss's
-  dP and the user side's K2 output, both partial), the reduce-scatter's adjoint an all-gather of
-  the slice gradients, which K2 (weights transposed) sends to the owned users; parameter gradients
-  are summed over ranks with one flat all-reduce.
+* post -> user relations (``rev_engages``): edges into owned users, read the all-gathered post
+  table — complete on the owner, no exchange;
+* user -> user relations (``social``): edges into owned users; the remote source rows (the halo)
+  arrive by one all-to-all per layer with static split sizes, and their gradients go back by the
+  reverse all-to-all;
+* user -> post relations (``engages``): a per-rank PARTIAL sum over the rank's edges, each edge
+  pre-scaled by 1/deg_global(post) (K1 with per-edge weights); one reduce-scatter gives each rank
+  the exact mean of its post slice, the post projection (K3) runs on that slice only, and one
+  all-gather rebuilds the full post table for the next layer and the loss.  A reduce-scatter +
+  all-gather moves what one all-reduce does, and the post-side compute is divided by the world
+  size instead of replicated;
+* post -> post relations (cfg5): edges into the owned post slice, read the full post table;
+* backward: every collective's adjoint (all-gather <-> reduce-scatter, all-to-all reversed);
+  parameter gradients are summed with one flat all-reduce;
 * the link loss is sharded the same way: rank r scores the positive edges of its users against
   the gathered post table; normalised by the GLOBAL edge count and mean(pos_weights), the
   per-rank losses add up to the reference loss (``train_gnn.py:259-281``).
 
-Per step: reduce-scatter + all-gather per layer forward, reduce-scatter + all-gather for the
-layer-2 post gradients and one reduce-scatter for the layer-1 post input gradient, plus the weight
-gradients.  All are asynchronous: the forward ones overlap the user side of the same (or next)
-layer; the gradient all-gather is handed on unfinished to its only consumer (K2's backward) so the
-user-side backward autograd runs before it overlaps it.  The compute ops are injected
-(``HipImpl`` here; the CPU gloo tests inject plain-torch ops to check the partitioning logic).
+All collectives are asynchronous: the forward ones overlap the local gathers of the same (or
+next) layer; gradient exchanges are handed on unfinished (``ops.defer_until``) to their single
+consumer so the backward kernels autograd runs in between overlap them.  The compute ops are
+injected (``HipImpl`` here; the CPU gloo tests inject plain-torch ops to check the partitioning
+logic).
 """
 from __future__ import annotations
 
