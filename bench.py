@@ -187,7 +187,8 @@ def main():
         cfg = gcfg
 
         def forward_loss():
-            h_u, h_p = shard.forward(model, x_user, x_post)
+            # the post table's last all-gather stays in flight under the negatives draw + sort
+            h_u, h_p = shard.forward(model, x_user, x_post, wait=False)
             neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
             return shard.loss(h_u, h_p, neg, neg_order="user")
 

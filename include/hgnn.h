@@ -194,6 +194,10 @@ int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n
  * 64-bit seed at d_seed (device memory: a torch Generator draws it without a host sync). */
 int hgnn_uniform_i32(const uint64_t* d_seed, int64_t n, int32_t hi, int32_t* out,
                      hgnn_stream_t stream);
+/* x[0:n] *= *d_scale in place, a no-op when *d_scale == 1 (read on the device).  The fused
+ * loss's autograd backward: its dU/dP are formed in the forward and scaled by the incoming
+ * gradient (1 for loss.backward()).  x 16-byte aligned. */
+int hgnn_scale_unless_one(float* x, int64_t n, const float* d_scale, hgnn_stream_t stream);
 
 /* ---- neighbour sampling for mini-batches (BASELINE cfg5; no reference counterpart) -----------
  * For each destination dst_ids[i] (rows of a destination-grouped CSR rowptr/col over n_rows):

@@ -34,7 +34,9 @@ class TorchImpl:
         return F.relu(y) if relu else y
 
     @staticmethod
-    def edge_bce_loss(U, P, pos, neg, n_total, cscale, neg_order="edge"):
+    def edge_bce_loss(U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None):
+        if ready is not None:
+            ready()
         u = U[pos[0]]
         s_pos = (u * P[pos[1]]).sum(1)
         s_neg = (u * P[neg]).sum(1)

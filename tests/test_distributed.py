@@ -40,7 +40,7 @@ def _worker(rank, world, port, q, kind="engage2"):
         shard = UserShard(edges, cfg.num_users, cfg.num_posts, env, impl=TorchImpl(),
                           pos_weights=pw)
         lo, hi = user_range(cfg.num_users, world, rank)
-        h_u, h_p = shard.forward(model, g.x_dict["user"][lo:hi], g.x_dict["post"])
+        h_u, h_p = shard.forward(model, g.x_dict["user"][lo:hi], g.x_dict["post"], wait=False)
         loss = shard.loss(h_u, h_p, shard.local_edges_of(neg))
         loss.backward()
         sync_grads(model, env)

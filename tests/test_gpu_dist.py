@@ -100,7 +100,7 @@ def _case_worker(rank, world, port, q, kind):
         shard = parallel.UserShard(ed, cfg.num_users, cfg.num_posts, env,
                                    pos_weights=pw.to(dev))
         xu = g.x_dict["user"].to(dev)[shard.lo:shard.hi].contiguous()
-        h_u, h_p = shard.forward(model, xu, g.x_dict["post"].to(dev))
+        h_u, h_p = shard.forward(model, xu, g.x_dict["post"].to(dev), wait=False)
         loss = shard.loss(h_u, h_p, shard.local_edges_of(neg.to(dev)))
         loss.backward()
         parallel.sync_grads(model, env)

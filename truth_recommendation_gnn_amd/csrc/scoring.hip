@@ -306,6 +306,37 @@ __global__ void k_uniform_i32(const uint64_t* seed, int64_t n, uint32_t hi, int3
   out[i] = (int32_t)(((x >> 32) * (uint64_t)hi) >> 32);
 }
 
+// x *= *s in place, skipped entirely when *s == 1 (read on the device: no host sync).  The
+// loss's backward scales its precomputed dU/dP by the incoming gradient, which is exactly 1 for
+// loss.backward(); the early exit turns a 256 MB read-modify-write into one launch.
+__global__ void k_scale_unless_one(float* x, int64_t n, const float* s) {
+  const float g = *s;
+  if (g == 1.0f) return;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float4* x4 = reinterpret_cast<float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = x4[i];
+    v.x *= g; v.y *= g; v.z *= g; v.w *= g;
+    x4[i] = v;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    x[i] *= g;
+}
+
+int hgnn_scale_unless_one(float* x, int64_t n, const float* d_scale, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (n < 0) return fail(HGNN_E_ARG, "scale_unless_one: n=%lld", (long long)n);
+  if (n == 0) return HGNN_OK;
+  if (!x || !d_scale) return fail(HGNN_E_ARG, "scale_unless_one: null pointer");
+  if (reinterpret_cast<uintptr_t>(x) & 15)
+    return fail(HGNN_E_ARG, "scale_unless_one: x must be 16-byte aligned");
+  const int64_t blocks = std::min<int64_t>(cdiv(cdiv(n, 4), 256), 2048);
+  hipLaunchKernelGGL(k_scale_unless_one, dim3((unsigned)blocks), dim3(256), 0, stream, x, n,
+                     d_scale);
+  return check_launch("k_scale_unless_one");
+}
+
 int hgnn_uniform_i32(const uint64_t* d_seed, int64_t n, int32_t hi, int32_t* out,
                      hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);

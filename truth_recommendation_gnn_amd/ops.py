@@ -398,7 +398,8 @@ def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tens
 
 class _EdgeBCELoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int):
+    def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
+                ready=None):
         U = _check_f32(U, "edge_bce_loss user_emb")
         P = _check_f32(P, "edge_bce_loss post_emb")
         dev = N.require_device(U, P, neg_u_order)
@@ -439,6 +440,13 @@ class _EdgeBCELoss(torch.autograd.Function):
                         N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
                         None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
                         "hgnn_sort_pairs_i64")
+        if ready is not None:
+            # P is still arriving (parallel.py's all-gather of the post table): the sort above
+            # needs only the edges, so it ran ahead; every kernel below reads P
+            ready()
+            if lanes.side is not None:
+                lanes.side.wait_stream(lanes.main)
+        with torch.cuda.stream(lanes.stream(1)):
             _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
             from .graph import GroupedEdges, Plan
             negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
@@ -463,21 +471,28 @@ class _EdgeBCELoss(torch.autograd.Function):
     @staticmethod
     def backward(ctx, go):
         dU, dP = ctx.saved_tensors
-        return dU.mul_(go), dP.mul_(go), None, None, None, None, None
+        g = go.to(torch.float32).reshape(()).contiguous()
+        lib, s = N.lib(), N.stream_ptr(dU.device)
+        for t in (dU, dP):   # in place; a no-op launch for loss.backward()'s gradient of 1
+            N.check(lib.hgnn_scale_unless_one(N.ptr(t), t.numel(), N.ptr(g), s),
+                    "hgnn_scale_unless_one")
+        return dU, dP, None, None, None, None, None, None
 
 
 def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
                   neg_p: torch.Tensor, pos_weights: Optional[torch.Tensor],
                   neg_order: str = "edge", check: bool = True,
                   n_edges_total: Optional[int] = None,
-                  cscale: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  cscale: Optional[torch.Tensor] = None, ready=None) -> torch.Tensor:
     """Fused HIP version of :func:`link_loss` (same value, same gradients).
 
     ``neg_order='edge'``: ``neg_p[e]`` is the negative of COO edge e (the reference's layout);
     ``'user'``: already in the user-grouped order (what :func:`sample_negatives` draws).
     ``check`` costs one host sync (the reference syncs every step with ``loss.item()``).
     ``n_edges_total`` / ``cscale`` (= mean of ALL pos_weights) let a shard of the positive edges
-    produce its additive share of the global loss (parallel.py)."""
+    produce its additive share of the global loss (parallel.py); ``ready()``, if given, is
+    called once the negatives sort is enqueued and before any kernel reads ``post_emb`` (the
+    sharded path's post-table all-gather finishes under the sort)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     if neg_p.shape[0] != csr.num_edges:
         raise ValueError("one negative per positive edge is required (train_gnn.py:272)")
@@ -485,7 +500,7 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
     if cscale is None:
         cscale = pos_weights.to(torch.float32).mean()
     n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
-    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total)
+    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total, ready)
 
 
 def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:

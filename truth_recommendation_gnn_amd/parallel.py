@@ -277,9 +277,9 @@ class HipImpl:
     fused_linear = staticmethod(ops.fused_linear)
 
     @staticmethod
-    def edge_bce_loss(U, P, pos, neg, n_total, cscale, neg_order="edge"):
+    def edge_bce_loss(U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None):
         return ops.edge_bce_loss(U, P, pos, neg, None, neg_order=neg_order, check=False,
-                                 n_edges_total=n_total, cscale=cscale)
+                                 n_edges_total=n_total, cscale=cscale, ready=ready)
 
 
 def model_layers(model) -> List[Tuple[Dict[str, torch.nn.Module], Layout]]:
@@ -452,10 +452,12 @@ class UserShard:
         recv = _AllToAll.apply(x_send, self.env, hl.send_splits, hl.recv_splits, pend, defer)
         return recv, pend
 
-    def forward(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor):
+    def forward(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor,
+                wait: bool = True):
         """Partitioned forward of ``model`` (``HeteroSAGE`` or a ``WeightedRGCN`` layout);
         returns (owned user embeddings, post embeddings of the whole padded table — rows >=
-        n_posts are padding)."""
+        n_posts are padding).  ``wait=False`` leaves the last all-gather of the post table in
+        flight for :meth:`loss`, which waits on it only after enqueueing the negatives sort."""
         impl, env = self.impl, self.env
         if x_post.shape[0] != self.n_posts_pad:
             x_post = torch.nn.functional.pad(x_post, (0, 0, 0, self.n_posts_pad - x_post.shape[0]))
@@ -517,16 +519,20 @@ class UserShard:
                     gathered = Pending()
                     h_p = _AllGather.apply(h_p_own, env, gathered)
             h_u = h_u_next
-        if gathered is not None:
-            gathered.wait()
+        self._post_pending = gathered or Pending()
+        if wait:
+            self._post_pending.wait()
         return h_u, h_p
 
     def loss(self, h_u_own, h_p, neg_local, neg_order="edge"):
         """This rank's additive share of the reference loss."""
         if self.cscale is None:
             raise ValueError("UserShard built without pos_weights")
+        pend = getattr(self, "_post_pending", None) or Pending()
+        self._post_pending = None
         return self.impl.edge_bce_loss(h_u_own, h_p, self.pos_local, neg_local,
-                                       self.num_edges_global, self.cscale, neg_order=neg_order)
+                                       self.num_edges_global, self.cscale, neg_order=neg_order,
+                                       ready=pend.wait)
 
 
 def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
