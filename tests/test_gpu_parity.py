@@ -408,10 +408,18 @@ def test_weighted_rgcn_fused_loss_step_matches_golden():
                                   (300000, 800000),      # 20 bits: 3 passes of 8
                                   (200000, 300000),      # 19 bits: 3 passes of 8
                                   (5000, 900),           # 10 bits: 2 passes of 8
-                                  (50000, 3_000_000)])   # 22 bits: 3 passes of 8
+                                  (50000, 3_000_000),    # 22 bits: 3 passes of 8
+                                  (8192, 1000),          # exactly one onesweep tile
+                                  (8193, 100),           # one item in a second tile
+                                  (2_500_001, 100_000),  # 306 tiles of look-back, ragged tail
+                                  (40000, -1)])          # every key equal: one digit holds all
 def test_sort_pairs_matches_numpy(E, nk):
-    rng = np.random.default_rng(9 + nk)
-    keys = torch.from_numpy(rng.integers(0, nk, E).astype(np.int32))
+    rng = np.random.default_rng(9 + abs(nk))
+    if nk < 0:
+        nk = 5000
+        keys = torch.full((E,), 4321, dtype=torch.int32)
+    else:
+        keys = torch.from_numpy(rng.integers(0, nk, E).astype(np.int32))
     a = torch.arange(E, dtype=torch.int32)
     b = torch.from_numpy(rng.integers(-5, 5, E).astype(np.int32))
     from truth_recommendation_gnn_amd import _native as Nn

@@ -8,6 +8,7 @@
 // oracle/csr_ref.py.
 #include "hgnn_common.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace hgnn {
@@ -166,20 +167,25 @@ __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const 
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(invalid, __popcll(m));
 }
 
-// counts[digit * nblocks + block] for this block's tile (RADIX = 1 << BITS digits).
-template <int BITS>
+// counts[digit * nblocks + block] for this block's tile (RADIX = 1 << BITS digits).  Every key of
+// the tile is loaded before the first LDS atomic, so all RR loads per thread are in flight.
+template <int BITS, int RR = kSortRounds>
 __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
                                                                int shift, int32_t* counts) {
   constexpr int R = 1 << BITS;
   __shared__ int hist[R];
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) hist[dd] = 0;
-  __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kSortTile;
-#pragma unroll 4
-  for (int r = 0; r < kSortRounds; ++r) {
-    int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
-    if (i < E) atomicAdd(&hist[(keys[i] >> shift) & (R - 1)], 1);
+  const int64_t base = (int64_t)blockIdx.x * (kSortThreads * RR);
+  int k[RR];
+#pragma unroll
+  for (int r = 0; r < RR; ++r) {
+    const int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
+    k[r] = i < E ? keys[i] : -1;
   }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < RR; ++r)
+    if (k[r] >= 0) atomicAdd(&hist[(k[r] >> shift) & (R - 1)], 1);
   __syncthreads();
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads)
     counts[(int64_t)dd * gridDim.x + blockIdx.x] = hist[dd];
@@ -201,19 +207,20 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
   return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-template <int BITS, bool HAS_B>
+template <int BITS, bool HAS_B, int RR = kSortRounds>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
     const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
   constexpr int R = 1 << BITS;
   constexpr int NW = kSortThreads / 64;
-  constexpr int PER_WAVE = kSortTile / NW;       // 1024
+  constexpr int TILE = kSortThreads * RR;
+  constexpr int PER_WAVE = TILE / NW;
   __shared__ int wcount[NW][R];                  // running count -> wave offset within tile
   __shared__ int dstart[R];                      // tile-local start of each digit
   __shared__ int gbase[R];                       // global start of this tile's digit run
-  __shared__ int skey[kSortTile];
-  __shared__ int sa[kSortTile];
-  __shared__ int sb[HAS_B ? kSortTile : 1];
+  __shared__ int skey[TILE];
+  __shared__ int sa[TILE];
+  __shared__ int sb[HAS_B ? TILE : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
@@ -222,16 +229,23 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   }
   __syncthreads();
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t tile0 = tile * kSortTile;
+  const int64_t tile0 = tile * TILE;
   const int64_t wave0 = tile0 + (int64_t)wid * PER_WAVE;
-  int key[kSortRounds], rank[kSortRounds], va[kSortRounds], vb[kSortRounds];
+  int key[RR], rank[RR], va[RR], vb[RR];
+  // every load of the tile issued before the ranking: the wave barriers and LDS traffic of the
+  // ranking loop would otherwise keep the compiler from hoisting them, one HBM latency per round
 #pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
+  for (int r = 0; r < RR; ++r) {
     const int64_t i = wave0 + r * 64 + lane;
     const bool valid = i < E;
     key[r] = valid ? keys_in[i] : 0;
     va[r] = valid ? (identity_a ? (int)i : a_in[i]) : 0;
     vb[r] = (HAS_B && valid) ? b_in[i] : 0;
+  }
+#pragma unroll
+  for (int r = 0; r < RR; ++r) {
+    const int64_t i = wave0 + r * 64 + lane;
+    const bool valid = i < E;
     const int digit = (key[r] >> shift) & (R - 1);
     unsigned long long match = __ballot(valid);
 #pragma unroll
@@ -287,7 +301,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < kSortRounds; ++r) {
+  for (int r = 0; r < RR; ++r) {
     if (rank[r] >= 0) {
       const int digit = (key[r] >> shift) & (R - 1);
       const int pos = wcount[wid][digit] + rank[r];
@@ -297,7 +311,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     }
   }
   __syncthreads();
-  const int n_tile = (int)min<int64_t>(kSortTile, E - tile0);
+  const int n_tile = (int)min<int64_t>(TILE, E - tile0);
   for (int j = threadIdx.x; j < n_tile; j += kSortThreads) {
     const int k = skey[j];
     const int digit = (k >> shift) & (R - 1);
@@ -371,17 +385,37 @@ __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
   if (i < n) p[i] = v;
 }
 
-// Digit width: 9 bits when that saves a pass (17-18-bit keys: 2 passes instead of 3), else 8.
-// (10-bit digits, 2 passes for the 19-20-bit post ids of the 4-8 GPU runs, measured slower than
-// 3 passes: 1024 digits leave runs of ~4 items per 4096-item tile, too short to coalesce —
-// 9.76 vs 9.55 ms per rank-of-8 step.)
+// Digit width: the one of 6..9 bits minimising passes x measured per-pass time (counts + scan +
+// scatter, 20M pairs on MI355X: 6 bits 108 us, 7 bits 117, 8 bits 147, 9 bits 183 — fewer digits
+// mean longer per-digit runs per 4096-item tile, so a 6-bit pass writes ~256-B runs where a 9-bit
+// one writes ~32-B runs).  17-bit post ids: 3 passes of 6 (339 us) beat 2 of 9 (381); 20-bit:
+// 3 of 7.  (10-bit digits, 2 passes for 19-20-bit ids, were measured slower than 3 passes of 8.)
 static void radix_plan(int64_t n_keys, int* passes, int* bits) {
   int b = 0;
   while ((int64_t(1) << b) <= n_keys) ++b;   // keys in [0, n_keys] incl. sentinel
-  const int p8 = (b + 7) / 8, p9 = (b + 8) / 9;
-  *bits = p9 < p8 ? 9 : 8;
-  *passes = p9 < p8 ? p9 : p8;
+  static const int cost[10] = {0, 0, 0, 0, 0, 0, 108, 117, 147, 183};
+  int best = 6, best_cost = 1 << 30;
+  for (int d = 6; d <= 9; ++d) {
+    const int c = ((b + d - 1) / d) * cost[d];
+    if (c < best_cost) best_cost = c, best = d;
+  }
+  *bits = best;
+  *passes = (b + best - 1) / best;
+  static const int forced = getenv("HGNN_SORT_BITS") ? atoi(getenv("HGNN_SORT_BITS")) : 0;
+  if (forced >= 6 && forced <= 9) {   // measurement override
+    *bits = forced;
+    *passes = (b + forced - 1) / forced;
+  }
+  if (*passes < 1) *passes = 1;
 }
+
+#define HGNN_BITS_SWITCH(bits, M) \
+  switch (bits) {                 \
+    case 6: M(6); break;          \
+    case 7: M(7); break;          \
+    case 8: M(8); break;          \
+    default: M(9); break;         \
+  }
 
 static size_t sort_ws_bytes(int64_t E) {
   int64_t nb = cdiv(E, kSortTile);
@@ -421,19 +455,19 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
     int32_t* aout = to_out ? a_out : ta;
     int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
     const int ident = (p == 0 && a_in == nullptr) ? 1 : 0;
-    if (bits == 9)
-      hipLaunchKernelGGL(k_digit_counts<9>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E,
-                         shift, counts);
-    else
-      hipLaunchKernelGGL(k_digit_counts<8>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E,
-                         shift, counts);
+#define HGNN_COUNTS(BV) \
+  hipLaunchKernelGGL(k_digit_counts<BV>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift, counts)
+    HGNN_BITS_SWITCH(bits, HGNN_COUNTS)
+#undef HGNN_COUNTS
     if (int rc = check_launch("k_digit_counts")) return rc;
     if (int rc = exclusive_scan_i32(counts, offs, ncount, scan_ws, &scan_b, stream)) return rc;
 #define HGNN_SCATTER(BV, HB)                                                                 \
   hipLaunchKernelGGL((k_digit_scatter<BV, HB>), dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, \
                      bin, E, shift, offs, kout, aout, bout, ident)
-    if (bits == 9) { if (b_in) HGNN_SCATTER(9, true); else HGNN_SCATTER(9, false); }
-    else { if (b_in) HGNN_SCATTER(8, true); else HGNN_SCATTER(8, false); }
+#define HGNN_SCATTER_B(BV) \
+  if (b_in) { HGNN_SCATTER(BV, true); } else { HGNN_SCATTER(BV, false); }
+    HGNN_BITS_SWITCH(bits, HGNN_SCATTER_B)
+#undef HGNN_SCATTER_B
 #undef HGNN_SCATTER
     if (int rc = check_launch("k_digit_scatter")) return rc;
     kin = kout;
