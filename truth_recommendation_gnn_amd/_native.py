@@ -7,12 +7,17 @@ device, the call raises.
 from __future__ import annotations
 
 import ctypes
+import os
 import pathlib
 from typing import Optional, Sequence
 
 import torch
 
 LIB_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "libhgnn.so"
+# A/B measurement of two builds of the same library (scripts/*_bench.py): HGNN_LIB names another
+# in-tree build under lib/ (e.g. libhgnn_old.so); never a path outside the package.
+if os.environ.get("HGNN_LIB"):
+    LIB_PATH = LIB_PATH.parent / pathlib.Path(os.environ["HGNN_LIB"]).name
 
 HGNN_MEAN = 1
 HGNN_ACCUMULATE = 2
