@@ -62,7 +62,10 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   using V = Vec<W>;
   constexpr int NS = 64 / LPR;
   __shared__ float red[2][4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave index through readfirstlane: u, the row bounds and n are then scalar (wave-uniform to
+  // the compiler), so the step loop's exits are scalar branches and the waitcnt pass can count
+  // the in-flight prefetch across them
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int slot = lane / LPR, sl = lane % LPR;
   const int64_t u = (int64_t)blockIdx.x * 4 + wave;
   const float c = *a.cscale;
@@ -87,22 +90,28 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         else nid = (int)nn;
       }
       float my_hp = 0.f, my_hn = 0.f;
-      // software pipeline: step j+NS's row loads are in flight during step j's arithmetic
-      typename V::T vp[VPL], vn[VPL], wp[VPL], wn[VPL];
+      // Software pipeline over steps of NS edges, two register sets in ping-pong: the rows of
+      // step j+NS are in flight while step j is scored, with no register copy between steps (a
+      // copy reads the prefetched registers, so it made each step wait for the next one's loads).
+      // Loads are unconditional: lanes past the chunk read post 0 (pid/nid are 0 there) and
+      // columns past d read column 0; neither reaches a result (their hp/hn are zeroed below, uv
+      // is 0 past d, and the dU store is guarded).  Under exec-mask branches the compiler's
+      // waitcnt pass could not count the prefetch and waited for it before using the previous
+      // step's rows.
+      typename V::T ap[VPL], an[VPL], bp[VPL], bn[VPL];
       auto load_step = [&](int j, typename V::T (&xp)[VPL], typename V::T (&xn)[VPL]) {
         const int e = j + slot;
         const int pp = __shfl(pid, e & 63, 64), qq = __shfl(nid, e & 63, 64);
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
           const int cc = (q * LPR + sl) * W;
-          const bool ok = e < n && cc < d;
-          xp[q] = ok ? V::load(a.P + (int64_t)pp * d + cc) : V::zero();
-          xn[q] = ok ? V::load(a.P + (int64_t)qq * d + cc) : V::zero();
+          const int ccl = cc < d ? cc : 0;
+          xp[q] = V::load(a.P + (int64_t)pp * d + ccl);
+          xn[q] = V::load(a.P + (int64_t)qq * d + ccl);
         }
       };
-      load_step(0, vp, vn);
-      for (int j = 0; j < n; j += NS) {
-        if (j + NS < n) load_step(j + NS, wp, wn);
+      auto score_step = [&](int j, const typename V::T (&vp)[VPL],
+                            const typename V::T (&vn)[VPL]) {
         const int e = j + slot;
         const float sp = slot_dot<LPR, VPL, W>(uv, vp);
         const float sn = slot_dot<LPR, VPL, W>(uv, vn);
@@ -120,8 +129,6 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         for (int q = 0; q < VPL; ++q) {
           V::fma(acc[q], hp, vp[q]);
           V::fma(acc[q], hn, vn[q]);
-          vp[q] = wp[q];
-          vn[q] = wn[q];
         }
         // hand edge e's weights to lane e (lanes j .. j+NS-1 read from slot lane*LPR)
         const int src = ((lane - j) & (NS - 1)) * LPR;
@@ -129,6 +136,14 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         if (lane >= j && lane < j + NS) {
           my_hp = thp; my_hn = thn;
         }
+      };
+      load_step(0, ap, an);
+      for (int j = 0; j < n; j += 2 * NS) {
+        load_step(j + NS, bp, bn);
+        score_step(j, ap, an);
+        if (j + NS >= n) break;
+        load_step(j + 2 * NS, ap, an);
+        score_step(j + NS, bp, bn);
       }
       if (lane < n) {
         const int64_t k = base + lane;
