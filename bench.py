@@ -232,7 +232,8 @@ def main():
         # (user table, 256 MB at cfg2).  The post-table gathers (25.6 MB source) are served from
         # the 256 MB Infinity Cache and read above the HBM peak in algorithmic bytes; they are
         # listed under "kernels".
-        fwd = {k: v for k, v in kern.items() if k.startswith("gather_fwd")}
+        # (sharded runs: the post partial sums are the weighted forward gathers, "gather_wfwd")
+        fwd = {k: v for k, v in kern.items() if k.startswith(("gather_fwd", "gather_wfwd"))}
         if fwd:
             src_rows = lambda k: int(k.split("<-")[1].split("]")[0])
             name = max(fwd, key=src_rows)
@@ -246,12 +247,16 @@ def main():
                 with open(pmc) as f:
                     pm = json.load(f)
                 traffic, tsrc = pm.get("hbm_bytes_per_launch"), "profiles/pmc_gather_r1.json"
-            roof = {"bound": "hbm", "kernel": f"k_gather K1 mean fwd {name}",
+            weighted = name.startswith("gather_wfwd")
+            roof = {"bound": "hbm",
+                    "kernel": (f"k_gather K1 weighted fwd (post partial sums) {name}" if weighted
+                               else f"k_gather K1 mean fwd {name}"),
                     "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": tsrc, "avg_launch_us": round(per_launch_ms * 1e3, 1),
                     "algorithmic_bytes_per_launch": int(per_launch_bytes),
-                    "bytes_formula": "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d"}
+                    "bytes_formula": ("4*E*(2+d) + 4*(N_dst+1) + 4*N_dst*d" if weighted
+                                      else "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d")}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, args.cpu_threads)

@@ -106,7 +106,7 @@ def gather_mean(x_src: torch.Tensor, csr: RelationCSR) -> torch.Tensor:
     return out
 
 
-def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
+def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None, kind=None):
     p = grouped.plan
     dev = out.device
     slab = None
@@ -115,7 +115,7 @@ def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None):
     flags = (N.HGNN_MEAN if csr_mean else 0) | (N.HGNN_ACCUMULATE if accumulate else 0)
     d = int(out.shape[1])
     weighted = edge_w is not None or col_w is not None
-    kind = "fwd" if csr_mean else "bwd"
+    kind = kind or ("fwd" if csr_mean else "bwd")   # "wfwd": weighted forward (parallel.py)
     name = f"gather_{kind}[{grouped.n_rows}<-{x.shape[0]}]x{d}"   # [dst rows <- src rows] x d
     E = int(grouped.col.numel())
     with _timed(name, gather_bytes(E, grouped.n_rows, d, weighted),
@@ -577,7 +577,8 @@ class _GatherWeighted(torch.autograd.Function):
     def forward(ctx, x_src, csr: RelationCSR, w_fwd, w_bwd):
         x_src = _check_f32(x_src, "weighted_gather")
         out = torch.empty(csr.n_dst, x_src.shape[1], dtype=torch.float32, device=x_src.device)
-        _gather(x_src, csr.fwd, None, csr_mean=False, out=out, accumulate=False, edge_w=w_fwd)
+        _gather(x_src, csr.fwd, None, csr_mean=False, out=out, accumulate=False, edge_w=w_fwd,
+                kind="wfwd")
         ctx.csr, ctx.w_bwd = csr, w_bwd
         return out
 
