@@ -412,7 +412,6 @@ class UserShard:
             rel = impl.relation(local, self.n_own, self.n_posts_pad)
             if et == ENGAGES:
                 self.mask, self.pos_local = m, local
-                self.rev_local = local.flip(0).contiguous()
             return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv))
         # post -> post: edges into the owned slice of the post table
         m = (dst >= self.p_lo) & (dst < self.p_hi)
@@ -435,7 +434,6 @@ class UserShard:
         dev = remote.device
         pick = torch.stack([ids - self.lo, torch.arange(n_send, dtype=torch.int64, device=dev)])
         rel_send = self.impl.relation(pick.contiguous(), self.n_own, n_send)
-        self._halo_pick = pick          # keeps the cached CSR's key alive
         return _Halo(rel_send, send_splits, recv_splits, int(sum(recv_splits)))
 
     def local_edges_of(self, per_edge: torch.Tensor) -> torch.Tensor:
