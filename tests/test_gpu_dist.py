@@ -38,6 +38,7 @@ def _worker(rank, world, port, q):
         model.load_state_dict(params)
         pw = torch.from_numpy(z["pos_weights"]).to(dev)
         env = parallel.DistEnv.from_torch()
+        env.side_adjoint = True      # the RCCL-path adjoints (side stream + deferred hand-off)
         shard = parallel.UserShard(ei, xu.shape[0], xp.shape[0], env, pos_weights=pw)
         assert shard.impl.defer_grad
         h_u, h_p = shard.forward(model, xu[shard.lo:shard.hi].contiguous(), xp)
@@ -96,6 +97,7 @@ def _case_worker(rank, world, port, q, kind):
         model.load_state_dict(params)
         model = model.to(dev)
         env = parallel.DistEnv.from_torch()
+        env.side_adjoint = True      # the RCCL-path adjoints (side stream + deferred hand-off)
         ed = {k: v.to(dev) for k, v in edges.items()}
         shard = parallel.UserShard(ed, cfg.num_users, cfg.num_posts, env,
                                    pos_weights=pw.to(dev))

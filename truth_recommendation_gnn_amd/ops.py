@@ -612,6 +612,7 @@ class _FusedLinear(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        await_pending(dy)    # a slice gradient whose reduce-scatter may be in flight (parallel.py)
         w, y, *segs = ctx.saved_tensors
         need = ctx.needs_input_grad
         dxs = [torch.empty_like(s) if need[3 + i] else None for i, s in enumerate(segs)]

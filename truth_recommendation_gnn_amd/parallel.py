@@ -51,6 +51,14 @@ class DistEnv:
     world: int = 1
     rank: int = 0
     group: Optional[object] = None
+    # backward all-gather adjoints finish on a side stream and are handed on unfinished (see
+    # _AllGather); None = with RCCL only.  Tests set True to run that path over gloo.
+    side_adjoint: Optional[bool] = None
+
+    def use_side_adjoint(self, t: torch.Tensor) -> bool:
+        if self.side_adjoint is not None:
+            return self.side_adjoint and t.is_cuda
+        return t.is_cuda and dist.get_backend(self.group) == "nccl"
 
     @classmethod
     def from_torch(cls) -> "DistEnv":
@@ -208,21 +216,68 @@ class _ReduceScatter(torch.autograd.Function):
         return full, None, None, None
 
 
+class _EventWait:
+    """A deferred gradient's completion as a recorded stream event (``ops.defer_until``)."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+        return True
+
+
+_SIDE: Dict[torch.device, torch.cuda.Stream] = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 class _AllGather(torch.autograd.Function):
-    """Concatenation of every rank's slice; adjoint: reduce-scatter of the gradient (waited at
-    once: autograd may add it to the slice's other gradients)."""
+    """Concatenation of every rank's slice; adjoint: reduce-scatter of the gradient.
+
+    With ``keep`` the slice is also returned as a second output (a copy) for the next layer's
+    root term, so the slice's two gradients — the reduce-scatter and the root's — meet inside
+    this backward rather than in autograd's accumulation, which would need the reduce-scatter
+    finished on the main stream.  Over RCCL (``defer``) the wait for the reduce-scatter and the
+    add run on a side stream, and the result is handed on unfinished to its single consumer
+    (the slice projection's backward, via ``ops.defer_until``): the main stream goes on with
+    the user-side backward while the collective runs."""
 
     @staticmethod
-    def forward(ctx, own, env: DistEnv, handle: "Pending"):
-        ctx.env = env
+    def forward(ctx, own, env: DistEnv, handle: "Pending", keep: bool, defer: bool):
+        ctx.env, ctx.defer = env, defer
         full, handle.work = env.all_gather_async(own.contiguous())
+        if keep:
+            return full, own.clone()
         return full
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, g_own=None):
         out, work = ctx.env.reduce_scatter_async(g.contiguous())
-        work.wait()
-        return out, None, None
+        if not (ctx.defer and ctx.env.use_side_adjoint(out)):
+            work.wait()
+            if g_own is not None:
+                out = out + g_own
+            return out, None, None, None, None
+        main = torch.cuda.current_stream(out.device)
+        side = _side_stream(out.device)
+        side.wait_stream(main)                # g_own (and the collective's input) are ready
+        with torch.cuda.stream(side):
+            work.wait()                       # the side stream waits for the reduce-scatter
+            if g_own is not None:
+                out.add_(g_own)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        out.record_stream(side)
+        if g_own is not None:
+            g_own.record_stream(side)
+        ops.defer_until(out, _EventWait(ev))
+        return out, None, None, None, None
 
 
 class _AllToAll(torch.autograd.Function):
@@ -463,7 +518,9 @@ class UserShard:
         h_p_own = x_post[self.p_lo:self.p_hi]
         gathered = None                       # in-flight all-gather of h_p
         defer = getattr(impl, "defer_grad", False)
-        for convs, layout in model_layers(model):
+        layers = model_layers(model)
+        n_layers = len(layers)
+        for li, (convs, layout) in enumerate(layers):
             shapes = {"user": h_u, "post": h_p}
             umsgs, pmsgs = layout.get("user", []), layout.get("post", [])
             for _, et, _ in umsgs + pmsgs:
@@ -515,7 +572,10 @@ class UserShard:
                     h_p = h_p_own
                 else:
                     gathered = Pending()
-                    h_p = _AllGather.apply(h_p_own, env, gathered)
+                    if li + 1 < n_layers:     # the slice is also the next layer's root input
+                        h_p, h_p_own = _AllGather.apply(h_p_own, env, gathered, True, defer)
+                    else:
+                        h_p = _AllGather.apply(h_p_own, env, gathered, False, defer)
             h_u = h_u_next
         self._post_pending = gathered or Pending()
         if wait:
