@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--dist", action="store_true",
                    help="take the sharded path (process group + collectives) even at world size 1: "
                         "runs the RCCL calls on a 1-GPU box")
+    p.add_argument("--autograd-sharded", action="store_true",
+                   help="sharded path through autograd (forward + loss + backward()) instead of "
+                        "UserShard.step's explicit collective schedule")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
@@ -198,8 +201,14 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=True)
-        loss = forward_loss()
-        loss.backward()
+        if sharded and not args.autograd_sharded:
+            # explicit schedule: each collective issued when its input is complete and waited
+            # for by its consumer only (parallel.UserShard.step; same kernels and gradients)
+            neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
+            loss = shard.step(model, x_user, x_post, neg, neg_order="user")
+        else:
+            loss = forward_loss()
+            loss.backward()
         if sharded:
             parallel.sync_grads(model, parallel.DistEnv.from_torch())
         opt.step()

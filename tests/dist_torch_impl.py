@@ -41,3 +41,50 @@ class TorchImpl:
         s_pos = (u * P[pos[1]]).sum(1)
         s_neg = (u * P[neg]).sum(1)
         return (cscale * F.softplus(-s_pos).sum() + F.softplus(s_neg).sum()) / n_total
+
+    # raw forms for UserShard.step's explicit schedule
+    gather_mean_raw = mean_gather
+
+    @staticmethod
+    def weighted_gather_raw(x, rel, w_fwd):
+        ei, _, n_dst = rel
+        return torch.zeros(n_dst, x.shape[1], dtype=x.dtype).index_add(0, ei[1],
+                                                                        x[ei[0]] * w_fwd[:, None])
+
+    @staticmethod
+    def scatter_mean_bwd_raw(g, rel, out=None):
+        ei, n_src, n_dst = rel
+        deg = torch.bincount(ei[1], minlength=n_dst).clamp(min=1).to(g.dtype)
+        if out is None:
+            out = torch.zeros(n_src, g.shape[1], dtype=g.dtype)
+        return out.index_add_(0, ei[0], g[ei[1]] / deg[ei[1]][:, None])
+
+    @staticmethod
+    def weighted_scatter_bwd_raw(g, rel, w_bwd, out=None):
+        ei, n_src, _ = rel
+        if out is None:
+            out = torch.zeros(n_src, g.shape[1], dtype=g.dtype)
+        return out.index_add_(0, ei[0], g[ei[1]] * w_bwd[:, None])
+
+    linear_fwd_raw = fused_linear
+
+    @staticmethod
+    def linear_bwd_raw(segs, w, dout, out_act, dxs, need_w, need_b):
+        dz = dout * (out_act > 0) if out_act is not None else dout
+        x = torch.cat(segs, 1)
+        dx = dz @ w
+        o = 0
+        for s, t in zip(segs, dxs):
+            if t is not None:
+                t.copy_(dx[:, o:o + s.shape[1]])
+            o += s.shape[1]
+        return (dz.T @ x if need_w else None), (dz.sum(0) if need_b else None)
+
+    def edge_bce_loss_raw(self, U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None):
+        if ready is not None:
+            ready()
+        U2, P2 = U.detach().requires_grad_(), P.detach().requires_grad_()
+        with torch.enable_grad():
+            loss = self.edge_bce_loss(U2, P2, pos, neg, n_total, cscale)
+            dU, dP = torch.autograd.grad(loss, (U2, P2))
+        return loss.detach(), dU, dP

@@ -46,6 +46,14 @@ def _worker(rank, world, port, q, kind="engage2"):
         sync_grads(model, env)
         total = env.all_reduce_(loss.detach().clone())
         grads = {n: p.grad.clone() for n, p in model.named_parameters()}
+        # the explicit schedule (UserShard.step) on the same shard: same loss and gradients
+        for p in model.parameters():
+            p.grad = None
+        step_loss = shard.step(model, g.x_dict["user"][lo:hi], g.x_dict["post"],
+                               shard.local_edges_of(neg))
+        sync_grads(model, env)
+        step_total = env.all_reduce_(step_loss.clone())
+        step_grads = {n: p.grad.clone() for n, p in model.named_parameters()}
         # reference on the whole graph, one process
         out, ref_loss, ref_grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
         res = {"rank": rank,
@@ -54,6 +62,10 @@ def _worker(rank, world, port, q, kind="engage2"):
                "post_err": float((h_p.detach()[:cfg.num_posts] - out["post"]).abs().max()),
                "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
                                max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
+               "step_loss_err": abs(float(step_total) - float(ref_loss)) / abs(float(ref_loss)),
+               "step_grad_err": max(float((step_grads[n] - ref_grads[n]).abs().max()) /
+                                    max(float(ref_grads[n].abs().max()), 1e-12)
+                                    for n in step_grads),
                "n_local": int(shard.pos_local.shape[1]), "n_total": int(pos.shape[1]),
                "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
         q.put(res)
@@ -86,6 +98,7 @@ def test_user_sharded_step_matches_single_process_oracle(world, kind):
         assert r["loss_err"] < 1e-5, r
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
         assert r["grad_err"] < 1e-4, r
+        assert r["step_loss_err"] < 1e-5 and r["step_grad_err"] < 1e-4, r
 
 
 def test_user_range_partitions_exactly():

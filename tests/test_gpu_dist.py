@@ -108,16 +108,28 @@ def _case_worker(rank, world, port, q, kind):
         parallel.sync_grads(model, env)
         total = env.all_reduce_(loss.detach().clone())
         torch.cuda.synchronize()
+        grads = {n: p.grad.cpu() for n, p in model.named_parameters()}
+        # the explicit schedule on the same shard and kernels
+        for p in model.parameters():
+            p.grad = None
+        step_loss = shard.step(model, xu, g.x_dict["post"].to(dev),
+                               shard.local_edges_of(neg.to(dev)))
+        parallel.sync_grads(model, env)
+        step_total = env.all_reduce_(step_loss.clone())
+        torch.cuda.synchronize()
         out, ref_loss, ref_grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
         res = {"rank": rank,
+               "step_loss_err": abs(float(step_total) - float(ref_loss)) / abs(float(ref_loss)),
+               "step_grad_err": max(float((p.grad.cpu() - ref_grads[n]).abs().max()) /
+                                    max(float(ref_grads[n].abs().max()), 1e-12)
+                                    for n, p in model.named_parameters()),
                "loss_err": abs(float(total) - float(ref_loss)) / abs(float(ref_loss)),
                "user_err": float((h_u.detach().cpu() - out["user"][shard.lo:shard.hi]).abs().max()
                                  / out["user"].abs().max()),
                "post_err": float((h_p.detach().cpu()[:cfg.num_posts] - out["post"]).abs().max()
                                  / out["post"].abs().max()),
-               "grad_err": max(float((p.grad.cpu() - ref_grads[n]).abs().max()) /
-                               max(float(ref_grads[n].abs().max()), 1e-12)
-                               for n, p in model.named_parameters()),
+               "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
+                               max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
                "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
         q.put(res)
     except Exception as e:   # surface worker failures in the parent
@@ -149,3 +161,4 @@ def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind):
         assert r["loss_err"] < 1e-4, r
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
         assert r["grad_err"] < 1e-4, r
+        assert r["step_loss_err"] < 1e-4 and r["step_grad_err"] < 1e-4, r

@@ -460,8 +460,15 @@ def test_user_shard_world1_matches_fused_model_and_oracle():
     loss = shard.loss(h_u, h_p, torch.from_numpy(z["neg_p"]).to(DEV))
     assert abs(float(loss.detach()) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
     loss.backward()
+    grads = {name: p.grad.clone() for name, p in model.named_parameters()}
     for name, p in model.named_parameters():
         close(p.grad, z["grad:" + name])
+        p.grad = None
+    # the explicit schedule (UserShard.step): same kernels, same loss and gradients
+    step_loss = shard.step(model, x["user"], x["post"], torch.from_numpy(z["neg_p"]).to(DEV))
+    assert torch.equal(step_loss, loss.detach())
+    for name, p in model.named_parameters():
+        torch.testing.assert_close(p.grad, grads[name], rtol=1e-6, atol=1e-7)
 
 
 def test_device_generated_graph_schema():

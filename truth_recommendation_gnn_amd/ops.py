@@ -396,75 +396,82 @@ def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tens
     return neg_p.to(torch.int64)[csr.bwd.perm.long()].contiguous()
 
 
+def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
+              ready=None):
+    """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP)."""
+    U = _check_f32(U, "edge_bce_loss user_emb")
+    P = _check_f32(P, "edge_bce_loss post_emb")
+    dev = N.require_device(U, P, neg_u_order)
+    lib, s = N.lib(), N.stream_ptr(dev)
+    nu, np_, d, E = U.shape[0], P.shape[0], int(U.shape[1]), csr.num_edges
+    if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
+        raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
+    ub, pf = csr.bwd, csr.fwd
+    dU = torch.empty_like(U)
+    part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
+    loss = torch.empty((), dtype=torch.float32, device=dev)
+    err = torch.zeros(2, dtype=torch.int32, device=dev)
+    c = cscale.to(torch.float32).reshape(()).contiguous()
+    inv_e = 1.0 / n_total if n_total > 0 else 0.0
+    uop = _user_of_pos(csr)
+    neg32 = neg_u_order.dtype == torch.int32          # sample_negatives' draws
+    neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
+    rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
+    nu_s = torch.empty(E, dtype=torch.int32, device=dev)
+    dP = torch.empty_like(P)
+    # dP chain (side stream under HGNN_STREAMS=1): sort the negatives (post, user) by post,
+    # then the two dP gathers, each edge's weight recomputed from <U[u], P[post]>
+    # (hgnn_score_gather); pass A (loss + dU) needs none of it.
+    lanes = _Lanes(dev, 2)
+    with torch.cuda.stream(lanes.stream(1)):
+        ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
+        if neg32:
+            # int32 keys: no validation pass (the scoring pass below counts out-of-range
+            # negatives; the sort only misplaces such a key, never dereferences it)
+            with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
+                N.check(lib.hgnn_sort_pairs_i32(
+                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                    None, None, N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                    "hgnn_sort_pairs_i32")
+        else:
+            with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
+                N.check(lib.hgnn_sort_pairs_i64(
+                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                    None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                    "hgnn_sort_pairs_i64")
+    if ready is not None:
+        # P is still arriving (parallel.py's all-gather of the post table): the sort above
+        # needs only the edges, so it ran ahead; every kernel below reads P
+        ready()
+        if lanes.side is not None:
+            lanes.side.wait_stream(lanes.main)
+    with torch.cuda.stream(lanes.stream(1)):
+        _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
+        from .graph import GroupedEdges, Plan
+        negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
+        _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
+    with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
+        if neg32:
+            N.check(lib.hgnn_edge_score_fwd_i32(
+                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                N.ptr(neg), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
+                N.ptr(err), s), "hgnn_edge_score_fwd_i32")
+        else:
+            N.check(lib.hgnn_edge_score_fwd(
+                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
+                N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
+    lanes.join()
+    if check and int(err[0]):
+        raise ValueError("edge_bce_loss: negative post id out of range")
+    return loss, dU, dP
+
+
 class _EdgeBCELoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
                 ready=None):
-        U = _check_f32(U, "edge_bce_loss user_emb")
-        P = _check_f32(P, "edge_bce_loss post_emb")
-        dev = N.require_device(U, P, neg_u_order)
-        lib, s = N.lib(), N.stream_ptr(dev)
-        nu, np_, d, E = U.shape[0], P.shape[0], int(U.shape[1]), csr.num_edges
-        if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
-            raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
-        ub, pf = csr.bwd, csr.fwd
-        dU = torch.empty_like(U)
-        part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
-        loss = torch.empty((), dtype=torch.float32, device=dev)
-        err = torch.zeros(2, dtype=torch.int32, device=dev)
-        c = cscale.to(torch.float32).reshape(()).contiguous()
-        inv_e = 1.0 / n_total if n_total > 0 else 0.0
-        uop = _user_of_pos(csr)
-        neg32 = neg_u_order.dtype == torch.int32          # sample_negatives' draws
-        neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
-        rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
-        nu_s = torch.empty(E, dtype=torch.int32, device=dev)
-        dP = torch.empty_like(P)
-        # dP chain (side stream under HGNN_STREAMS=1): sort the negatives (post, user) by post,
-        # then the two dP gathers, each edge's weight recomputed from <U[u], P[post]>
-        # (hgnn_score_gather); pass A (loss + dU) needs none of it.
-        lanes = _Lanes(dev, 2)
-        with torch.cuda.stream(lanes.stream(1)):
-            ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-            if neg32:
-                # int32 keys: no validation pass (the scoring pass below counts out-of-range
-                # negatives; the sort only misplaces such a key, never dereferences it)
-                with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
-                    N.check(lib.hgnn_sort_pairs_i32(
-                        N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
-                        None, None, N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                        "hgnn_sort_pairs_i32")
-            else:
-                with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
-                    N.check(lib.hgnn_sort_pairs_i64(
-                        N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
-                        None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                        "hgnn_sort_pairs_i64")
-        if ready is not None:
-            # P is still arriving (parallel.py's all-gather of the post table): the sort above
-            # needs only the edges, so it ran ahead; every kernel below reads P
-            ready()
-            if lanes.side is not None:
-                lanes.side.wait_stream(lanes.main)
-        with torch.cuda.stream(lanes.stream(1)):
-            _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
-            from .graph import GroupedEdges, Plan
-            negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
-            _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
-        with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
-            if neg32:
-                N.check(lib.hgnn_edge_score_fwd_i32(
-                    N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                    N.ptr(neg), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
-                    N.ptr(err), s), "hgnn_edge_score_fwd_i32")
-            else:
-                N.check(lib.hgnn_edge_score_fwd(
-                    N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
-                    N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
-                    N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
-        lanes.join()
-        if check and int(err[0]):
-            raise ValueError("edge_bce_loss: negative post id out of range")
+        loss, dU, dP = _edge_bce(U, P, csr, neg_u_order, cscale, check, n_total, ready)
         ctx.save_for_backward(dU, dP)
         return loss
 
@@ -501,6 +508,16 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
         cscale = pos_weights.to(torch.float32).mean()
     n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
     return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total, ready)
+
+
+def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
+                      neg_p: torch.Tensor, n_edges_total: int, cscale: torch.Tensor,
+                      neg_order: str = "user", ready=None):
+    """:func:`edge_bce_loss` outside autograd: (loss, dL/dU, dL/dP) from the same kernels, for
+    callers that run their own backward schedule (``parallel.UserShard.step``)."""
+    csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
+    neg_u = negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
+    return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready)
 
 
 def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:
@@ -570,6 +587,25 @@ def await_pending(t: torch.Tensor) -> torch.Tensor:
         with torch.no_grad():
             entry[1].wait()   # NCCL: the current stream waits on the collective (no host sync)
     return t
+
+
+def weighted_gather_raw(x_src: torch.Tensor, csr: RelationCSR, w_fwd: torch.Tensor) -> torch.Tensor:
+    """``out[i] = sum_{p in row i} w_fwd[p] x_src[col[p]]`` (K1 with per-edge weights)."""
+    x_src = _check_f32(x_src, "weighted_gather")
+    out = torch.empty(csr.n_dst, x_src.shape[1], dtype=torch.float32, device=x_src.device)
+    _gather(x_src, csr.fwd, None, csr_mean=False, out=out, accumulate=False, edge_w=w_fwd,
+            kind="wfwd")
+    return out
+
+
+def weighted_scatter_bwd_raw(g: torch.Tensor, csr: RelationCSR, w_bwd: torch.Tensor,
+                             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Transpose of :func:`weighted_gather_raw` over the CSC (K2), accumulating into ``out``."""
+    acc = out is not None
+    if out is None:
+        out = torch.empty(csr.n_src, g.shape[1], dtype=torch.float32, device=g.device)
+    _gather(g.contiguous(), csr.bwd, None, csr_mean=False, out=out, accumulate=acc, edge_w=w_bwd)
+    return out
 
 
 class _GatherWeighted(torch.autograd.Function):

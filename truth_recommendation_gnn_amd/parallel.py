@@ -336,6 +336,41 @@ class HipImpl:
         return ops.edge_bce_loss(U, P, pos, neg, None, neg_order=neg_order, check=False,
                                  n_edges_total=n_total, cscale=cscale, ready=ready)
 
+    # raw kernels (no autograd) for UserShard.step's explicit schedule
+    gather_mean_raw = staticmethod(ops.gather_mean)
+    weighted_gather_raw = staticmethod(ops.weighted_gather_raw)
+    weighted_scatter_bwd_raw = staticmethod(ops.weighted_scatter_bwd_raw)
+    linear_fwd_raw = staticmethod(ops.linear_fwd)
+    linear_bwd_raw = staticmethod(ops.linear_bwd)
+    edge_bce_loss_raw = staticmethod(ops.edge_bce_loss_raw)
+
+    @staticmethod
+    def scatter_mean_bwd_raw(g, rel, out=None):
+        return ops.scatter_mean_bwd(g, rel, out=out)
+
+
+def _grads_to_params(convs, msgs, dW: torch.Tensor, db: Optional[torch.Tensor]) -> None:
+    """Adjoint of ``nn._fused_weights``: W = [w_1 W_l,1 | ... | w_R W_l,R | sum_r w_r W_r,r],
+    b = sum_r w_r b_r.  Accumulates into each parameter's ``.grad``."""
+    def acc(p, g):                              # g is always a fresh tensor
+        if p.grad is None:
+            p.grad = g
+        else:
+            p.grad.add_(g)
+    off = 0
+    for name, _, wt in msgs:
+        conv = convs[name]
+        k = conv.lin_l.weight.shape[1]
+        acc(conv.lin_l.weight, (dW[:, off:off + k] * wt).contiguous())
+        if conv.lin_l.bias is not None and db is not None:
+            acc(conv.lin_l.bias, db * wt)
+        off += k
+    root = dW[:, off:]
+    for name, _, wt in msgs:
+        conv = convs[name]
+        if conv.lin_r is not None:
+            acc(conv.lin_r.weight, (root * wt).contiguous())
+
 
 def model_layers(model) -> List[Tuple[Dict[str, torch.nn.Module], Layout]]:
     """[(convs, layout)] per layer: ``HeteroSAGE`` (relation list, L layers) or a
@@ -582,6 +617,28 @@ class UserShard:
             self._post_pending.wait()
         return h_u, h_p
 
+    def step(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor,
+             neg_local: torch.Tensor, neg_order: str = "edge") -> torch.Tensor:
+        """One training step's forward, loss and backward for this rank, with an explicit
+        schedule instead of autograd's: the same kernels, and the parameter gradients
+        ``forward`` + ``loss`` + ``backward()`` give (accumulated into ``.grad``); returns the
+        rank's loss share (detached).  Autograd runs backward nodes newest first, so a
+        collective's consumer ran right after the collective was issued and the main stream
+        waited for it; here every collective is issued as soon as its input is complete and
+        waited for only by its consumer, with independent work in between:
+
+        * the post-table gradient's reduce-scatter runs under the user-side projection
+          backward;
+        * the post partial sums' slice-gradient all-gather runs under the K2s into the
+          previous layer's post table (and the halo's reverse all-to-all);
+        * the previous layer's reduce-scatter runs under the user rows' K2s and the next
+          projection backward.
+        """
+        if self.cscale is None:
+            raise ValueError("UserShard built without pos_weights")
+        with torch.no_grad():
+            return _step(self, model, x_user_own, x_post, neg_local, neg_order)
+
     def loss(self, h_u_own, h_p, neg_local, neg_order="edge"):
         """This rank's additive share of the reference loss."""
         if self.cscale is None:
@@ -591,6 +648,161 @@ class UserShard:
         return self.impl.edge_bce_loss(h_u_own, h_p, self.pos_local, neg_local,
                                        self.num_edges_global, self.cscale, neg_order=neg_order,
                                        ready=pend.wait)
+
+
+def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
+    """UserShard.step: forward, loss and backward with every collective issued as early as its
+    input exists and waited as late as its consumer allows (see the method docstring)."""
+    impl, env = shard.impl, shard.env
+    multi = env.world > 1
+    if x_post.shape[0] != shard.n_posts_pad:
+        x_post = torch.nn.functional.pad(x_post, (0, 0, 0, shard.n_posts_pad - x_post.shape[0]))
+    layers = model_layers(model)
+    for convs, _ in layers:
+        if any(c.lin_r is None for c in convs.values()):
+            raise NotImplementedError("UserShard.step expects SAGEConv(root_weight=True) layers")
+    h_u, h_p, h_p_own = x_user_own, x_post, x_post[shard.p_lo:shard.p_hi]
+    ag = None                                   # in-flight all-gather of h_p
+    saved = []
+    for convs, layout in layers:
+        um, pm = layout.get("user", []), layout.get("post", [])
+        for _, et, _ in um + pm:
+            if et not in shard.rels:
+                raise KeyError(f"relation {et} is not in the sharded graph")
+        shapes = {"user": h_u, "post": h_p}
+        Wu, bu = _fused_weights(convs, um, shapes) if um else (None, None)
+        Wp, bp = _fused_weights(convs, pm, shapes) if pm else (None, None)
+        # F1 halo rows out; F2 post partial sums -> reduce-scatter (both in flight from here)
+        halo, halo_w = None, _Done()
+        if multi and shard.halo is not None and any(et[0] == "user" for _, et, _ in um):
+            hl = shard.halo
+            halo, halo_w = env.all_to_all_async(impl.gather_mean_raw(h_u, hl.rel_send),
+                                                hl.send_splits, hl.recv_splits)
+        rs = {}
+        for _, et, _ in pm:
+            r = shard.rels[et]
+            if r.kind[0] == "user":
+                part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd)
+                rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
+        if ag is not None:                      # F3 the previous layer's post table
+            ag.wait()
+            ag = None
+        # F4 user side
+        a_u, x_ext = [], None
+        for _, et, _ in um:
+            r = shard.rels[et]
+            if r.kind[0] == "post":
+                a_u.append(impl.gather_mean_raw(h_p, r.csr))
+            else:
+                if x_ext is None:
+                    halo_w.wait()
+                    x_ext = h_u if halo is None else torch.cat([h_u, halo])
+                a_u.append(impl.gather_mean_raw(x_ext, r.csr))
+        y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True) if um else h_u
+        # F5 post side on the owned slice, then its all-gather
+        a_p = []
+        for _, et, _ in pm:
+            r = shard.rels[et]
+            if r.kind[0] == "post":
+                a_p.append(impl.gather_mean_raw(h_p, r.csr))
+            else:
+                a, w = rs[et]
+                w.wait()
+                a_p.append(a)
+        if pm:
+            y_p_own = impl.linear_fwd_raw(a_p + [h_p_own], Wp, bp, True)
+            y_p, ag = env.all_gather_async(y_p_own) if multi else (y_p_own, None)
+        else:
+            y_p_own, y_p = h_p_own, h_p
+        saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu, Wp,
+                      bu is not None, bp is not None))
+        h_u, h_p, h_p_own = y_u, y_p, y_p_own
+    # loss: the negatives sort runs while the last all-gather lands
+    loss, G_u, G_full = impl.edge_bce_loss_raw(h_u, h_p, shard.pos_local, neg_local,
+                                               shard.num_edges_global, shard.cscale, neg_order,
+                                               ag.wait if ag is not None else None)
+    G_own = None
+    R = None                                    # reduce-scatter of G_full, once issued
+    for li in reversed(range(len(layers))):
+        (convs, um, pm, hu, hp, hpo, x_ext, a_u, a_p, yu, ypo, Wu, Wp, has_bu, has_bp) = saved[li]
+        need_x = li > 0                         # layer 0's inputs are the (fixed) features
+        if pm and R is None:                    # B1 adjoint of the post-table all-gather
+            g = G_full if G_full is not None else torch.zeros_like(hp)
+            R = env.reduce_scatter_async(g) if multi else (g, _Done())
+        # B2a user-side projection backward
+        dxu = []
+        if um:
+            dxu = [torch.empty_like(a) if need_x else None for a in a_u]
+            dxu.append(torch.empty_like(hu) if need_x else None)
+            dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True, has_bu)
+            _grads_to_params(convs, um, dW, db)
+            d_hu = dxu[-1]
+        else:
+            d_hu = G_u if need_x else None
+        # B3 post-side projection backward (waits for the reduce-scatter)
+        dxp = []
+        d_hpo = G_own
+        if pm:
+            r_slice, r_w = R
+            r_w.wait()
+            R = None
+            g_slice = r_slice if G_own is None else r_slice + G_own
+            dxp = [torch.empty_like(a) if need_x else None for a in a_p]
+            dxp.append(torch.empty_like(hpo) if need_x else None)
+            dW, db = impl.linear_bwd_raw(a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, True,
+                                         has_bp)
+            _grads_to_params(convs, pm, dW, db)
+            d_hpo = dxp[-1]
+        if not need_x:
+            break
+        # B4 slice gradients of the post partial sums: all-gather (in flight over B2b)
+        gath = {}
+        for j, (_, et, _) in enumerate(pm):
+            if shard.rels[et].kind[0] == "user":
+                gath[et] = env.all_gather_async(dxp[j]) if multi else (dxp[j], _Done())
+        # B2b gradients into the previous layer's post table and the halo (a layer without a
+        # post side passes the table through: its gradient flows on unchanged)
+        G_prev = None if pm else G_full
+        d_xext = None
+        for j, (_, et, _) in enumerate(um):
+            r = shard.rels[et]
+            if r.kind[0] == "post":
+                if G_prev is None:
+                    G_prev = torch.zeros_like(hp)
+                impl.scatter_mean_bwd_raw(dxu[j], r.csr, out=G_prev)
+            else:
+                if d_xext is None:
+                    d_xext = torch.zeros_like(x_ext)
+                impl.scatter_mean_bwd_raw(dxu[j], r.csr, out=d_xext)
+        for j, (_, et, _) in enumerate(pm):
+            r = shard.rels[et]
+            if r.kind[0] == "post":
+                if G_prev is None:
+                    G_prev = torch.zeros_like(hp)
+                impl.scatter_mean_bwd_raw(dxp[j], r.csr, out=G_prev)
+        back, back_w = None, _Done()
+        if d_xext is not None:
+            n_own = hu.shape[0]
+            d_hu.add_(d_xext[:n_own])
+            if x_ext.shape[0] > n_own:
+                hl = shard.halo
+                back, back_w = env.all_to_all_async(d_xext[n_own:].contiguous(), hl.recv_splits,
+                                                    hl.send_splits)
+        # the previous layer's post-table gradient is complete: its reduce-scatter starts now
+        prev_pm = saved[li - 1][2]
+        if prev_pm:
+            g = G_prev if G_prev is not None else torch.zeros_like(hp)
+            R = env.reduce_scatter_async(g) if multi else (g, _Done())
+        # B5 user rows' share of the post partial sums, then the halo rows' gradients
+        for et, (full, w) in gath.items():
+            w.wait()
+            r = shard.rels[et]
+            impl.weighted_scatter_bwd_raw(full, r.csr, r.w_bwd, out=d_hu)
+        if back is not None:
+            back_w.wait()
+            impl.scatter_mean_bwd_raw(back, shard.halo.rel_send, out=d_hu)
+        G_u, G_full, G_own = d_hu, G_prev, d_hpo
+    return loss
 
 
 def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
