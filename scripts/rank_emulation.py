@@ -53,7 +53,14 @@ def main():
         step()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
-    print(json.dumps({"world": args.world, "posts": cfg.num_posts, "ms_per_step_compute": round(ms, 3)}))
+    timer = ops.KernelTimer()                 # one more pass for the per-kernel split
+    ops.set_timer(timer)
+    for _ in range(args.steps):
+        step()
+    ops.set_timer(None)
+    kern = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(timer.summary().items())}
+    print(json.dumps({"world": args.world, "posts": cfg.num_posts,
+                      "ms_per_step_compute": round(ms, 3), "kernels_ms_per_step": kern}))
 
 
 if __name__ == "__main__":
