@@ -13,7 +13,9 @@ users, N·100k posts, N·20M engages), destination-partitioned (parallel.py): ea
 cfg2-sized user range and a 1/N row slice of the post table.  Per layer one RCCL reduce-scatter
 of the post partial sums and one all-gather of the projected slices (their adjoints in the
 backward), a halo all-to-all for user->user relations when the config has them (cfg5), weight
-gradients all-reduced once per step.
+gradients all-reduced once per step.  The step is ``UserShard.step``: the same kernels as the
+autograd path, with every collective issued as soon as its input is complete and awaited only
+by its consumer (``--autograd-sharded`` runs forward + loss + backward() instead).
 value = all ranks' edges / max-over-ranks time.
 
 Prints ONE JSON line (rank 0) with ``roofline`` for the dominant kernel (the K1 forward gather:
