@@ -20,7 +20,13 @@ class TorchImpl:
     @staticmethod
     def mean_gather(x, rel):
         ei, _, n_dst = rel
-        return sage_ref.mean_aggregate(x, ei, n_dst)
+        out = sage_ref.mean_aggregate(x, ei, n_dst)
+        if ei.shape[1] == 0:
+            # connected to x, as the HIP op is (its backward returns a zero gradient): every
+            # rank's autograd graph then has the same shape, so the collective adjoints run in
+            # the same order everywhere
+            out = out + x.sum() * 0.0
+        return out
 
     @staticmethod
     def weighted_gather(x, rel, w_fwd, w_bwd):

@@ -139,11 +139,15 @@ def _case_worker(rank, world, port, q, kind):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "rgcn"), (3, "rel4")])
+@pytest.mark.parametrize("world,kind", [(2, "rgcn"), (3, "rel4"), (3, "tiny_rgcn"),
+                                        (3, "tiny4")])
 def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind):
     """The reference WeightedRGCN (social relation through the halo all-to-all) and the
     4-relation cfg5 graph on the HIP kernels, world 2/3 on one device (gloo over device
-    tensors, the exchange via host memory), against the CPU oracle of the whole graph."""
+    tensors, the exchange via host memory), against the CPU oracle of the whole graph.  The
+    tiny cases give a rank no engages edge, no social in-edge, no halo row and an empty
+    post->post slice: E=0 launches on that rank, which must still take part in every
+    collective (its weight gradients enter the all-reduce as zeros)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -157,7 +161,8 @@ def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind):
     errs = [r["error"] for r in res if "error" in r]
     assert not errs, errs
     for r in res:
-        assert r["n_halo"] > 0, r
+        if not kind.startswith("tiny"):
+            assert r["n_halo"] > 0, r
         assert r["loss_err"] < 1e-4, r
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
         assert r["grad_err"] < 1e-4, r

@@ -558,9 +558,13 @@ class _GatherMean(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
-            return None, None
         await_pending(g)     # the halo exchange's adjoint may still be in flight (parallel.py)
+        if not ctx.needs_input_grad[0]:
+            return None, None
+        if ctx.csr.num_edges == 0:
+            # a zero gradient, not None: a rank holding no edge of this relation still has to
+            # reach the collective adjoints upstream (parallel.py's halo exchange)
+            return g.new_zeros(ctx.csr.n_src, g.shape[1]), None
         return scatter_mean_bwd(g.contiguous(), ctx.csr), None
 
 
@@ -620,10 +624,12 @@ class _GatherWeighted(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if not ctx.needs_input_grad[0] or ctx.csr.num_edges == 0:
+        await_pending(g)
+        if not ctx.needs_input_grad[0]:
             return None, None, None, None
         csr = ctx.csr
-        await_pending(g)
+        if csr.num_edges == 0:   # zero, not None: see _GatherMean.backward
+            return g.new_zeros(csr.n_src, g.shape[1]), None, None, None
         out = torch.empty(csr.n_src, g.shape[1], dtype=torch.float32, device=g.device)
         _gather(g.contiguous(), csr.bwd, None, csr_mean=False, out=out, accumulate=False,
                 edge_w=ctx.w_bwd)

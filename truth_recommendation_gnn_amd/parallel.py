@@ -784,7 +784,9 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
         if d_xext is not None:
             n_own = hu.shape[0]
             d_hu.add_(d_xext[:n_own])
-            if x_ext.shape[0] > n_own:
+            # every rank joins the reverse exchange, also one without halo rows of its own (its
+            # rows may still be in other ranks' halos)
+            if multi and shard.halo is not None:
                 hl = shard.halo
                 back, back_w = env.all_to_all_async(d_xext[n_own:].contiguous(), hl.recv_splits,
                                                     hl.send_splits)
@@ -806,14 +808,21 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
 
 
 def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
-    """Sum parameter gradients over ranks with one flat all-reduce."""
+    """Sum parameter gradients over ranks with one flat all-reduce.  Every rank contributes every
+    trainable parameter (zeros where its backward produced no gradient — a rank whose shard holds
+    no edge of some relation), so the flat buffers line up across ranks."""
     if env.world == 1:
         return
-    params = [p for p in model.parameters() if p.grad is not None]
-    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    params = [p for p in model.parameters() if p.requires_grad]
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                      for p in params])
     env.all_reduce_(flat)
     o = 0
     for p in params:
         n = p.numel()
-        p.grad.copy_(flat[o:o + n].view_as(p))
+        g = flat[o:o + n].view_as(p)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
         o += n
