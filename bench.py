@@ -40,6 +40,7 @@ from truth_recommendation_gnn_amd import HeteroSAGE, ops, synth  # noqa: E402
 from truth_recommendation_gnn_amd import parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
+FP32_MFMA_PEAK_TFS = 157.3  # same table: dense fp32 matrix (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
 # every relation a config may hold, with the reference's weights (train_gnn.py:163-164:
 # w_direct 1.0, w_social 0.75); cfg5's post-post relation takes 1.0
 ALL_RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
@@ -253,12 +254,13 @@ def main():
             per_launch_bytes = r["bytes"] / r["launches"]
             ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
             traffic, tsrc = None, None
+            weighted = name.startswith("gather_wfwd")
             pmc = os.path.join(ROOT, "profiles", "pmc_gather_r1.json")
-            if os.path.exists(pmc) and world == 1 and cfg.name == "cfg2":
+            # the PMC passes measured the unweighted K1 launch of the cfg2 single-GPU step
+            if os.path.exists(pmc) and world == 1 and cfg.name == "cfg2" and not weighted:
                 with open(pmc) as f:
                     pm = json.load(f)
                 traffic, tsrc = pm.get("hbm_bytes_per_launch"), "profiles/pmc_gather_r1.json"
-            weighted = name.startswith("gather_wfwd")
             roof = {"bound": "hbm",
                     "kernel": (f"k_gather K1 weighted fwd (post partial sums) {name}" if weighted
                                else f"k_gather K1 mean fwd {name}"),
@@ -268,6 +270,30 @@ def main():
                     "algorithmic_bytes_per_launch": int(per_launch_bytes),
                     "bytes_formula": ("4*E*(2+d) + 4*(N_dst+1) + 4*N_dst*d" if weighted
                                       else "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d")}
+        # The dense projection (K3) against the fp32 MFMA peak: the largest forward launch (the
+        # user side), HIP-event timed like the gather; the PMC MFMA-busy fraction of the same
+        # kernel comes from profiles/pmc_k3_r1.json (scripts/pmc_k3.sh) for cfg2.
+        proj = None
+        lin = {k: v for k, v in kern.items() if k.startswith("linear_fwd[") and v["flops"]}
+        if lin:
+            name = max(lin, key=lambda k: lin[k]["flops"] / lin[k]["launches"])
+            r = lin[name]
+            tfs = r["flops"] / (r["ms"] * 1e-3) / 1e12
+            busy, bsrc = None, None
+            pk = os.path.join(ROOT, "profiles", "pmc_k3_r1.json")
+            if os.path.exists(pk) and cfg.name == "cfg2" and cfg.hidden == 64:
+                with open(pk) as f:
+                    busy = json.load(f)["kernels"].get("hgnn::k_linear_fwd_v4<64, 128>", {}).get(
+                        "mfma_util")
+                bsrc = "profiles/pmc_k3_r1.json"
+            proj = {"bound": "mfma", "kernel": f"k_linear_fwd_v4 K3 {name}",
+                    "achieved": round(tfs, 1), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
+                    "hbm_GB/s": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1),
+                    "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 1),
+                    "flops_per_launch": int(r["flops"] / r["launches"]),
+                    "flops_formula": "2*N*K*H (K = sum of the input segments)",
+                    "mfma_busy_pmc": busy, "mfma_busy_source": bsrc}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, args.cpu_threads)
@@ -286,11 +312,13 @@ def main():
                        "parallelism": (f"user-shard x{world} (post-table slices: RCCL "
                                        "reduce-scatter / all-gather per layer)"
                                        if sharded else "single")},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "projection": proj, "cpu_baseline": cpu,
             "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
                             "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
                             "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
-                                                if v["ms"] else None)}
+                                                if v["ms"] else None),
+                            **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
+                               if v["flops"] and v["ms"] else {})}
                         for k, v in sorted(kern.items())},
             "loss": float(loss.detach()),
         }

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 400 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -8 gpurun_out/gpu_tests.log
   ok $rc || exit $rc
   timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1

@@ -37,18 +37,21 @@ class KernelTimer:
     bench.py inside its timed region; ``None`` when off (zero overhead)."""
 
     def __init__(self):
-        self.records = []   # (name, algorithmic bytes, start event, end event, compulsory bytes)
+        # (name, algorithmic bytes, start event, end event, compulsory bytes, flops)
+        self.records = []
 
     def summary(self):
         torch.cuda.synchronize()
         agg = {}
-        for name, nbytes, s, e, cbytes in self.records:
+        for name, nbytes, s, e, cbytes, flops in self.records:
             ms = s.elapsed_time(e)
-            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0, "cbytes": 0})
+            a = agg.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0, "cbytes": 0,
+                                      "flops": 0})
             a["launches"] += 1
             a["ms"] += ms
             a["bytes"] += nbytes
             a["cbytes"] += cbytes
+            a["flops"] += flops
         return agg
 
 
@@ -62,10 +65,11 @@ def set_timer(t: Optional[KernelTimer]) -> None:
 
 class _timed:
     """``cbytes``: compulsory bytes (every table row counted once), when it differs from the
-    algorithmic figure — the honest number for a gather whose source table is cache-resident."""
+    algorithmic figure — the honest number for a gather whose source table is cache-resident.
+    ``flops``: algorithmic flops of an MFMA kernel (K3), 0 elsewhere."""
 
-    def __init__(self, name, nbytes, cbytes=None):
-        self.name, self.nbytes = name, nbytes
+    def __init__(self, name, nbytes, cbytes=None, flops=0):
+        self.name, self.nbytes, self.flops = name, nbytes, flops
         self.cbytes = nbytes if cbytes is None else cbytes
 
     def __enter__(self):
@@ -78,7 +82,8 @@ class _timed:
         if _timer is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            _timer.records.append((self.name, int(self.nbytes), self.s, e, int(self.cbytes)))
+            _timer.records.append((self.name, int(self.nbytes), self.s, e, int(self.cbytes),
+                                   int(self.flops)))
 
 
 def gather_bytes(n_edges: int, n_rows: int, d: int, weighted: bool) -> int:
@@ -171,7 +176,8 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
         raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(ks)}")
     dev = w.device
     out = torch.empty(n, h, dtype=torch.float32, device=dev)
-    with _timed(f"linear_fwd_h{h}", 4 * n * (sum(ks) + h)):
+    k = sum(ks)
+    with _timed(f"linear_fwd[{n}x{k}->{h}]", 4 * n * (k + h), flops=2 * n * k * h):
         N.check(N.lib().hgnn_linear_fwd(len(segs), N.ptr_array(segs), N.int_array(ks), n,
                                         N.ptr(w), h, N.ptr(b), 1 if relu else 0, N.ptr(out),
                                         N.stream_ptr(dev)), "hgnn_linear_fwd")
@@ -189,8 +195,10 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     ws = None
     if need_w or need_b:
         ws = N.workspace(N.lib().hgnn_linear_bwd_ws_bytes(n, sum(ks), h), dev)
-    nb = 4 * n * (2 * h + sum(ks) + sum(k for k, dx in zip(ks, dxs) if dx is not None))
-    with _timed(f"linear_bwd_h{h}", nb):
+    k_dx = sum(k for k, dx in zip(ks, dxs) if dx is not None)
+    nb = 4 * n * (2 * h + sum(ks) + k_dx)
+    fl = 2 * n * h * k_dx + (2 * n * sum(ks) * h if need_w else 0)   # dgrad + wgrad
+    with _timed(f"linear_bwd[{n}x{sum(ks)}->{h}]", nb, flops=fl):
         N.check(N.lib().hgnn_linear_bwd(
             len(segs), N.ptr_array(segs), N.int_array(ks), n, N.ptr(w), h, N.ptr(dout),
             N.ptr(out_act), N.ptr_array(dxs), N.ptr(dw), N.ptr(db), N.ptr(ws),
@@ -406,6 +414,14 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     nu, np_, d, E = U.shape[0], P.shape[0], int(U.shape[1]), csr.num_edges
     if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
         raise ValueError("edge_bce_loss: embedding shapes do not match the positive edges")
+    if E == 0:
+        # a shard without positive edges (parallel.py): its share of the loss and gradients is
+        # zero, and no kernel would read a negative (the C ABI rejects the empty tensor's null
+        # pointer whenever the global edge count is non-zero)
+        if ready is not None:
+            ready()
+        return (torch.zeros((), dtype=torch.float32, device=dev), torch.zeros_like(U),
+                torch.zeros_like(P))
     ub, pf = csr.bwd, csr.fwd
     dU = torch.empty_like(U)
     part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
