@@ -141,6 +141,19 @@ int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t 
                       int32_t chunk, float* slab, float* out, int32_t accumulate,
                       hgnn_stream_t stream);
 
+/* Both dP gathers of the fused loss in one pass (replaces a mode-1 hgnn_score_gather over the
+ * positives followed by an accumulating mode-2 one over the negatives):
+ *   out[r,:] = sum_{p in rowptr/col row r} w_1(s) x[col[p],:]  +  sum_{p in rowptr_n/col_n row r}
+ *              w_2(s) x[col_n[p],:]
+ * with w_1, w_2 as hgnn_score_gather's modes 1 and 2.  The heavy-row plan applies to the positive
+ * list only (the uniform negatives have no heavy rows); every row is written (no accumulate). */
+int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t d,
+                       const int32_t* rowptr, const int32_t* col, const int32_t* rowptr_n,
+                       const int32_t* col_n, int64_t n_rows, const float* cscale, float inv_e,
+                       const int32_t* heavy_rows, const int32_t* heavy_first, int64_t n_heavy,
+                       int64_t n_chunks, int32_t chunk, float* slab, float* out,
+                       hgnn_stream_t stream);
+
 /* ---- edge scoring + weighted BCE (train_gnn.py:259-281), fused with its gradient --------------
  * Positive edges grouped by user (rowptr_u/col_u = post ids); neg_u_order[k] = the negative post
  * drawn for position k; to_post_pos[k] = that edge's position in the post-grouped CSR.

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the sharded N-GPU bench step (``UserShard.step``), on one GPU.
+
+Rank 0 of the weak-scaled graph (``synth.replicated(cfg, N)``: N x the users, posts and edges)
+runs the real sharded code path — its user range, the post-table slice, the explicit collective
+schedule — with every collective replaced by a local stand-in of the same shape (reduce-scatter:
+this rank's slice of its own partial sums; all-gather: the own slice tiled N times; all-reduce:
+identity).  So it times what one rank computes at N GPUs, collectives excluded (RCCL needs one GPU
+per rank); the numbers are wrong (local degrees, tiled tables), the work is not.
+python scripts/shard_emulation.py --world 8 [--steps 20]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from truth_recommendation_gnn_amd import HeteroSAGE, ops, parallel, synth  # noqa: E402
+
+RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+
+
+class EmulEnv(parallel.DistEnv):
+    """``world`` ranks seen from ``rank``, every collective a local stand-in (timing only)."""
+
+    def use_side_adjoint(self, t):
+        return False
+
+    def all_reduce_(self, t):
+        return t
+
+    def reduce_scatter_async(self, full):
+        S = full.shape[0] // self.world
+        return full[self.rank * S:(self.rank + 1) * S].clone(), parallel._Done()
+
+    def all_gather_async(self, own):
+        return own.repeat(self.world, *([1] * (own.dim() - 1))), parallel._Done()
+
+    def all_to_all_async(self, inp, send_splits, recv_splits):
+        return inp.new_zeros((int(sum(recv_splits)),) + tuple(inp.shape[1:])), parallel._Done()
+
+    def all_reduce_async(self, t):
+        return parallel._Done()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda")
+    gcfg = synth.replicated(args.config, args.world)
+    g = synth.make_graph(gcfg, device=dev, device_gen=True)
+    pos_g = g.edge_index_dict[synth.ENGAGES]
+    pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
+    env = EmulEnv(world=args.world, rank=0)
+    shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in RELATIONS},
+                               gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g)
+    x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
+    x_post = g.x_dict["post"]
+    edges_local = sum(int(r.csr.num_edges) for r in shard.rels.values()) * gcfg.layers
+    del g, pos_g, pw_g
+    torch.cuda.empty_cache()
+    model = HeteroSAGE(gcfg.hidden, RELATIONS, num_layers=gcfg.layers).to(dev)
+    with torch.no_grad():
+        shard.forward(model, x_user, x_post)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    gen = torch.Generator(device=dev).manual_seed(3)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
+        shard.step(model, x_user, x_post, neg, neg_order="user")
+        opt.step()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    timer = ops.KernelTimer()                 # one more pass for the per-kernel split
+    ops.set_timer(timer)
+    for _ in range(args.steps):
+        step()
+    ops.set_timer(None)
+    kern = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(timer.summary().items())}
+    print(json.dumps({"world": args.world, "rank": 0, "config": gcfg.name,
+                      "users_own": shard.n_own, "posts_padded": shard.n_posts_pad,
+                      "local_edges_per_step": edges_local,
+                      "ms_per_step_compute": round(ms, 3),
+                      "kernels_ms_per_step": kern, "kernels_sum_ms": round(sum(kern.values()), 3)}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()

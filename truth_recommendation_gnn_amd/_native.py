@@ -51,6 +51,8 @@ _SIGS = {
     "hgnn_score_gather": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _c_i64, _c_i32, _p,
                                    ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p,
                                    _c_i32, _p]),
+    "hgnn_score_gather2": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _c_i64, _p,
+                                    ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_neighbors": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p,
                                        _p, _p, _c_sz, _p]),

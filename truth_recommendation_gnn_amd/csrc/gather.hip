@@ -38,13 +38,19 @@ struct GatherArgs {
   const float* cscale;
   float inv_e;
   int32_t score;               // 1: c*inv_e*(sigmoid(s)-1)   2: inv_e*sigmoid(s)
+  // hgnn_score_gather2: a second grouped list (the negatives, mode 2, no heavy-row plan) summed
+  // into the same rows in the same pass; null otherwise
+  const int32_t* rowptr2;
+  const int32_t* col2;
 };
 
-// Sum of row segment [beg, end) into acc (per lane: VPL vectors of width W).  SC: the weight of
-// each edge is recomputed from the score <x[col[p]], rv> (rv = the row's own vector, e.g. P[post]
-// for the loss gradient dP), so no per-edge weight array is stored or read.
+// Sum of row segment [beg, end) of `col` into acc (per lane: VPL vectors of width W; each slot of
+// LPR lanes holds its own partial sum, combined by slot_combine).  SC: the weight of each edge is
+// recomputed from the score <x[col[p]], rv> (rv = the row's own vector, e.g. P[post] for the loss
+// gradient dP) with weight mode `score`, so no per-edge weight array is stored or read.
 template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC>
-__device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, int64_t end,
+__device__ __forceinline__ void segment_sum(const GatherArgs& a, const int32_t* col, int score,
+                                            int64_t beg, int64_t end,
                                             const typename Vec<W>::T (&rv)[VPL],
                                             typename Vec<W>::T (&acc)[VPL]) {
   using V = Vec<W>;
@@ -57,7 +63,7 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
     int cidx = 0;
     float wv = 1.f;
     if (lane < n) {
-      cidx = a.col[base + lane];
+      cidx = col[base + lane];
       if (HAS_W) {
         wv = a.edge_w ? a.edge_w[base + lane] : 1.f;
         if (a.col_w) wv *= a.col_w[cidx];
@@ -79,7 +85,7 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
         }
       }
       if constexpr (SC) {
-        const float cw = a.score == 1 ? *a.cscale * a.inv_e : a.inv_e;
+        const float cw = score == 1 ? *a.cscale * a.inv_e : a.inv_e;
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
           float sdot = 0.f;
@@ -87,7 +93,7 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
           for (int q = 0; q < VPL; ++q) sdot += V::dot(rv[q], v[u][q]);
           sdot = slot_sum<LPR>(sdot);
           const float sg = sigmoid_t(sdot, exp_neg_abs(sdot));
-          we[u] = cw * (a.score == 1 ? sg - 1.f : sg);
+          we[u] = cw * (score == 1 ? sg - 1.f : sg);
         }
       }
 #pragma unroll
@@ -99,7 +105,12 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, int64_t beg, in
         }
     }
   }
-  // combine the NS slots (lanes sl, sl+LPR, ...)
+}
+
+// combine the NS slots (lanes sl, sl+LPR, ...)
+template <int LPR, int VPL, int W>
+__device__ __forceinline__ void slot_combine(typename Vec<W>::T (&acc)[VPL]) {
+  using V = Vec<W>;
 #pragma unroll
   for (int m = LPR; m < 64; m <<= 1)
 #pragma unroll
@@ -117,11 +128,16 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
   int64_t row, beg, end;
   float* dst;
   bool partial;
+  const bool two = SC && a.rowptr2;             // hgnn_score_gather2: + the negatives' segment
+  bool own = true;                              // this wave sums the row's (first) segment
   if (item < a.n_rows) {                       // light row: whole row in this wave
     row = item;
     beg = a.rowptr[row];
     end = a.rowptr[row + 1];
-    if (end - beg > a.chunk) return;            // heavy: handled by chunks + fixup
+    if (end - beg > a.chunk) {                  // heavy: handled by chunks + fixup ...
+      if (!two) return;
+      own = false;                              // ... the second list's segment still here
+    }
     dst = a.out + row * a.d;
     partial = false;
   } else {                                      // chunk of a heavy row -> slab slot
@@ -145,7 +161,11 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
     const int c = (q * LPR + sl) * W;
     rv[q] = (SC && c < a.d) ? V::load(a.rowvec + row * a.d + c) : V::zero();
   }
-  segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, beg, end, rv, acc);
+  if (own) segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, a.col, a.score, beg, end, rv, acc);
+  if (two && !partial)
+    segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, a.col2, 2, a.rowptr2[row], a.rowptr2[row + 1],
+                                                rv, acc);
+  slot_combine<LPR, VPL, W>(acc);
   if (!writer) return;
   float s = 1.f;
   if (!partial && a.mean) s = end > beg ? 1.f / (float)(end - beg) : 0.f;
@@ -207,7 +227,7 @@ __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
       typename V::T t = buf[threadIdx.x];
       V::scale(t, s);
       float* o = a.out + row * a.d + c;
-      if (a.accumulate) V::add(t, V::load(o));
+      if (a.accumulate || a.rowptr2) V::add(t, V::load(o));
       V::store(o, t);
     }
     __syncthreads();
@@ -258,6 +278,8 @@ static int run_gather(GatherArgs a, hipStream_t stream) {
   const bool has_w = a.edge_w || a.col_w;
   if (a.score && (has_w || a.mean || !a.rowvec || (a.score == 1 && !a.cscale)))
     return fail(HGNN_E_ARG, "score_gather: bad mode/arguments");
+  if (a.rowptr2 && (a.score != 1 || a.accumulate))
+    return fail(HGNN_E_ARG, "score_gather2: needs mode 1 for the first list, no accumulate");
   if (int rc = dispatch_gather(a, has_w, stream)) return rc;
   if (a.n_heavy > 0) {
     const dim3 grid((unsigned)a.n_heavy), block(256);
@@ -323,6 +345,24 @@ int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t 
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
   a.d = d; a.chunk = chunk; a.accumulate = accumulate ? 1 : 0;
   a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = mode;
+  return run_gather(a, as_stream(stream));
+}
+
+int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t d,
+                       const int32_t* rowptr, const int32_t* col, const int32_t* rowptr_n,
+                       const int32_t* col_n, int64_t n_rows, const float* cscale, float inv_e,
+                       const int32_t* heavy_rows, const int32_t* heavy_first, int64_t n_heavy,
+                       int64_t n_chunks, int32_t chunk, float* slab, float* out,
+                       hgnn_stream_t stream) {
+  (void)n_x;
+  if (!rowptr_n && n_rows > 0) return fail(HGNN_E_ARG, "score_gather2: rowptr_n is null");
+  GatherArgs a{};
+  a.x = x; a.rowptr = rowptr; a.col = col;
+  a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
+  a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
+  a.d = d; a.chunk = chunk; a.accumulate = 0;
+  a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = 1;
+  a.rowptr2 = rowptr_n; a.col2 = col_n;
   return run_gather(a, as_stream(stream));
 }
 

@@ -152,6 +152,30 @@ def _score_gather(U, P, grouped, mode, cscale, inv_e, out, accumulate, tag):
             N.stream_ptr(dev)), "hgnn_score_gather")
 
 
+def _score_gather2(U, P, pos, negs, cscale, inv_e, out):
+    """Both dP gathers in one pass (hgnn_score_gather2): row r sums its positive edges (mode 1,
+    heavy-row plan) and its negatives (mode 2) into one accumulator and writes dP[r] once."""
+    p = pos.plan
+    dev = out.device
+    d = int(out.shape[1])
+    n = pos.n_rows
+    slab = None
+    if p.n_heavy:
+        slab = torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
+    E = int(pos.col.numel()) + int(negs.col.numel())
+    nb = gather_bytes(E, n, d, False) + 4 * (n + 1) + 4 * n * d
+    cb = gather_compulsory_bytes(E, n, int(U.shape[0]), d, False) + 4 * (n + 1) + 4 * n * d
+    with _timed(f"score_gather[{n}<-{U.shape[0]}]x{d}", nb, cb):
+        N.check(N.lib().hgnn_score_gather2(
+            N.ptr(U), U.shape[0], N.ptr(P), d, N.ptr(pos.rowptr), N.ptr(pos.col),
+            N.ptr(negs.rowptr), N.ptr(negs.col), n, N.ptr(cscale), inv_e, N.ptr(p.heavy_rows),
+            N.ptr(p.heavy_first), p.n_heavy, p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out),
+            N.stream_ptr(dev)), "hgnn_score_gather2")
+
+
+_SCORE2 = os.environ.get("HGNN_SCORE2", "1") == "1"   # 0: the two separate dP gathers (A/B)
+
+
 def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K2: ``grad_x_src[j] (+)= sum_{(j->i)} grad_aggr[i] / deg_i`` over the CSC."""
@@ -462,10 +486,13 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
         if lanes.side is not None:
             lanes.side.wait_stream(lanes.main)
     with torch.cuda.stream(lanes.stream(1)):
-        _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
         from .graph import GroupedEdges, Plan
         negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
-        _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
+        if _SCORE2:
+            _score_gather2(U, P, pf, negs, c, inv_e, dP)
+        else:
+            _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
+            _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
     with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
         if neg32:
             N.check(lib.hgnn_edge_score_fwd_i32(

@@ -650,6 +650,15 @@ class UserShard:
                                        ready=pend.wait)
 
 
+def _k2_into(impl, buf, g, csr):
+    """K2 of ``g`` over ``csr`` added into ``buf``; the first contribution writes a fresh buffer
+    (every row, zero where no edge), so no zero fill of the whole table precedes it."""
+    if buf is None:
+        return impl.scatter_mean_bwd_raw(g, csr)
+    impl.scatter_mean_bwd_raw(g, csr, out=buf)
+    return buf
+
+
 def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
     """UserShard.step: forward, loss and backward with every collective issued as early as its
     input exists and waited as late as its consumer allows (see the method docstring)."""
@@ -767,19 +776,13 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
         for j, (_, et, _) in enumerate(um):
             r = shard.rels[et]
             if r.kind[0] == "post":
-                if G_prev is None:
-                    G_prev = torch.zeros_like(hp)
-                impl.scatter_mean_bwd_raw(dxu[j], r.csr, out=G_prev)
+                G_prev = _k2_into(impl, G_prev, dxu[j], r.csr)
             else:
-                if d_xext is None:
-                    d_xext = torch.zeros_like(x_ext)
-                impl.scatter_mean_bwd_raw(dxu[j], r.csr, out=d_xext)
+                d_xext = _k2_into(impl, d_xext, dxu[j], r.csr)
         for j, (_, et, _) in enumerate(pm):
             r = shard.rels[et]
             if r.kind[0] == "post":
-                if G_prev is None:
-                    G_prev = torch.zeros_like(hp)
-                impl.scatter_mean_bwd_raw(dxp[j], r.csr, out=G_prev)
+                G_prev = _k2_into(impl, G_prev, dxp[j], r.csr)
         back, back_w = None, _Done()
         if d_xext is not None:
             n_own = hu.shape[0]
