@@ -22,6 +22,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _maxabs(t):
+    return float(t.abs().max()) if t.numel() else 0.0
+
+
 def _worker(rank, world, port, q, kind="engage2"):
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
@@ -58,7 +62,7 @@ def _worker(rank, world, port, q, kind="engage2"):
         out, ref_loss, ref_grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
         res = {"rank": rank,
                "loss_err": abs(float(total) - float(ref_loss)) / abs(float(ref_loss)),
-               "user_err": float((h_u.detach() - out["user"][lo:hi]).abs().max()),
+               "user_err": _maxabs(h_u.detach() - out["user"][lo:hi]),   # 0 rows: a rank with no users
                "post_err": float((h_p.detach()[:cfg.num_posts] - out["post"]).abs().max()),
                "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
                                max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
@@ -78,7 +82,8 @@ def _worker(rank, world, port, q, kind="engage2"):
 
 @pytest.mark.parametrize("world,kind", [(2, "engage2"), (3, "engage2"), (2, "rgcn"),
                                         (3, "rgcn"), (2, "rel4"), (3, "rel4"),
-                                        (3, "tiny_rgcn"), (3, "tiny4")])
+                                        (4, "rel4"), (3, "tiny_rgcn"), (3, "tiny4"),
+                                        (8, "tiny4")])
 def test_user_sharded_step_matches_single_process_oracle(world, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
