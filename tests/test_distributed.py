@@ -1,8 +1,10 @@
-"""CPU, world_size 2 and 3 (gloo): the destination-partitioned step of parallel.py reproduces the
-single-process oracle — outputs, loss and every parameter gradient — for the two-relation
-training graph, the reference ``WeightedRGCN`` (with the social user->user relation, whose
-remote sources come through the halo all-to-all) and the 4-relation cfg5 graph (user-user and
-post-post added)."""
+"""CPU, world_size 2, 3, 4 and 8 (gloo): the destination-partitioned step of parallel.py
+reproduces the single-process oracle — outputs, loss and every parameter gradient, through both
+the autograd path and UserShard.step's explicit schedule — for the two-relation training graph,
+the reference ``WeightedRGCN`` (with the social user->user relation, whose remote sources come
+through the halo all-to-all) and the 4-relation cfg5 graph (user-user and post-post added).  The
+tiny graphs put ranks with no edges of a relation, no halo rows, and (world 8, 7 users) no users
+at all beside ranks that have them: every rank must still join every collective."""
 import os
 import socket
 
