@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--autograd-sharded", action="store_true",
                    help="sharded path through autograd (forward + loss + backward()) instead of "
                         "UserShard.step's explicit collective schedule")
+    p.add_argument("--strong", action="store_true",
+                   help="N>1: partition the config's own graph over the ranks (strong scaling, e.g. "
+                        "BASELINE cfg4 on 8 GPUs) instead of an N-times larger one")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
@@ -172,7 +175,7 @@ def main():
                                      check=False, cscale=cscale)
     else:
         env = parallel.DistEnv.from_torch()
-        gcfg = synth.replicated(args.config, world) if args.scale == 1.0 else cfg
+        gcfg = cfg if (args.strong or args.scale != 1.0) else synth.replicated(args.config, world)
         g = synth.make_graph(gcfg, device=dev, device_gen=True)   # identical on every rank
         pos_g = g.edge_index_dict[synth.ENGAGES]
         pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
@@ -301,7 +304,7 @@ def main():
             "metric": "edges/s (fwd+bwd) hetero message-passing",
             "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded numpy PCG64 graph, Zipf post degrees; random-init weights)",
             "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
                                    f"E_engage={cfg.num_engages} (+reverse), "

@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Per-rank compute of the sharded N-GPU bench step (``UserShard.step``), on one GPU.
 
-Rank 0 of the weak-scaled graph (``synth.replicated(cfg, N)``: N x the users, posts and edges)
-runs the real sharded code path — its user range, the post-table slice, the explicit collective
+Rank 0 of the weak-scaled graph (``synth.replicated(cfg, N)``: N x the users, posts and edges),
+or with ``--strong`` of the config's own graph split N ways (BASELINE cfg4 on 8 GPUs), runs the
+real sharded code path — its user range, the post-table slice, the explicit collective
 schedule — with every collective replaced by a local stand-in of the same shape (reduce-scatter:
 this rank's slice of its own partial sums; all-gather: the own slice tiled N times; all-reduce:
 identity).  So it times what one rank computes at N GPUs, collectives excluded (RCCL needs one GPU
 per rank); the numbers are wrong (local degrees, tiled tables), the work is not.
-python scripts/shard_emulation.py --world 8 [--steps 20]"""
+python scripts/shard_emulation.py --world 8 [--steps 20] [--config cfg4 --strong]"""
 import argparse
 import json
 import os
@@ -50,9 +51,11 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--strong", action="store_true",
+                    help="partition the config's own graph (e.g. cfg4 over 8 ranks), not N x it")
     args = ap.parse_args()
     dev = torch.device("cuda")
-    gcfg = synth.replicated(args.config, args.world)
+    gcfg = synth.CONFIGS[args.config] if args.strong else synth.replicated(args.config, args.world)
     g = synth.make_graph(gcfg, device=dev, device_gen=True)
     pos_g = g.edge_index_dict[synth.ENGAGES]
     pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
@@ -91,6 +94,7 @@ def main():
     ops.set_timer(None)
     kern = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(timer.summary().items())}
     print(json.dumps({"world": args.world, "rank": 0, "config": gcfg.name,
+                      "scaling": "strong" if args.strong else "weak",
                       "users_own": shard.n_own, "posts_padded": shard.n_posts_pad,
                       "local_edges_per_step": edges_local,
                       "ms_per_step_compute": round(ms, 3),
