@@ -673,7 +673,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
     h_u, h_p, h_p_own = x_user_own, x_post, x_post[shard.p_lo:shard.p_hi]
     ag = None                                   # in-flight all-gather of h_p
     saved = []
-    for convs, layout in layers:
+    for li, (convs, layout) in enumerate(layers):
         um, pm = layout.get("user", []), layout.get("post", [])
         for _, et, _ in um + pm:
             if et not in shard.rels:
@@ -707,7 +707,11 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
                     halo_w.wait()
                     x_ext = h_u if halo is None else torch.cat([h_u, halo])
                 a_u.append(impl.gather_mean_raw(x_ext, r.csr))
-        y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True) if um else h_u
+        # the last layer's user projection waits until the post table's all-gather is issued: the
+        # loss needs that table at once, so the projection and the negatives sort both run under
+        # the collective (the reduce-scatter still has the user-side gathers under it)
+        late_u = multi and bool(pm) and bool(um) and li == len(layers) - 1
+        y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True) if um and not late_u else h_u
         # F5 post side on the owned slice, then its all-gather
         a_p = []
         for _, et, _ in pm:
@@ -723,6 +727,8 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
             y_p, ag = env.all_gather_async(y_p_own) if multi else (y_p_own, None)
         else:
             y_p_own, y_p = h_p_own, h_p
+        if late_u:
+            y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True)
         saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu, Wp,
                       bu is not None, bp is not None))
         h_u, h_p, h_p_own = y_u, y_p, y_p_own
