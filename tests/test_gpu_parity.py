@@ -119,6 +119,31 @@ def test_score_gather_matches_float64(d, mode):
     close(out, ref + 0.5)
 
 
+@pytest.mark.parametrize("d", [5, 64, 128])
+def test_score_gather2_matches_float64(d):
+    """hgnn_score_gather2: positives (mode 1, heavy rows split with chunk=16) and negatives (mode 2)
+    summed into one dP pass; includes posts with no positive or no negative edge."""
+    rng = np.random.default_rng(40 + d)
+    n_u, n_p, E = 600, 250, 9000
+    pos = rand_coo(rng, n_u, n_p, E, skew=True)                  # Zipf head -> heavy rows
+    neg = torch.stack([pos[0], torch.from_numpy(rng.integers(0, n_p - 10, E))])  # 10 posts unused
+    U = torch.from_numpy(rng.standard_normal((n_u, d)).astype(np.float32) * 0.3)
+    P = torch.from_numpy(rng.standard_normal((n_p, d)).astype(np.float32) * 0.3)
+    c, inv_e = 1.7, 1.0 / 12345
+    ref = torch.zeros(n_p, d, dtype=torch.float64)
+    for ei, mode in ((pos, 1), (neg, 2)):
+        sg = torch.sigmoid((U.double()[ei[0]] * P.double()[ei[1]]).sum(1))
+        w = c * inv_e * (sg - 1) if mode == 1 else inv_e * sg
+        ref.index_add_(0, ei[1], w[:, None] * U.double()[ei[0]])
+    csr = graph.RelationCSR(pos.to(DEV), n_u, n_p, chunk=16)
+    assert csr.fwd.plan.n_heavy > 0
+    ncsr = graph.RelationCSR(neg.to(DEV), n_u, n_p, chunk=1 << 30)
+    out = torch.full((n_p, d), 0.5, device=DEV)                 # every row must be written
+    ops._score_gather2(U.to(DEV), P.to(DEV), csr.fwd, ncsr.fwd, torch.tensor(c, device=DEV),
+                       inv_e, out)
+    close(out, ref)
+
+
 def test_gather_is_deterministic_bitwise():
     rng = np.random.default_rng(5)
     ei = rand_coo(rng, 5000, 200, 100000, skew=True).to(DEV)
