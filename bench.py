@@ -79,6 +79,8 @@ def parse():
     p.add_argument("--strong", action="store_true",
                    help="N>1: partition the config's own graph over the ranks (strong scaling, e.g. "
                         "BASELINE cfg4 on 8 GPUs) instead of an N-times larger one")
+    p.add_argument("--rccl-normal-priority", action="store_true",
+                   help="RCCL collectives on a normal-priority stream (default: high priority)")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
     return p.parse_args()
@@ -128,6 +130,21 @@ def cpu_baseline(cfg, threads):
                       f"bwd+Adam, mean of {n} steps after 1 warmup (oracle/sage_ref.py, torch CPU)"}
 
 
+def _pg_options(args):
+    """RCCL on a high-priority stream: every collective of the sharded step runs under compute
+    kernels that fill the GPU, and the priority lets its workgroups be dispatched as soon as CUs
+    free up instead of queueing behind the compute grid (``--rccl-normal-priority`` turns it
+    off)."""
+    if args.dist_backend != "nccl" or args.rccl_normal_priority:
+        return None
+    try:
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        return opts
+    except (AttributeError, RuntimeError):
+        return None
+
+
 def _barrier(args, local):
     if args.dist_backend == "nccl":
         dist.barrier(device_ids=[local])
@@ -148,7 +165,7 @@ def main():
         if "MASTER_ADDR" not in os.environ:          # plain `python bench.py --dist`
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0",
                               WORLD_SIZE="1")
-        dist.init_process_group(args.dist_backend)
+        dist.init_process_group(args.dist_backend, pg_options=_pg_options(args))
     dev = torch.device("cuda", local)
     cfg = synth.CONFIGS[args.config]
     if args.scale != 1.0:
