@@ -252,7 +252,20 @@ static int dispatch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) 
     const int nv = d / 4;  // float4 vectors per row
     if (nv <= 4) return launch_gather<4, 1, 4, 4>(a, has_w, stream);
     if (nv <= 8) return launch_gather<8, 1, 4, 4>(a, has_w, stream);
-    if (nv <= 16) return launch_gather<16, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 16) {
+      // d = 64: rows in flight per wave (4 x UNROLL) chosen per variant on cfg2 (MI355X).  The
+      // mean gathers take 32: user rows average 20 edges, so one round of loads covers most of
+      // them (user<-post 0.84 -> 0.80 ms); the weighted K2 24 (0.50 -> 0.485 ms); the score
+      // gather keeps 16 (its dot products hold more registers: 1.39 ms at 16, 1.50 at 32).
+      const dim3 grid((unsigned)cdiv(a.n_items, 4)), block(256);
+      if (a.score)
+        hipLaunchKernelGGL((k_gather<16, 1, 4, 4, false, true>), grid, block, 0, stream, a);
+      else if (has_w)
+        hipLaunchKernelGGL((k_gather<16, 1, 4, 6, true>), grid, block, 0, stream, a);
+      else
+        hipLaunchKernelGGL((k_gather<16, 1, 4, 8, false>), grid, block, 0, stream, a);
+      return check_launch("k_gather");
+    }
     if (nv <= 32) return launch_gather<32, 1, 4, 4>(a, has_w, stream);
     if (nv <= 64) return launch_gather<64, 1, 4, 4>(a, has_w, stream);
     if (nv <= 128) return launch_gather<64, 2, 4, 2>(a, has_w, stream);
