@@ -819,19 +819,18 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
 def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
     """Sum parameter gradients over ranks with one flat all-reduce.  Every rank contributes every
     trainable parameter (zeros where its backward produced no gradient — a rank whose shard holds
-    no edge of some relation), so the flat buffers line up across ranks."""
+    no edge of some relation), so the flat buffers line up across ranks.  One concatenation in,
+    one multi-tensor copy out (not a copy kernel per parameter)."""
     if env.world == 1:
         return
     params = [p for p in model.parameters() if p.requires_grad]
     flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
                       for p in params])
     env.all_reduce_(flat)
-    o = 0
-    for p in params:
-        n = p.numel()
-        g = flat[o:o + n].view_as(p)
+    views = [v.view_as(p) for v, p in zip(torch.split(flat, [p.numel() for p in params]), params)]
+    have = [i for i, p in enumerate(params) if p.grad is not None]
+    if have:
+        torch._foreach_copy_([params[i].grad for i in have], [views[i] for i in have])
+    for i, p in enumerate(params):
         if p.grad is None:
-            p.grad = g.clone()
-        else:
-            p.grad.copy_(g)
-        o += n
+            p.grad = views[i].clone()
