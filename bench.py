@@ -1,32 +1,46 @@
 #!/usr/bin/env python3
 """Headline bench: edges/s (fwd+bwd) of hetero message passing on MI355X (BASELINE.json).
 
-Workload (N=1): BASELINE config 2 — synthetic user<->post graph, 1M users / 100k posts / 20M
-engages (+ the 20M reverse relation), d = h = 64, 2-layer relation-weighted SAGE
-(``HeteroSAGE`` = the reference ``WeightedRGCN`` layer stacked twice).  One step = one training
-step of ``train_gnn.py:242-285``: forward, the reference link loss over all 20M positive edges
-with fresh ``torch.randint`` negatives, full backward, Adam.  Inputs resident in HBM before the
-timed region.  Metric numerator = sum over layers and relations of E_r = 80M edges/step.
+Workload — BASELINE ``configs[3]``, the graph the north_star's targets are stated on (cfg4):
+synthetic 9M users / 1M posts (10M nodes) / 200M engages + the 200M reverse relation, d = h =
+128, 2-layer relation-weighted SAGE (``HeteroSAGE`` = the reference ``WeightedRGCN`` layer
+stacked twice).  One step = one training step of ``train_gnn.py:242-285``: forward, the
+reference link loss over all 200M positive edges with fresh ``torch.randint``-distributed
+negatives, full backward, Adam.  Inputs are resident in HBM before the timed region.  Metric
+numerator = sum over layers and relations of E_r = 800M edges/step.
 
-N>1 (``torch.distributed.run``): weak scaling — one global graph N times the cfg2 size (N·1M
-users, N·100k posts, N·20M engages), destination-partitioned (parallel.py): each rank owns a
-cfg2-sized user range and a 1/N row slice of the post table.  Per layer one RCCL reduce-scatter
-of the post partial sums and one all-gather of the projected slices (their adjoints in the
-backward), a halo all-to-all for user->user relations when the config has them (cfg5), weight
-gradients all-reduced once per step.  The step is ``UserShard.step``: the same kernels as the
-autograd path, with every collective issued as soon as its input is complete and awaited only
-by its consumer (``--autograd-sharded`` runs forward + loss + backward() instead).
-value = all ranks' edges / max-over-ranks time.
+* ``--gpus 1`` (default): the whole cfg4 graph on one MI355X (it fits: ~60 GB resident).
+* ``--gpus N`` (N > 1): STRONG scaling of the same cfg4 graph, destination-partitioned over N
+  ranks (``parallel.UserShard``): each rank owns 1/N of the users and a 1/N row slice of the post
+  table; per layer one RCCL reduce-scatter of the post partial sums and one all-gather of the
+  projected slices (their adjoints in the backward); weight gradients all-reduced once per step.
+  ``--weak`` instead grows the graph N-fold (each rank a cfg-sized share).
+  Launch: under ``torch.distributed.run`` (RANK/WORLD_SIZE in the environment) every process is
+  one rank; run as plain ``python bench.py --gpus N`` the script starts the N rank processes
+  itself (spawned interpreters, before this process touches the GPU) and exits with their
+  status.  A world size that disagrees with ``--gpus`` is an error, never a silent 1-GPU run.
+* ``--config cfg2|cfg3`` (1 GPU): the smaller BASELINE configs; ``--config cfg5``: the
+  4-relation neighbour-sampled mini-batch workload (``sampler.py``; one step = one mini-batch per
+  rank, data-parallel over N ranks).
 
-Prints ONE JSON line (rank 0) with ``roofline`` for the dominant kernel (the K1 forward gather:
-algorithmic bytes per launch / HIP-event-timed duration inside the timed region) and
-``cpu_baseline`` (the plain-torch CPU oracle on a bounded sample, rank 0 only).
+value = all ranks' edges / max-over-ranks wall time of exactly ``--steps`` steps, bracketed by a
+barrier + device synchronise, with NO per-kernel events inside.  A second, separately timed run
+of ``--timer-steps`` steps records HIP events around every kernel (on the stream it is launched
+on) for ``roofline`` — the dominant HBM kernel, the K1 forward gather over the largest source
+table: algorithmic bytes per launch / average launch time, ``traffic`` from the committed PMC
+passes of the same launch (``profiles/pmc_r2.json``) — and for ``projection`` (K3 vs the fp32
+MFMA peak).  ``cpu_baseline`` (rank 0, N=1 only): the plain-torch CPU oracle (PyG's op pattern)
+on the box's allotted host cores, median of 5 steps after 2 warm-ups, on a stated down-scaled
+sample of the same graph family (same degree distributions, so per-edge work is the same).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -36,15 +50,19 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from truth_recommendation_gnn_amd import HeteroSAGE, ops, synth  # noqa: E402
+from truth_recommendation_gnn_amd import HeteroSAGE, synth  # noqa: E402
 from truth_recommendation_gnn_amd import parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 FP32_MFMA_PEAK_TFS = 157.3  # same table: dense fp32 matrix (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
+DEFAULT_CONFIG = "cfg4"
 # every relation a config may hold, with the reference's weights (train_gnn.py:163-164:
 # w_direct 1.0, w_social 0.75); cfg5's post-post relation takes 1.0
 ALL_RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
                  (synth.POST_POST, 1.0)]
+# CPU-baseline sample: the config scaled by this factor (≈5 s per CPU step on 8 container cores,
+# so 7 steps stay within the bench's few-minute budget)
+CPU_SAMPLE_SCALE = {"cfg1": 1.0, "cfg2": 1 / 16, "cfg3": 1 / 16, "cfg4": 1 / 128, "cfg5": 1 / 128}
 
 
 def relations_of(cfg):
@@ -57,41 +75,84 @@ def relations_of(cfg):
     return [(et, w) for et, w in ALL_RELATIONS if et in have]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="cfg2")
+    p.add_argument("--config", default=DEFAULT_CONFIG)
+    p.add_argument("--weak", action="store_true",
+                   help="N>1: an N-times larger graph, each rank a config-sized share (default: "
+                        "strong scaling, the config's own graph split N ways)")
+    p.add_argument("--strong", action="store_true", help="(the default at N>1; kept for old "
+                   "command lines)")
+    p.add_argument("--full-batch", action="store_true",
+                   help="cfg5: the full-graph 4-relation step instead of the sampled mini-batches")
+    p.add_argument("--batch-seeds", type=int, default=1024,
+                   help="cfg5 mini-batch: seed users and seed posts per batch per rank")
     p.add_argument("--scale", type=float, default=1.0, help="shrink the config (debug only)")
+    p.add_argument("--timer-steps", type=int, default=5,
+                   help="steps of the separate per-kernel-event run (0: none)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=None,
+                   help="default: the box's allotted CPUs (OMP_NUM_THREADS / affinity)")
+    p.add_argument("--cpu-sample-scale", type=float, default=None)
     p.add_argument("--profile-steps", action="store_true",
-                   help="no per-kernel events (for rocprofv3 runs)")
+                   help="no per-kernel-event run (for rocprofv3 runs)")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL, the product path); gloo only to rehearse N>1 on one GPU")
     p.add_argument("--dist", action="store_true",
-                   help="take the sharded path (process group + collectives) even at world size 1: "
-                        "runs the RCCL calls on a 1-GPU box")
+                   help="take the sharded path (process group + collectives) even at world size 1")
     p.add_argument("--autograd-sharded", action="store_true",
                    help="sharded path through autograd (forward + loss + backward()) instead of "
                         "UserShard.step's explicit collective schedule")
-    p.add_argument("--strong", action="store_true",
-                   help="N>1: partition the config's own graph over the ranks (strong scaling, e.g. "
-                        "BASELINE cfg4 on 8 GPUs) instead of an N-times larger one")
     p.add_argument("--rccl-normal-priority", action="store_true",
                    help="RCCL collectives on a normal-priority stream (default: high priority)")
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal on a 1-GPU box, with --dist-backend gloo)")
-    return p.parse_args()
+    p.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                   help="cpu: rehearse the launcher and sharded schedule on host cores with the "
+                        "compute ops a test injects (tests/test_bench_launch.py); never a "
+                        "measurement")
+    p.add_argument("--json-out", default=None, help="also write the JSON line to this file")
+    return p.parse_args(argv)
 
 
-def cpu_baseline(cfg, threads):
-    """Oracle (plain torch CPU, PyG's op pattern) on a bounded cfg sample; edges/s."""
+# ----------------------------------------------------------------------------- CPU baseline
+def host_cores():
+    """(physical cores of the host from lscpu, CPUs allotted to this job)."""
+    phys = None
+    try:
+        out = subprocess.run(["lscpu", "-p=CORE,SOCKET"], capture_output=True, text=True,
+                             timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")}) or None
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        allotted = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allotted = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        allotted = min(allotted, int(omp))
+    if phys:
+        allotted = min(allotted, phys)
+    return phys, allotted
+
+
+def cpu_baseline(cfg, threads=None, scale=None):
+    """The plain-torch CPU oracle (PyG's op pattern: materialised ``index_select``,
+    ``scatter_reduce`` mean, ``addmm``) running the same training step on a down-scaled graph of
+    the same family; edges/s = median over 5 steps after 2 warm-ups."""
     from oracle import sage_ref
+    phys, allotted = host_cores()
+    threads = threads or allotted
     torch.set_num_threads(threads)
     rels = relations_of(cfg)
-    sample = synth.scaled(cfg.name, 0.05) if cfg.num_engages > 1_000_000 else cfg
+    f = scale if scale is not None else CPU_SAMPLE_SCALE.get(cfg.name.split("x")[0], 1 / 64)
+    sample = cfg if f >= 1.0 else synth.dataclasses.replace(
+        synth.scaled(cfg.name.split("x")[0], f), dim=cfg.dim, hidden=cfg.hidden,
+        layers=cfg.layers)
     g = synth.make_graph(sample)
     names = []
     for l in range(sample.layers):
@@ -113,29 +174,70 @@ def cpu_baseline(cfg, threads):
         loss.backward()
         opt.step()
 
-    step()
-    t0 = time.perf_counter()
-    n = 0
-    while True:
+    for _ in range(2):
         step()
-        n += 1
-        if time.perf_counter() - t0 > 10.0 or n >= 5:
-            break
-    dt = (time.perf_counter() - t0) / n
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    dt = statistics.median(times)
     edges = sample.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
-    return {"value": edges / dt, "unit": "edges/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{sample.name}: U={sample.num_users} P={sample.num_posts} "
-                      f"E_engage={sample.num_engages} d={sample.dim}, {sample.layers}-layer fwd+loss+"
-                      f"bwd+Adam, mean of {n} steps after 1 warmup (oracle/sage_ref.py, torch CPU)"}
+    return {"value": round(edges / dt, 1), "unit": "edges/s", "cores": threads,
+            "host_physical_cores": phys, "kind": "port",
+            "sample": f"{cfg.name} family scaled x{f:g}: U={sample.num_users} "
+                      f"P={sample.num_posts} E_engage={sample.num_engages} d=h={sample.dim}, "
+                      f"{sample.layers}-layer fwd+loss+bwd+Adam ({edges} edges/step); median of "
+                      f"5 steps after 2 warm-ups ({dt:.2f} s/step), oracle/sage_ref.py on torch "
+                      f"CPU with {threads} threads = the CPUs allotted to this job "
+                      f"(host has {phys} physical cores); edges/s extrapolates linearly "
+                      f"(per-edge work is scale-free, the sample's smaller tables favour the CPU)"}
 
 
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(local_rank, world, port, argv, impl_factory):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    run(parse(argv), impl=impl_factory() if impl_factory is not None else None)
+
+
+def launch(argv, impl_factory=None):
+    """Start ``--gpus`` rank processes of this bench (fresh interpreters: nothing here has
+    touched the GPU) and wait for them; a failing rank fails the launch."""
+    import torch.multiprocessing as mp
+    args = parse(argv)
+    mp.start_processes(_rank_entry, args=(args.gpus, _free_port(), argv, impl_factory),
+                       nprocs=args.gpus, join=True, start_method="spawn")
+
+
+def main(argv=None, impl_factory=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            launch(argv, impl_factory)
+            return
+    elif int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}; "
+                         "refusing to report a world size the run does not use")
+    run(args, impl=impl_factory() if impl_factory is not None else None)
+
+
+# ----------------------------------------------------------------------------- one rank
 def _pg_options(args):
     """RCCL on a high-priority stream: every collective of the sharded step runs under compute
     kernels that fill the GPU, and the priority lets its workgroups be dispatched as soon as CUs
     free up instead of queueing behind the compute grid (``--rccl-normal-priority`` turns it
     off)."""
-    if args.dist_backend != "nccl" or args.rccl_normal_priority:
+    if args.dist_backend != "nccl" or args.rccl_normal_priority or args.device == "cpu":
         return None
     try:
         opts = dist.ProcessGroupNCCL.Options()
@@ -145,33 +247,105 @@ def _pg_options(args):
         return None
 
 
-def _barrier(args, local):
-    if args.dist_backend == "nccl":
-        dist.barrier(device_ids=[local])
-    else:
-        dist.barrier()
+def _pmc_traffic(cfg_name, world, kernel):
+    """Per-launch HBM bytes of ``kernel`` from the committed PMC passes (scripts/pmc_round.sh
+    -> profiles/pmc_r2.json), for the same config and world size; (None, None) if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_r2.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pm = json.load(f)
+    rec = pm.get("launches", {}).get(f"{cfg_name}|n{world}|{kernel}")
+    if not rec:
+        return None, None
+    return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_r2.json ({rec.get('source', '')})"
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    sharded = world > 1 or args.dist
-    if args.same_device:
-        local = 0
-    torch.cuda.set_device(local)
-    if sharded:
-        if "MASTER_ADDR" not in os.environ:          # plain `python bench.py --dist`
-            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29531", RANK="0",
-                              WORLD_SIZE="1")
-        dist.init_process_group(args.dist_backend, pg_options=_pg_options(args))
-    dev = torch.device("cuda", local)
+def _workload_config(args, world):
     cfg = synth.CONFIGS[args.config]
     if args.scale != 1.0:
         cfg = synth.scaled(args.config, args.scale)
+    if world > 1 and args.weak:
+        cfg = synth.replicated(args.config, world) if args.scale == 1.0 else \
+            synth.dataclasses.replace(
+                cfg, name=f"{cfg.name}x{world}gpu", num_users=cfg.num_users * world,
+                num_posts=cfg.num_posts * world, num_engages=cfg.num_engages * world,
+                num_social=cfg.num_social * world, num_post_post=cfg.num_post_post * world)
+    return cfg
+
+
+class _Clock:
+    """Barrier + device synchronise on both sides; max over ranks."""
+
+    def __init__(self, dev, sharded, args, local):
+        self.dev, self.sharded, self.args, self.local = dev, sharded, args, local
+
+    def sync(self):
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+        if self.sharded:
+            if self.args.dist_backend == "nccl" and self.dev.type == "cuda":
+                dist.barrier(device_ids=[self.local])
+            else:
+                dist.barrier()
+
+    def time(self, fn, n):
+        self.sync()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(n):
+            out = fn()
+        self.sync()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=self.dev)
+        if self.sharded:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return float(el), out
+
+
+def run(args, impl=None):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_cpu = args.device == "cpu"
+    if on_cpu and impl is None:
+        raise SystemExit("bench.py --device cpu is a launcher rehearsal: the compute ops must be "
+                         "injected (tests/test_bench_launch.py); there is no CPU product path")
+    sharded = world > 1 or args.dist or on_cpu
+    if args.same_device:
+        local = 0
+    if not on_cpu:
+        torch.cuda.set_device(local)
+    if sharded:
+        if "MASTER_ADDR" not in os.environ:          # plain `python bench.py --dist`
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                              RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("gloo" if on_cpu else args.dist_backend,
+                                pg_options=_pg_options(args))
+    dev = torch.device("cpu") if on_cpu else torch.device("cuda", local)
+    try:
+        if args.config == "cfg5" and not args.full_batch:
+            line = _run_minibatch(args, dev, world, rank, local, sharded, impl)
+        else:
+            line = _run_full_batch(args, dev, world, rank, local, sharded, impl)
+        if rank == 0:
+            s = json.dumps(line)
+            print(s, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(s + "\n")
+    finally:
+        if sharded:
+            dist.destroy_process_group()
+
+
+def _run_full_batch(args, dev, world, rank, local, sharded, impl):
+    from truth_recommendation_gnn_amd import ops
+    on_cpu = dev.type == "cpu"
+    cfg = _workload_config(args, world)
     torch.manual_seed(synth.WEIGHT_SEED)
     gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED + rank)
+    rels = relations_of(cfg)
+    t_setup = time.perf_counter()
     if not sharded:
         g = synth.make_graph(cfg, device=dev)
         pos = g.edge_index_dict[synth.ENGAGES]
@@ -179,58 +353,61 @@ def main():
         # BCEWithLogitsLoss() collapses the per-edge interaction weights to their mean
         # (train_gnn.py:276-281); the weights are static graph data, so the mean is taken once
         cscale = pw.mean()
-        rels = relations_of(cfg)
-        model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers).to(dev)
+        model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers, in_channels=cfg.dim).to(dev)
         with torch.no_grad():
-            model(g.x_dict, g.edge_index_dict)  # materialise lazy weights, build + cache CSR/CSC
+            model(g.x_dict, g.edge_index_dict)  # build + cache the CSR/CSC of every relation
         edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
 
-        def forward_loss():
+        def loss_fn():
             out = model(g.x_dict, g.edge_index_dict)
             neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
             return ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
                                      check=False, cscale=cscale)
     else:
         env = parallel.DistEnv.from_torch()
-        gcfg = cfg if (args.strong or args.scale != 1.0) else synth.replicated(args.config, world)
-        g = synth.make_graph(gcfg, device=dev, device_gen=True)   # identical on every rank
+        # every rank generates the identical seeded global graph on its own device (a few
+        # hundred ms on the GPU, cheaper than broadcasting 6.4 GB of edges), keeps its shard's
+        # CSRs and drops the global tensors before the timed region
+        g = synth.make_graph(cfg, device=dev, device_gen=not on_cpu)
         pos_g = g.edge_index_dict[synth.ENGAGES]
-        pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
-        rels = relations_of(gcfg)
-        shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in rels}, gcfg.num_users,
-                                   gcfg.num_posts, env, pos_weights=pw_g)
+        pw_g = synth.interaction_weights(cfg.num_posts).to(dev)[pos_g[1]]
+        shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in rels}, cfg.num_users,
+                                   cfg.num_posts, env, impl=impl, pos_weights=pw_g)
         x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
         x_post = g.x_dict["post"]
-        # global count over all relations
-        edges_step = gcfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
+        edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
         del g, pos_g, pw_g
-        torch.cuda.empty_cache()
-        model = HeteroSAGE(gcfg.hidden, rels, num_layers=gcfg.layers).to(dev)
+        if not on_cpu:
+            torch.cuda.empty_cache()
+        model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers, in_channels=cfg.dim).to(dev)
         with torch.no_grad():
             shard.forward(model, x_user, x_post)
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-        cfg = gcfg
 
-        def forward_loss():
+        def negatives():
+            if on_cpu:
+                return torch.randint(0, cfg.num_posts, (shard.pos_local.shape[1],),
+                                     generator=gen, device=dev)
+            return ops.sample_negatives(shard.pos_local, cfg.num_posts, generator=gen)
+
+        def loss_fn():
             # the post table's last all-gather stays in flight under the negatives draw + sort
             h_u, h_p = shard.forward(model, x_user, x_post, wait=False)
-            neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
-            return shard.loss(h_u, h_p, neg, neg_order="user")
+            return shard.loss(h_u, h_p, negatives(), neg_order="user")
 
-    # the reference's optimizer (train_gnn.py:207, Adam lr 0.001) as torch's fused kernel: one
-    # launch for every parameter instead of a multi-tensor chain per Adam stage
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    # the reference's optimizer (train_gnn.py:207, Adam lr 0.001); on the GPU torch's fused
+    # kernel: one launch for every parameter instead of a multi-tensor chain per Adam stage
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=not on_cpu)
 
     def step():
         opt.zero_grad(set_to_none=True)
         if sharded and not args.autograd_sharded:
             # explicit schedule: each collective issued when its input is complete and waited
             # for by its consumer only (parallel.UserShard.step; same kernels and gradients)
-            neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
-            loss = shard.step(model, x_user, x_post, neg, neg_order="user")
+            loss = shard.step(model, x_user, x_post, negatives(), neg_order="user")
         else:
-            loss = forward_loss()
+            loss = loss_fn()
             loss.backward()
         if sharded:
             parallel.sync_grads(model, parallel.DistEnv.from_torch())
@@ -239,112 +416,207 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    timer = None if args.profile_steps else ops.KernelTimer()
-    torch.cuda.synchronize()
+    clock = _Clock(dev, sharded, args, local)
+    setup_s = time.perf_counter() - t_setup
+    elapsed, loss = clock.time(step, args.steps)             # the headline: no events inside
+    value = edges_step * args.steps / elapsed                 # edges_step is the global count
+    # per-kernel HIP events: a separate run, so the headline carries none of their cost
+    kern, timer_ms = {}, None
+    if not on_cpu and not args.profile_steps and args.timer_steps > 0:
+        timer = ops.KernelTimer()
+        ops.set_timer(timer)
+        t_el, _ = clock.time(step, args.timer_steps)
+        ops.set_timer(None)
+        kern = timer.summary()
+        timer_ms = t_el / args.timer_steps * 1e3
+    # the reference's train() returns the global loss: sum the per-rank shares
+    loss_t = loss.detach().to(torch.float64).reshape(1).clone()
     if sharded:
-        _barrier(args, local)
-    ops.set_timer(timer)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
-    torch.cuda.synchronize()
+        dist.all_reduce(loss_t)
+    if rank != 0:
+        return None
+    roof = _roofline(kern, cfg, world)
+    proj = _projection(kern)
+    cpu = None
+    if not args.no_cpu_baseline and world == 1 and not on_cpu:
+        cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
+    strong = world == 1 or not args.weak
+    return {
+        "metric": "edges/s (fwd+bwd) hetero message-passing",
+        "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "strong" if strong else "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded graph, uniform users / Zipf post degrees; random-init weights)",
+        "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
+                               f"E_engage={cfg.num_engages} (+reverse), "
+                               f"relations={'+'.join(et[1] for et, _ in rels)}, "
+                               f"d=h={cfg.dim}, "
+                               f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
+                   "edges_per_step": edges_step, "global_batch": edges_step,
+                   "parallelism": (f"dst-partitioned x{world} (user shards + post-table slices: "
+                                   "RCCL reduce-scatter / all-gather per layer)"
+                                   if sharded and world > 1 else "single")},
+        "roofline": roof, "projection": proj, "cpu_baseline": cpu,
+        "kernel_timer": {"steps": args.timer_steps if kern else 0,
+                         "ms_per_step": round(timer_ms, 3) if timer_ms else None,
+                         "note": "per-kernel HIP events, separate run after the timed region"},
+        "kernels": {k: {"launches": v["launches"],
+                        "ms_per_step": round(v["ms"] / args.timer_steps, 4),
+                        "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
+                        "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
+                                            if v["ms"] else None),
+                        **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
+                           if v["flops"] and v["ms"] else {})}
+                    for k, v in sorted(kern.items())},
+        "loss": float(loss_t),
+        "setup_s": round(setup_s, 1),
+    }
+
+
+def _roofline(kern, cfg, world):
+    """The dominant HBM kernel: the K1 forward gather over the largest source table (the user
+    table; at N>1 the weighted post partial sums over the rank's own users)."""
+    fwd = {k: v for k, v in kern.items() if k.startswith(("gather_fwd", "gather_wfwd"))}
+    if not fwd:
+        return None
+    src_rows = lambda k: int(k.split("<-")[1].split("]")[0])
+    name = max(fwd, key=lambda k: (src_rows(k), fwd[k]["ms"]))
+    r = fwd[name]
+    per_launch_ms = r["ms"] / r["launches"]
+    per_launch_bytes = r["bytes"] / r["launches"]
+    ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
+    weighted = name.startswith("gather_wfwd")
+    traffic, tsrc = _pmc_traffic(cfg.name, world, name)
+    return {"bound": "hbm",
+            "kernel": (f"k_gather K1 weighted fwd (post partial sums) {name}" if weighted
+                       else f"k_gather K1 mean fwd {name}"),
+            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": tsrc, "avg_launch_us": round(per_launch_ms * 1e3, 1),
+            "algorithmic_bytes_per_launch": int(per_launch_bytes),
+            "bytes_formula": ("4*E*(2+d) + 4*(N_dst+1) + 4*N_dst*d" if weighted
+                              else "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d")}
+
+
+def _projection(kern):
+    """The dense projection (K3) against the fp32 MFMA peak: the largest forward launch."""
+    lin = {k: v for k, v in kern.items() if k.startswith("linear_fwd[") and v["flops"]}
+    if not lin:
+        return None
+    name = max(lin, key=lambda k: lin[k]["flops"] / lin[k]["launches"])
+    r = lin[name]
+    tfs = r["flops"] / (r["ms"] * 1e-3) / 1e12
+    return {"bound": "mfma", "kernel": f"k_linear_fwd K3 {name}",
+            "achieved": round(tfs, 1), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
+            "hbm_GB/s": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1),
+            "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 1),
+            "flops_per_launch": int(r["flops"] / r["launches"]),
+            "flops_formula": "2*N*K*H (K = sum of the input segments)"}
+
+
+# ----------------------------------------------------------------------------- cfg5 mini-batch
+def _run_minibatch(args, dev, world, rank, local, sharded, impl):
+    """BASELINE cfg5: the 4-relation graph (cfg4 + 90M user->user follows + 10M post->post),
+    neighbour-sampled (fanout [15, 10], PyG NeighborLoader semantics, ``sampler.py``), one
+    mini-batch of ``--batch-seeds`` seed users + seed posts per rank per step: sample -> 2-layer
+    hetero SAGE on the blocks (K1/K2/K3) -> link loss on the seed pairs -> backward -> Adam.
+    N ranks are data-parallel (each holds the graph, samples its own slice of the epoch's seed
+    order; one RCCL all-reduce of the weight gradients per step).  Edges = the sampled message
+    edges of every block and relation (what the gathers aggregate), summed over ranks."""
+    from truth_recommendation_gnn_amd import ops, sampler
+    if dev.type == "cpu":
+        raise SystemExit("the cfg5 mini-batch bench runs the HIP sampler: no CPU rehearsal")
+    cfg = synth.CONFIGS["cfg5"] if args.scale == 1.0 else synth.scaled("cfg5", args.scale)
+    t_setup = time.perf_counter()
+    g = synth.make_graph(cfg, device=dev, device_gen=True)
+    rels = relations_of(cfg)
+    fanouts = [15, 10]
+    s = sampler.NeighborSampler({"user": cfg.num_users, "post": cfg.num_posts},
+                                g.edge_index_dict, [et for et, _ in rels], fanouts)
+    torch.manual_seed(synth.WEIGHT_SEED)
+    model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers, in_channels=cfg.dim).to(dev)
+    env = parallel.DistEnv.from_torch()
     if sharded:
-        _barrier(args, local)
-    t1 = time.perf_counter()
-    ops.set_timer(None)
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    gen = torch.Generator(device=dev).manual_seed(0)
+    # one shuffle per epoch, as a loader over the seed nodes does; batches are slices of it
+    order = {"user": torch.randperm(cfg.num_users, device=dev, generator=gen),
+             "post": torch.randperm(cfg.num_posts, device=dev, generator=gen)}
+    nb = args.batch_seeds
+    per_epoch = min(cfg.num_users, cfg.num_posts) // (nb * world)
+    state = {"b": 0, "edges": 0}
+
+    def step():
+        gb = (state["b"] % max(per_epoch, 1)) * world + rank   # this rank's slice of the order
+        state["b"] += 1
+        seeds = {t: o[gb * nb:(gb + 1) * nb] for t, o in order.items()}
+        mb = s.sample(seeds, seed=gb)
+        state["edges"] += sum(blk.csr[et].num_edges for blk in mb.blocks for et in blk.csr)
+        out = sampler.forward_blocks(model, mb, g.x_dict)
+        # link loss on (seed user i, seed post i) pairs against the next seed post as negative
+        u, p = out["user"], out["post"]
+        pos = (u * p).sum(1)
+        neg = (u * p.roll(1, 0)).sum(1)
+        loss = (torch.nn.functional.softplus(-pos).mean()
+                + torch.nn.functional.softplus(neg).mean())
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        parallel.sync_grads(model, env)          # no-op at world size 1
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    setup_s = time.perf_counter() - t_setup
+    clock = _Clock(dev, sharded, args, local)
+    state["edges"] = 0
+    elapsed, loss = clock.time(step, args.steps)
+    edges = torch.tensor([float(state["edges"])], dtype=torch.float64, device=dev)
     if sharded:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed)
-    value = edges_step * args.steps / elapsed     # edges_step is already the global count
-    kern = timer.summary() if timer else {}
-    if rank == 0:
-        roof = None
-        # Roofline kernel: K1 forward gather with the largest source table — the HBM-bound one
-        # (user table, 256 MB at cfg2).  The post-table gathers (25.6 MB source) are served from
-        # the 256 MB Infinity Cache and read above the HBM peak in algorithmic bytes; they are
-        # listed under "kernels".
-        # (sharded runs: the post partial sums are the weighted forward gathers, "gather_wfwd")
-        fwd = {k: v for k, v in kern.items() if k.startswith(("gather_fwd", "gather_wfwd"))}
-        if fwd:
-            src_rows = lambda k: int(k.split("<-")[1].split("]")[0])
-            name = max(fwd, key=src_rows)
-            r = fwd[name]
-            per_launch_ms = r["ms"] / r["launches"]
-            per_launch_bytes = r["bytes"] / r["launches"]
-            ach = per_launch_bytes / (per_launch_ms * 1e-3) / 1e9
-            traffic, tsrc = None, None
-            weighted = name.startswith("gather_wfwd")
-            pmc = os.path.join(ROOT, "profiles", "pmc_gather_r1.json")
-            # the PMC passes measured the unweighted K1 launch of the cfg2 single-GPU step
-            if os.path.exists(pmc) and world == 1 and cfg.name == "cfg2" and not weighted:
-                with open(pmc) as f:
-                    pm = json.load(f)
-                traffic, tsrc = pm.get("hbm_bytes_per_launch"), "profiles/pmc_gather_r1.json"
-            roof = {"bound": "hbm",
-                    "kernel": (f"k_gather K1 weighted fwd (post partial sums) {name}" if weighted
-                               else f"k_gather K1 mean fwd {name}"),
-                    "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "traffic_source": tsrc, "avg_launch_us": round(per_launch_ms * 1e3, 1),
-                    "algorithmic_bytes_per_launch": int(per_launch_bytes),
-                    "bytes_formula": ("4*E*(2+d) + 4*(N_dst+1) + 4*N_dst*d" if weighted
-                                      else "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d")}
-        # The dense projection (K3) against the fp32 MFMA peak: the largest forward launch (the
-        # user side), HIP-event timed like the gather; the PMC MFMA-busy fraction of the same
-        # kernel comes from profiles/pmc_k3_r1.json (scripts/pmc_k3.sh) for cfg2.
-        proj = None
-        lin = {k: v for k, v in kern.items() if k.startswith("linear_fwd[") and v["flops"]}
-        if lin:
-            name = max(lin, key=lambda k: lin[k]["flops"] / lin[k]["launches"])
-            r = lin[name]
-            tfs = r["flops"] / (r["ms"] * 1e-3) / 1e12
-            busy, bsrc = None, None
-            pk = os.path.join(ROOT, "profiles", "pmc_k3_r1.json")
-            if os.path.exists(pk) and cfg.name == "cfg2" and cfg.hidden == 64:
-                with open(pk) as f:
-                    busy = json.load(f)["kernels"].get("hgnn::k_linear_fwd_v4<64, 128>", {}).get(
-                        "mfma_util")
-                bsrc = "profiles/pmc_k3_r1.json"
-            proj = {"bound": "mfma", "kernel": f"k_linear_fwd_v4 K3 {name}",
-                    "achieved": round(tfs, 1), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
-                    "hbm_GB/s": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1),
-                    "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 1),
-                    "flops_per_launch": int(r["flops"] / r["launches"]),
-                    "flops_formula": "2*N*K*H (K = sum of the input segments)",
-                    "mfma_busy_pmc": busy, "mfma_busy_source": bsrc}
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(cfg, args.cpu_threads)
-        line = {
-            "metric": "edges/s (fwd+bwd) hetero message-passing",
-            "value": round(value, 1), "unit": "edges/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (seeded numpy PCG64 graph, Zipf post degrees; random-init weights)",
-            "config": {"workload": f"{cfg.name}: U={cfg.num_users} P={cfg.num_posts} "
-                                   f"E_engage={cfg.num_engages} (+reverse), "
-                                   f"relations={'+'.join(et[1] for et, _ in relations_of(cfg))}, "
-                                   f"d=h={cfg.dim}, "
-                                   f"{cfg.layers}-layer hetero-SAGE train step (fwd+loss+bwd+Adam)",
-                       "edges_per_step": edges_step, "global_batch": edges_step,
-                       "parallelism": (f"user-shard x{world} (post-table slices: RCCL "
-                                       "reduce-scatter / all-gather per layer)"
-                                       if sharded else "single")},
-            "roofline": roof, "projection": proj, "cpu_baseline": cpu,
-            "kernels": {k: {"launches": v["launches"], "ms_per_step": round(v["ms"] / args.steps, 4),
-                            "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
-                            "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
-                                                if v["ms"] else None),
-                            **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
-                               if v["flops"] and v["ms"] else {})}
-                        for k, v in sorted(kern.items())},
-            "loss": float(loss.detach()),
-        }
-        print(json.dumps(line), flush=True)
-    if sharded:
-        dist.destroy_process_group()
+        dist.all_reduce(edges)
+    edges = float(edges)
+    kern = {}
+    if not args.profile_steps and args.timer_steps > 0:
+        timer = ops.KernelTimer()
+        ops.set_timer(timer)
+        clock.time(step, args.timer_steps)
+        ops.set_timer(None)
+        kern = timer.summary()
+    if rank != 0:
+        return None
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
+        cpu["sample"] = "full-batch " + cpu["sample"] + " (the oracle has no sampler: the " \
+                        "per-edge rate of the full-batch step is the CPU comparison)"
+    return {
+        "metric": "edges/s (fwd+bwd) hetero message-passing",
+        "value": round(edges / elapsed, 1), "unit": "edges/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded graph; random-init weights)",
+        "config": {"workload": f"{cfg.name} neighbour-sampled: U={cfg.num_users} "
+                               f"P={cfg.num_posts} E_engage={cfg.num_engages} (+reverse) "
+                               f"social={cfg.num_social} post_post={cfg.num_post_post}, "
+                               f"d=h={cfg.dim}, fanout {fanouts}, {nb}+{nb} seeds per rank per "
+                               "step, sample + 2-layer fwd + loss + bwd + Adam",
+                   "edges_per_step": round(edges / args.steps),
+                   "global_batch": 2 * nb * world,
+                   "batches_per_s": round(world * args.steps / elapsed, 1),
+                   "parallelism": f"data-parallel x{world}" if world > 1 else "single"},
+        "roofline": _roofline(kern, cfg, world), "projection": _projection(kern),
+        "cpu_baseline": cpu,
+        "kernels": {k: {"launches": v["launches"],
+                        "ms_per_step": round(v["ms"] / args.timer_steps, 4),
+                        "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
+                    for k, v in sorted(kern.items())},
+        "loss": float(loss.detach()), "setup_s": round(setup_s, 1),
+    }
 
 
 if __name__ == "__main__":

@@ -519,7 +519,14 @@ class _EdgeBCELoss(torch.autograd.Function):
         return loss
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, go):
+        # dU/dP are scaled in place by the upstream gradient: a second backward through the
+        # same graph (retain_graph=True) would scale them twice, so it is refused
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("edge_bce_loss: backward ran twice through the same graph; "
+                               "recompute the loss instead of retain_graph=True")
+        ctx.consumed = True
         dU, dP = ctx.saved_tensors
         g = go.to(torch.float32).reshape(()).contiguous()
         lib, s = N.lib(), N.stream_ptr(dU.device)
