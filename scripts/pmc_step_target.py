@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""rocprofv3 --pmc target: the single-GPU training step of bench.py (default cfg4) — forward,
+fused link loss, backward, Adam — for 1 warm-up + STEPS steps, after the one-time graph build.
+Prints ``PMC_TARGET {json}``: for every HBM kernel of the step, its launch grid (threads) and
+algorithmic bytes per launch (the formulas of ops.py / bench.py), so scripts/pmc_step_summarize.py
+can attribute the counter rows.  usage: pmc_step_target.py [cfg4] [steps]"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from truth_recommendation_gnn_amd import HeteroSAGE, graph, ops, synth  # noqa: E402
+
+name = sys.argv[1] if len(sys.argv) > 1 else "cfg4"
+STEPS = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+dev = torch.device("cuda")
+cfg = synth.CONFIGS[name]
+rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+g = synth.make_graph(cfg, device=dev)
+e = g.edge_index_dict
+pos = e[synth.ENGAGES]
+pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
+cscale = pw.mean()
+torch.manual_seed(synth.WEIGHT_SEED)
+model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers, in_channels=cfg.dim).to(dev)
+opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED)
+
+
+def step():
+    opt.zero_grad(set_to_none=True)
+    out = model(g.x_dict, e)
+    neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
+    loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
+                             check=False, cscale=cscale)
+    loss.backward()
+    opt.step()
+
+
+step()
+torch.cuda.synchronize()
+for _ in range(STEPS):
+    step()
+torch.cuda.synchronize()
+
+U, P, E, d = cfg.num_users, cfg.num_posts, cfg.num_engages, cfg.dim
+eng = graph.relation_csr(e[synth.ENGAGES], U, P)
+rev = graph.relation_csr(e[synth.REV_ENGAGES], P, U)
+
+
+def grid(grouped):
+    return -(-(grouped.n_rows + grouped.plan.n_chunks) // 4) * 256
+
+
+gb = ops.gather_bytes
+roles = {
+    # (kernel-name fragment, grid threads) -> role, algorithmic bytes per launch
+    "gather_fwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, false, false>", "grid": grid(eng.fwd),
+                               "alg_bytes": gb(E, P, d, False), "per_step": 2},
+    "gather_fwd[user<-post]": {"kernel": "k_gather<32, 1, 4, 4, false, false>", "grid": grid(rev.fwd),
+                               "alg_bytes": gb(E, U, d, False), "per_step": 2},
+    "gather_bwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, true, false>", "grid": grid(rev.bwd),
+                               "alg_bytes": gb(E, P, d, True), "per_step": 1},
+    "gather_bwd[user<-post]": {"kernel": "k_gather<32, 1, 4, 4, true, false>", "grid": grid(eng.bwd),
+                               "alg_bytes": gb(E, U, d, True), "per_step": 1},
+    "score_gather[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, false, true>", "grid": grid(eng.fwd),
+                                 "alg_bytes": gb(2 * E, P, d, False) + 4 * (P + 1) + 4 * P * d,
+                                 "per_step": 1},
+    "edge_score": {"kernel": "k_edge_score", "grid": None,
+                   "alg_bytes": 4 * E * (2 * d + 1 + 2) + 8 * U * d, "per_step": 1},
+    "sort_negatives": {"kernel": ["k_digit_counts", "k_digit_scatter", "k_tile_scan",
+                                  "k_rowptr_from_sorted"], "grid": None,
+                       "alg_bytes": 4 * E * (2 * 4) + 4 * E, "per_step": 1,
+                       "note": "all kernels of the per-step sort summed (launches per step)"},
+    "fixup": {"kernel": "k_fixup", "grid": None, "alg_bytes": None, "per_step": None},
+    "uniform_i32": {"kernel": "k_uniform_i32", "grid": None, "alg_bytes": 4 * E, "per_step": 1},
+}
+print("PMC_TARGET " + json.dumps({"config": cfg.name, "steps": STEPS + 1, "E": E, "U": U, "P": P,
+                                  "d": d, "roles": roles}), flush=True)

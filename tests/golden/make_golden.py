@@ -11,6 +11,7 @@ generator (``truth_recommendation_gnn_amd.synth``).
   loss, all 9 parameter gradients.
 * ``cfg2_slice_hetero_sage.npz`` — a 20k-edge slice of config 2 (U=1000, P=100, Zipf posts),
   2-layer HeteroSAGE over engages + rev_engages: outputs, loss, all parameter gradients.
+* ``cfg3_slice_hetero_sage.npz`` — the same slice at d = h = 128 (config 3/4 width).
 """
 from __future__ import annotations
 
@@ -109,6 +110,29 @@ def main():
     for k, v in grads.items():
         arrs["grad:" + k] = v.numpy()
     np.savez_compressed(OUT / "cfg2_slice_hetero_sage.npz", **arrs)
+
+    # ---------------- cfg3 slice: the same 2-layer model at d = h = 128 (BASELINE configs 3-4
+    # width: K=256 projection variants, d=128 gathers, the fused loss at d=128)
+    cfg = synth.scaled("cfg3", 0.001)
+    g = synth.make_graph(cfg)
+    params = sage_ref.init_params(hetero_param_shapes(rels, cfg.dim, cfg.hidden, cfg.layers),
+                                  seed=synth.WEIGHT_SEED)
+    pos = g.edge_index_dict[synth.ENGAGES]
+    neg = synth.negative_posts(g.num_posts, pos.shape[1])
+    pw = synth.interaction_weights(g.num_posts)[pos[1]]
+    fwd = lambda P: sage_ref.hetero_sage(P, g.x_dict, g.edge_index_dict, rels, cfg.layers)
+    out, loss, grads = sage_ref.train_step_grads(params, fwd, pos, neg, pw)
+    ld = dense_ref.link_loss_dense(out["user"], out["post"], pos.numpy(), neg.numpy(), pw.numpy())
+    assert abs(ld - float(loss)) < 1e-5 * max(1.0, abs(ld)), (ld, float(loss))
+    arrs = {"x_user": g.x_dict["user"].numpy(), "x_post": g.x_dict["post"].numpy(),
+            "ei_engages": pos.numpy(), "neg_p": neg.numpy(), "pos_weights": pw.numpy(),
+            "out_user": out["user"].numpy(), "out_post": out["post"].numpy(),
+            "loss": np.array(float(loss), np.float32)}
+    for k, v in params.items():
+        arrs["param:" + k] = v.numpy()
+    for k, v in grads.items():
+        arrs["grad:" + k] = v.numpy()
+    np.savez_compressed(OUT / "cfg3_slice_hetero_sage.npz", **arrs)
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

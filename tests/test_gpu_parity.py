@@ -276,6 +276,52 @@ def test_hetero_sage_two_layer_matches_golden():
         close(p.grad, z["grad:" + name])
 
 
+@pytest.mark.parametrize("fixture,d", [("cfg2_slice_hetero_sage.npz", 64),
+                                       ("cfg3_slice_hetero_sage.npz", 128)])
+def test_hetero_sage_two_layer_fused_loss_matches_golden(fixture, d):
+    """The training step as bench.py runs it — 2-layer model, the fused link loss (scoring pass,
+    negatives sort, score-recomputing dP gather) driving the backward — at d = h = 64 and at the
+    BASELINE cfg3/cfg4 width d = h = 128 (K=256 projection variants, d=128 gathers)."""
+    z = np.load(GOLD / fixture)
+    ei = torch.from_numpy(z["ei_engages"]).to(DEV)
+    e = {synth.ENGAGES: ei, synth.REV_ENGAGES: ei.flip(0)}
+    x = {"user": torch.from_numpy(z["x_user"]).to(DEV), "post": torch.from_numpy(z["x_post"]).to(DEV)}
+    assert x["user"].shape[1] == d
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+    model = HeteroSAGE(d, rels, num_layers=2).to(DEV)
+    model.load_state_dict({k[6:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("param:")})
+    out = model(x, e)
+    close(out["user"], z["out_user"])
+    close(out["post"], z["out_post"])
+    loss = ops.edge_bce_loss(out["user"], out["post"], ei, torch.from_numpy(z["neg_p"]).to(DEV),
+                             torch.from_numpy(z["pos_weights"]).to(DEV))
+    assert abs(float(loss.detach()) - float(z["loss"])) <= RTOL * abs(float(z["loss"]))
+    loss.backward()
+    for name, p in model.named_parameters():
+        close(p.grad, z["grad:" + name])
+
+
+def test_fused_loss_refuses_second_backward():
+    """dU/dP are scaled in place by the upstream gradient, so a retained graph must not be
+    back-propagated twice (it would scale them twice)."""
+    z = np.load(GOLD / "cfg2_slice_hetero_sage.npz")
+    ei = torch.from_numpy(z["ei_engages"]).to(DEV)
+    U = torch.from_numpy(z["out_user"]).to(DEV).requires_grad_()
+    P = torch.from_numpy(z["out_post"]).to(DEV).requires_grad_()
+    loss = ops.edge_bce_loss(U, P, ei, torch.from_numpy(z["neg_p"]).to(DEV),
+                             torch.from_numpy(z["pos_weights"]).to(DEV))
+    (2.0 * loss).backward(retain_graph=True)
+    g1 = U.grad.clone()
+    with pytest.raises(RuntimeError, match="backward ran twice"):
+        loss.backward()
+    U2 = U.detach().clone().requires_grad_()
+    P2 = P.detach().clone().requires_grad_()
+    ref = ops.link_loss(U2, P2, ei, torch.from_numpy(z["neg_p"]).to(DEV),
+                        torch.from_numpy(z["pos_weights"]).to(DEV))
+    (2.0 * ref).backward()
+    close(g1, U2.grad)
+
+
 def test_sage_conv_standalone_and_homogeneous_input():
     rng = np.random.default_rng(1)
     ei = rand_coo(rng, 50, 50, 400)
