@@ -261,6 +261,16 @@ def _pmc_traffic(cfg_name, world, kernel):
     return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_r2.json ({rec.get('source', '')})"
 
 
+def _pmc_ratio(cfg_name, world, kernel):
+    """PMC HBM bytes / algorithmic bytes of ``kernel`` (profiles/pmc_r2.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_r2.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get("launches", {}).get(f"{cfg_name}|n{world}|{kernel}")
+    return rec.get("traffic_over_algorithmic") if rec else None
+
+
 def _workload_config(args, world):
     cfg = synth.CONFIGS[args.config]
     if args.scale != 1.0:
@@ -466,6 +476,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                         "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
                         "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
                                             if v["ms"] else None),
+                        "pmc_traffic_over_algorithmic": _pmc_ratio(cfg.name, world, k),
                         **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
                            if v["flops"] and v["ms"] else {})}
                     for k, v in sorted(kern.items())},
