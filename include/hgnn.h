@@ -117,12 +117,26 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
                     const float* w, int32_t h, const float* bias, int32_t relu, float* out,
                     hgnn_stream_t stream);
 
+/* hgnn_linear_fwd with an additive input: out = act( sum_s xs[s] @ w_s^T + bias + add ), add is
+ * [n_rows, h] (nullable).  The destination update of a relation whose lin_l was applied to the
+ * SOURCE table before the mean gather (mean is linear: lin_l(mean x_j) = mean(lin_l x_j) - 
+ * ops.py "pre-projected relations"): add = the gathered projected rows. */
+int hgnn_linear_fwd_add(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                        const float* w, int32_t h, const float* bias, const float* add,
+                        int32_t relu, float* out, hgnn_stream_t stream);
+
 /* Backward of hgnn_linear_fwd.  dz = dout * (out > 0) when out != NULL (ReLU), else dout.
  *   dxs[s] = dz @ w[:, seg s]           (skipped for NULL entries)
  *   dw     = dz^T @ [xs...]             (NULL: skipped; same for db = colsum(dz))
  * Deterministic (per-block partials reduced in block order).  Workspace:
  * hgnn_linear_bwd_ws_bytes(n_rows, sum(ks), h). */
 size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h);
+/* hgnn_linear_bwd that also writes the masked dz ([n_rows, h], dz_out) — the gradient a
+ * pre-projected relation's K2 scatters (ops.py) — from the pass that masks it anyway. */
+int hgnn_linear_bwd_dz(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                       const float* w, int32_t h, const float* dout, const float* out,
+                       float* const* dxs, float* dw, float* db, float* dz_out, void* ws,
+                       size_t ws_bytes, hgnn_stream_t stream);
 int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,

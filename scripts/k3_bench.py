@@ -29,10 +29,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--dims", default="64,128", help="d = h values to time")
+    ap.add_argument("--shapes", default=None,
+                    help="K:H pairs, e.g. 128:128,256:128 (K = two segments of K/2); "
+                         "overrides --dims")
+    ap.add_argument("--check", action="store_true", help="check outputs against float64 torch")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n = a.rows
-    for d, h in ((64, 64), (128, 128)):
+    shapes = ([tuple(int(v) for v in x.split(":")) for x in a.shapes.split(",")] if a.shapes
+              else [(2 * int(x), int(x)) for x in a.dims.split(",")])
+    for kk, h in shapes:
+        d = kk // 2
         g = torch.Generator(device=dev).manual_seed(0)
         A = torch.randn(n, d, device=dev, generator=g)
         X = torch.randn(n, d, device=dev, generator=g)
@@ -51,6 +59,22 @@ def main():
         t = timeit(lambda: ops.linear_bwd([A, X], W, dout, out, [dA, dX], True, True), a.reps)
         print(f"bwd  K={k} H={h}: {t * 1e3:7.1f} us  {2 * fl / t / 1e9:6.1f} TF/s  "
               f"{4 * n * (2 * h + 2 * k) / t / 1e6:6.0f} GB/s", flush=True)
+        if a.check:
+            ops.linear_bwd([A, X], W, dout, out, [dA, dX], True, True)
+            dz = dout.double() * (out > 0)
+            Xd = torch.cat([A, X], 1).double()
+            dx_ref = dz @ W.double()
+            e1 = float((torch.cat([dA, dX], 1) - dx_ref).abs().max() / dx_ref.abs().max())
+            dw, db = ops.linear_bwd([A, X], W, dout, out, [None, None], True, True)
+            dw_ref = dz.T @ Xd
+            e2 = float((dw - dw_ref).abs().max() / dw_ref.abs().max())
+            print(f"      check: dx rel err {e1:.1e}, dw rel err {e2:.1e}", flush=True)
+        dz = torch.empty_like(out)
+        t = timeit(lambda: ops.linear_bwd([A, X], W, dout, out, [dA, dX], True, True, dz_out=dz),
+                   a.reps)
+        print(f"bwd+dz K={k} H={h}: {t * 1e3:7.1f} us", flush=True)
+        t = timeit(lambda: ops.linear_bwd([A, X], W, dout, out, [dA, dX], False, False), a.reps)
+        print(f"dgrad K={k} H={h}: {t * 1e3:7.1f} us  {fl / t / 1e9:6.1f} TF/s", flush=True)
         t = timeit(lambda: ops.linear_bwd([A, X], W, dout, out, [None, None], True, True), a.reps)
         print(f"wgrad K={k} H={h}: {t * 1e3:7.1f} us  {fl / t / 1e9:6.1f} TF/s  "
               f"{4 * n * (2 * h + k) / t / 1e6:6.0f} GB/s", flush=True)

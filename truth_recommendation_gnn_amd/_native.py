@@ -42,9 +42,13 @@ _SIGS = {
     "hgnn_scatter_mean_bwd": (_c_i32, [_p, _c_i64, _p, _p, _p, _c_i64, _c_i32, _p, _p, _c_i64,
                                        _c_i64, _c_i32, _p, _p, _c_i32, _p]),
     "hgnn_linear_fwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _c_i32, _p, _p]),
+    "hgnn_linear_fwd_add": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _c_i32, _p,
+                                     _p]),
     "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
                                  _c_sz, _p]),
+    "hgnn_linear_bwd_dz": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
+                                    _p, _c_sz, _p]),
     "hgnn_sort_pairs_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
     "hgnn_sort_pairs_i32": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_sort_pairs_i64": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
@@ -161,4 +165,11 @@ def int_array(vals: Sequence[int]):
     arr = (_c_i32 * MAX_SEG)()
     for i, v in enumerate(vals):
         arr[i] = int(v)
+    return arr
+
+
+def float_array(vals: Sequence[float]):
+    arr = (ctypes.c_float * MAX_SEG)()
+    for i, v in enumerate(vals):
+        arr[i] = float(v)
     return arr

@@ -35,6 +35,8 @@ struct LinArgs {
   const float* bias;
   const float* dout;
   const float* out_act;   // ReLU output for the backward mask (nullable)
+  const float* add;       // forward: [n, h] rows added before the activation (nullable)
+  float* dz_out;          // backward: the masked dz written out as well (nullable; dgrad kernels)
   float* out;
   float* slab;            // wgrad partials [gx][h][k_total+1]
   int64_t n;
@@ -663,6 +665,10 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
         float4 v = make_float4(acc[tt][0] + bb.x, acc[tt][1] + bb.y, acc[tt][2] + bb.z,
                                acc[tt][3] + bb.w);
+        if (a.add) {
+          const float4 ad = *reinterpret_cast<const float4*>(a.add + row * H + tt * 16 + 4 * g);
+          v.x += ad.x; v.y += ad.y; v.z += ad.z; v.w += ad.w;
+        }
         if (a.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
@@ -671,6 +677,92 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
     }
 #pragma unroll
     for (int c = 0; c < KC; ++c) av[c] = an[c];
+  }
+}
+
+// Forward v5 (persistent, same tiling and W image as v4), reorganised for 2 waves per SIMD (the
+// K = 256 W image takes 135 KB of LDS, so one 8-wave block per CU):
+//  * k-step-major over the NT accumulators: consecutive MFMAs are independent, so no MFMA waits
+//    on the 40-cycle dependent-accumulator latency (v4's 4-deep chains did, with LDS reads issued
+//    just before their use);
+//  * each W fragment of chunk c+1 is read from LDS right after its last use in chunk c, a whole
+//    k-sweep (NT MFMAs) ahead of its first use;
+//  * the next tile's X chunk c is loaded into av[c] as soon as chunk c has been consumed (no second
+//    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
+//    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
+//    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
+template <int H, int K>
+__global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const ChunkTab tab,
+                                                          int64_t n_tiles) {
+  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
+  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
+  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
+    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
+    *reinterpret_cast<float4*>(ws + j * LDW + k) =
+        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  const int64_t last = a.n - 1;
+  auto src = [&](int64_t t, int c) {
+    const int64_t row = min<int64_t>(t * 16 + i, last);
+    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  float4 av[KC];
+  if (t < n_tiles) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
+  }
+  __syncthreads();
+  const int wl0 = i * LDW + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    // the last tile of a wave re-loads itself (cached, never used) instead of branching
+    const int64_t tn = t + nw < n_tiles ? t + nw : t;
+    int wo = wl0;
+    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
+    const float* wl = ws + wo;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bw[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW);
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].x, av[c].x, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].y, av[c].y, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].z, av[c].z, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        acc[tt] = mfma4(bw[tt].w, av[c].w, acc[tt]);
+        if (c + 1 < KC)
+          bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + (c + 1) * 16);
+      }
+      av[c] = *src(tn, c);
+    }
+    const int64_t row = t * 16 + i;
+    if (row < a.n) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = make_float4(acc[tt][0] + bb.x, acc[tt][1] + bb.y, acc[tt][2] + bb.z,
+                               acc[tt][3] + bb.w);
+        if (a.add) {
+          const float4 ad = *reinterpret_cast<const float4*>(a.add + row * H + tt * 16 + 4 * g);
+          v.x += ad.x; v.y += ad.y; v.z += ad.z; v.w += ad.w;
+        }
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
+      }
+    }
   }
 }
 
@@ -735,6 +827,15 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
     for (int64_t it = 0; it <= n_my; ++it) {
       if (it < n_my) {
         float* dz_w = dzb + (it & 1) * T * LZ + (zrow * 16 + i) * LZ + 4 * g;
+        if (a.dz_out) {
+          const int64_t row = (blockIdx.x + it * gridDim.x) * T + zrow * 16 + i;
+          if (row < a.n) {
+#pragma unroll
+            for (int c = 0; c < HC; ++c)
+              if (c >= zcol0 && c < zcol0 + ZC)
+                *reinterpret_cast<float4*>(a.dz_out + row * H + c * 16 + 4 * g) = zc[c];
+          }
+        }
 #pragma unroll
         for (int c = 0; c < HC; ++c) {
           if (c >= zcol0 && c < zcol0 + ZC) *reinterpret_cast<float4*>(dz_w + c * 16) = zc[c];
@@ -860,6 +961,154 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
   }
 }
 
+// Weight gradient alone, v5: dW = dz^T [X_0 .. X_{S-1}] and db = colsum(dz), dz = dout * [out > 0].
+// Persistent 512-thread blocks; every wave stages a share of each T-row tile (masked dz and X,
+// float4 loads issued one tile ahead into registers) into double-buffered LDS, one barrier per
+// tile, and EVERY wave runs MFMAs on the tile (v4's wgrad-only variant left the four dz-loading
+// waves without MFMA work: one MFMA wave per SIMD).  Wave w owns 2 j-tiles x KW k-tiles of the
+// [H][K] output: per 4-row k-step 2 + KW b32 LDS reads feed 2 KW independent MFMAs.  Row strides
+// H+16 / K+16 keep the b32 reads conflict-free.  The block's partial dW/db goes to its slab
+// (k_wgrad_reduce sums the slabs in block order: deterministic).
+template <int H, int K, int T>
+__global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const ChunkTab tab,
+                                                         int64_t n_tiles) {
+  constexpr int HC = H / 16, KC = K / 16;
+  constexpr int JG = HC / 2;                 // j-tile pairs
+  constexpr int KG = 8 / JG;                 // k groups per j pair (8 waves)
+  constexpr int KW = KC / KG;                // k tiles per wave
+  static_assert(JG * KG == 8 && KW * KG == KC, "wave split");
+  constexpr int LZ = H + 16, LX = K + 16;
+  constexpr int ZQ = T * H / 4 / 512;        // dz float4 per thread per tile
+  constexpr int XQ = T * K / 4 / 512;        // X float4 per thread per tile
+  static_assert(ZQ >= 1 && XQ >= 1, "tile too small for 512 threads");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* dzb = smem;                         // 2 x [T][LZ]
+  float* xsb = dzb + 2 * T * LZ;             // 2 x [T][LX]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int jt0 = 2 * (wave / KG), kt0 = (wave % KG) * KW;
+  // fixed staging columns per thread (H/4 and K/4 divide 512)
+  const int zc4 = threadIdx.x % (H / 4), zr0 = threadIdx.x / (H / 4);
+  constexpr int ZR = 512 / (H / 4);          // rows apart between a thread's dz float4
+  const int xk4 = threadIdx.x % (K / 4), xr0 = threadIdx.x / (K / 4);
+  constexpr int XR = 512 / (K / 4);
+  const int xc = xk4 / 4;
+  const float* xseg = tab.x[xc] + tab.col[xc] + 4 * (xk4 % 4);
+  const int xld = tab.ld[xc];
+  const bool masked = a.out_act != nullptr;
+  const int64_t n_my = (n_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
+  const int64_t last = a.n - 1;
+  float4 zp[ZQ], mp[ZQ], xp[XQ];
+  auto issue = [&](int64_t it) {
+    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
+#pragma unroll
+    for (int q = 0; q < ZQ; ++q) {
+      const int64_t row = min<int64_t>(r0 + zr0 + q * ZR, last);
+      zp[q] = *reinterpret_cast<const float4*>(a.dout + row * H + 4 * zc4);
+      if (masked) mp[q] = *reinterpret_cast<const float4*>(a.out_act + row * H + 4 * zc4);
+    }
+#pragma unroll
+    for (int q = 0; q < XQ; ++q) {
+      const int64_t row = min<int64_t>(r0 + xr0 + q * XR, last);
+      xp[q] = *reinterpret_cast<const float4*>(xseg + row * xld);
+    }
+  };
+  f32x4 acc[2][KW];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < KW; ++k) acc[j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n_my > 0) issue(0);
+  for (int64_t it = 0; it < n_my; ++it) {
+    const int b = it & 1;
+    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
+    float* dz_w = dzb + b * T * LZ;
+    float* xs_w = xsb + b * T * LX;
+#pragma unroll
+    for (int q = 0; q < ZQ; ++q) {
+      const int r = zr0 + q * ZR;
+      float4 v = zp[q];
+      if (masked) {
+        v.x = mp[q].x > 0.f ? v.x : 0.f; v.y = mp[q].y > 0.f ? v.y : 0.f;
+        v.z = mp[q].z > 0.f ? v.z : 0.f; v.w = mp[q].w > 0.f ? v.w : 0.f;
+      }
+      if (r0 + r >= a.n) v = make_float4(0.f, 0.f, 0.f, 0.f);   // clamped rows contribute 0
+      dbacc.x += v.x; dbacc.y += v.y; dbacc.z += v.z; dbacc.w += v.w;
+      *reinterpret_cast<float4*>(dz_w + r * LZ + 4 * zc4) = v;
+    }
+#pragma unroll
+    for (int q = 0; q < XQ; ++q)
+      *reinterpret_cast<float4*>(xs_w + (xr0 + q * XR) * LX + 4 * xk4) = xp[q];
+    if (it + 1 < n_my) issue(it + 1);
+    __syncthreads();
+    const float* dz_r = dz_w + g * LZ + jt0 * 16 + i;
+    const float* xs_r = xs_w + g * LX + kt0 * 16 + i;
+#pragma unroll 4
+    for (int s4 = 0; s4 < T / 4; ++s4) {
+      const float a0 = dz_r[s4 * 4 * LZ], a1 = dz_r[s4 * 4 * LZ + 16];
+#pragma unroll
+      for (int k = 0; k < KW; ++k) {
+        const float bx = xs_r[s4 * 4 * LX + k * 16];
+        acc[0][k] = mfma4(a0, bx, acc[0][k]);
+        acc[1][k] = mfma4(a1, bx, acc[1][k]);
+      }
+    }
+  }
+  constexpr int KEXT = K + 1;
+  float* slab = a.slab + (int64_t)blockIdx.x * H * KEXT;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int k = 0; k < KW; ++k)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        slab[(int64_t)((jt0 + j) * 16 + 4 * g + r) * KEXT + (kt0 + k) * 16 + i] = acc[j][k][r];
+  // db: thread partials (fixed column 4*zc4) reduced through LDS in a fixed order
+  __syncthreads();
+  float4* red = reinterpret_cast<float4*>(smem);
+  red[threadIdx.x] = dbacc;
+  __syncthreads();
+  if (threadIdx.x < H / 4) {
+    float4 t = red[threadIdx.x];
+    for (int m = threadIdx.x + H / 4; m < 512; m += H / 4) {
+      const float4 u = red[m];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const int c = threadIdx.x * 4;
+    slab[(int64_t)(c + 0) * KEXT + K] = t.x;
+    slab[(int64_t)(c + 1) * KEXT + K] = t.y;
+    slab[(int64_t)(c + 2) * KEXT + K] = t.z;
+    slab[(int64_t)(c + 3) * KEXT + K] = t.w;
+  }
+}
+
+// T-row tiles need every one of the 512 threads to stage at least one float4 of dz and of X
+template <int H, int K, int T>
+constexpr bool wgrad5_valid() { return T * H / 4 >= 512 && T * K / 4 >= 512; }
+
+template <int H, int K>
+static void launch_wgrad5(int t, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+                          const LinArgs& a, const ChunkTab& tab, int64_t n_tiles) {
+  if constexpr (wgrad5_valid<H, K, 16>()) {
+    if (t == 16) {
+      hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 16>), grid, block, lds, stream, a, tab, n_tiles);
+      return;
+    }
+  }
+  if constexpr (wgrad5_valid<H, K, 32>()) {
+    if (t == 32) {
+      hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 32>), grid, block, lds, stream, a, tab, n_tiles);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 64>), grid, block, lds, stream, a, tab, n_tiles);
+}
+
+static size_t wgrad5_lds(int h, int k, int t) {
+  return std::max<size_t>(((size_t)2 * t * (h + 16) + (size_t)2 * t * (k + 16)) * 4, 512 * 16);
+}
+
 static size_t v4_bwd_lds(int h, int k, bool dx, int t = 64) {
   return ((dx ? (size_t)k * (h + 8) : 0) + (size_t)2 * t * (h + 16) + (size_t)2 * t * (k + 16)) *
          4;
@@ -910,6 +1159,11 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
     asm volatile("" : "+v"(wo));   // keep W^T fragments as per-tile LDS reads (see fwd v4)
     const float* wt_r = wt + wo;
     const int64_t row = t * 16 + i;
+    if (a.dz_out && row < a.n) {
+#pragma unroll
+      for (int c = 0; c < HC; ++c)
+        *reinterpret_cast<float4*>(a.dz_out + row * H + c * 16 + 4 * g) = zc[c];
+    }
 #pragma unroll
     for (int ct = 0; ct < KC; ct += 2) {
       f32x4 o0 = f32x4{0.f, 0.f, 0.f, 0.f}, o1 = o0;
@@ -940,6 +1194,101 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
 }
 
 static size_t dgrad4_lds(int h, int k) { return (size_t)k * (h + 8) * 4; }
+
+// dgrad v5: v4's tiling and W^T image, reorganised like fwd v5 for 2 waves per SIMD: G column
+// tiles in flight (G independent accumulators, k-step-major), W^T fragments read one k-sweep ahead
+// (across column-group boundaries too), and the next tile's raw dout / out fragments held as
+// loaded — the ReLU mask is applied when the tile becomes current, so no load is waited for at
+// issue.  Rows past the end are clamped (loaded, never stored).
+template <int H, int K>
+__global__ void __launch_bounds__(512, 2) k_linear_dgrad_v5(const LinArgs a, const ChunkTab tab,
+                                                            int64_t n_tiles) {
+  constexpr int HC = H / 16, KC = K / 16, LWT = H + 8;
+  constexpr int G = KC < 8 ? KC : 8, NG = KC / G;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* wt = smem;   // [K][LWT]
+  for (int idx = threadIdx.x; idx < H * K; idx += 512) {
+    const int j = idx / K, k = idx % K;
+    wt[k * LWT + j] = a.w[(int64_t)j * K + k];
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  const int64_t last = a.n - 1;
+  const bool masked = a.out_act != nullptr;
+  float4 zr[HC], mr[HC];
+  auto issue = [&](int64_t t) {
+    const int64_t row = min<int64_t>(t * 16 + i, last);
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      zr[c] = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
+      if (masked) mr[c] = *reinterpret_cast<const float4*>(a.out_act + row * H + c * 16 + 4 * g);
+    }
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  if (t < n_tiles) issue(t);
+  __syncthreads();
+  const int wr0 = i * LWT + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    float4 zc[HC];
+#pragma unroll
+    for (int c = 0; c < HC; ++c) {
+      zc[c] = zr[c];
+      if (masked) {
+        zc[c].x = mr[c].x > 0.f ? zc[c].x : 0.f; zc[c].y = mr[c].y > 0.f ? zc[c].y : 0.f;
+        zc[c].z = mr[c].z > 0.f ? zc[c].z : 0.f; zc[c].w = mr[c].w > 0.f ? zc[c].w : 0.f;
+      }
+    }
+    issue(t + nw < n_tiles ? t + nw : t);
+    int wo = wr0;
+    asm volatile("" : "+v"(wo));   // keep W^T fragments as per-tile LDS reads (see fwd v4)
+    const float* wt_r = wt + wo;
+    const int64_t row = t * 16 + i;
+    if (a.dz_out && row < a.n) {
+#pragma unroll
+      for (int c = 0; c < HC; ++c)
+        *reinterpret_cast<float4*>(a.dz_out + row * H + c * 16 + 4 * g) = zc[c];
+    }
+    float4 bw[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) bw[j] = *reinterpret_cast<const float4*>(wt_r + j * 16 * LWT);
+#pragma unroll
+    for (int gi = 0; gi < NG; ++gi) {
+      f32x4 o[G];
+#pragma unroll
+      for (int j = 0; j < G; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < HC; ++c) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) o[j] = mfma4(bw[j].x, zc[c].x, o[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) o[j] = mfma4(bw[j].y, zc[c].y, o[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) o[j] = mfma4(bw[j].z, zc[c].z, o[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          o[j] = mfma4(bw[j].w, zc[c].w, o[j]);
+          if (c + 1 < HC)
+            bw[j] = *reinterpret_cast<const float4*>(wt_r + (gi * G + j) * 16 * LWT + (c + 1) * 16);
+          else if (gi + 1 < NG)
+            bw[j] = *reinterpret_cast<const float4*>(wt_r + ((gi + 1) * G + j) * 16 * LWT);
+        }
+      }
+      if (row < a.n) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          const int ct = gi * G + j;
+          float* dx = tab.dx[ct];
+          if (dx)
+            *reinterpret_cast<float4*>(dx + row * tab.ld[ct] + tab.col[ct] + 4 * g) =
+                make_float4(o[j][0], o[j][1], o[j][2], o[j][3]);
+        }
+      }
+    }
+  }
+}
+
+
 
 // the persistent forward also takes K = 256 (W: H*(K+8)*4 <= 135 KB of LDS, one block per CU)
 static bool fwd4_ok(const LinArgs& a, bool vec) {
@@ -997,6 +1346,12 @@ extern "C" {
 int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* bias, int32_t relu, float* out,
                     hgnn_stream_t stream_) {
+  return hgnn_linear_fwd_add(n_seg, xs, ks, n_rows, w, h, bias, nullptr, relu, out, stream_);
+}
+
+int hgnn_linear_fwd_add(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                        const float* w, int32_t h, const float* bias, const float* add,
+                        int32_t relu, float* out, hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   LinArgs a{};
   bool vec;
@@ -1004,8 +1359,19 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   if (n_rows == 0) return HGNN_OK;
   if (!out) return fail(HGNN_E_ARG, "linear_fwd: out is null");
   vec = vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
-        reinterpret_cast<uintptr_t>(bias) % 16 == 0;
+        reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&
+        reinterpret_cast<uintptr_t>(add) % 16 == 0;
+  if (add && !fwd4_ok(a, vec)) {
+    // general shapes: the projection (no activation), then act(out + add) in one streaming pass
+    if (int rc = hgnn_linear_fwd_add(n_seg, xs, ks, n_rows, w, h, bias, nullptr, 0, out,
+                                     stream_))
+      return rc;
+    const float* ins[2] = {out, add};
+    const float ws2[2] = {1.f, 1.f};
+    return hgnn_hetero_epilogue(2, ins, ws2, n_rows * h, relu, out, stream_);
+  }
   a.bias = bias;
+  a.add = add;
   a.out = out;
   a.relu = relu;
   const unsigned gx = (unsigned)cdiv(n_rows, kRowsPerBlock);
@@ -1017,8 +1383,15 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
                                                                       256 * per_cu))),
         block(512);
-#define HGNN_FWD4(HV, KV) \
-  hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV>), grid, block, 0, stream, a, tab, n_tiles)
+    // v5 measured faster only at H = K = 128 (2.87 vs 3.24 ms at N = 9M); v4 elsewhere (K = 256:
+    // 5.12 vs 5.45 ms; H = 64, K = 128: 1.61 vs 1.65 ms at N = 1M)
+    static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
+    const int fwd_ver = fwd_env ? fwd_env : (h == 128 && a.k_total == 128 ? 5 : 4);
+#define HGNN_FWD4(HV, KV)                                                                        \
+  if (fwd_ver == 4)                                                                              \
+    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV>), grid, block, 0, stream, a, tab, n_tiles);      \
+  else                                                                                           \
+    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV>), grid, block, 0, stream, a, tab, n_tiles);
     switch (h * 1000 + a.k_total) {
       case 64064: HGNN_FWD4(64, 64); break;
       case 64128: HGNN_FWD4(64, 128); break;
@@ -1077,7 +1450,7 @@ size_t hgnn_linear_bwd_ws_bytes(int64_t n_rows, int32_t k_total, int32_t h) {
   int64_t gx, rpb;
   wgrad_grid(n_rows < 1 ? 1 : n_rows, k_total, h, &gx, &rpb);
   gx = std::max<int64_t>(gx, fast_grid(cdiv(n_rows < 1 ? 1 : n_rows, FT)));
-  gx = std::max<int64_t>(gx, 256);   // persistent v4 backward: at most 256 blocks
+  gx = std::max<int64_t>(gx, 512);   // persistent v4/v5 backward: at most 512 blocks
   return align_up((size_t)gx * h * (k_total + 1) * 4, 256) + 256;
 }
 
@@ -1085,6 +1458,14 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,
                     hgnn_stream_t stream_) {
+  return hgnn_linear_bwd_dz(n_seg, xs, ks, n_rows, w, h, dout, out, dxs, dw, db, nullptr, ws,
+                            ws_bytes, stream_);
+}
+
+int hgnn_linear_bwd_dz(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                       const float* w, int32_t h, const float* dout, const float* out,
+                       float* const* dxs, float* dw, float* db, float* dz_out, void* ws,
+                       size_t ws_bytes, hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   LinArgs a{};
   bool vec;
@@ -1093,7 +1474,8 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   a.dout = dout;
   a.out_act = out;
   vec = vec && reinterpret_cast<uintptr_t>(dout) % 16 == 0 &&
-        (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0);
+        (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+        reinterpret_cast<uintptr_t>(dz_out) % 16 == 0;
   for (int s = 0; s < n_seg; ++s)
     vec = vec && (!a.seg[s].dx || reinterpret_cast<uintptr_t>(a.seg[s].dx) % 16 == 0);
   if (n_rows == 0) {  // no rows: weight grads are zero
@@ -1103,19 +1485,41 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
   }
   bool any_dx = false;
   for (int s = 0; s < n_seg; ++s) any_dx |= a.seg[s].dx != nullptr;
+  if (dz_out && !(fwd4_ok(a, vec) && any_dx)) {
+    // dz written by a streaming pass, then the backward from it with no mask left to apply
+    const float one = 1.f;
+    if (int rc = hgnn_hetero_epilogue_bwd(1, &one, n_rows * h, out ? 1 : 0, out, dout, &dz_out,
+                                          stream_))
+      return rc;
+    return hgnn_linear_bwd_dz(n_seg, xs, ks, n_rows, w, h, dz_out, nullptr, dxs, dw, db,
+                              nullptr, ws, ws_bytes, stream_);
+  }
+  a.dz_out = dz_out;
   if (fwd4_ok(a, vec)) {
     // fused two-role backward when W^T and two dz / X tiles fit the LDS; otherwise persistent
     // dgrad + wgrad-only (T = 32 tiles for K = 256)
     const ChunkTab tab = chunk_table(a);
     const int K = a.k_total;
-    const bool fused = any_dx && (dw || db) && K <= 128 && v4_bwd_lds(h, K, true) <= 160 * 1024;
+    // H = K = 128: persistent dgrad v5 + wgrad v5 (T = 16) beat the fused two-role kernel
+    // (6.21 vs 8.29 ms at N = 9M); H = 64, K = 128: the fused kernel wins (3.18 vs 3.94 ms)
+    static const int split_env =
+        getenv("HGNN_K3_BWD_SPLIT") ? atoi(getenv("HGNN_K3_BWD_SPLIT")) : -1;
+    const bool split = split_env >= 0 ? split_env != 0 : (h == 128 && K == 128);
+    const bool fused = !split && any_dx && (dw || db) && K <= 128 &&
+                       v4_bwd_lds(h, K, true) <= 160 * 1024;
     if (any_dx && !fused) {
       const int64_t n16 = cdiv(n_rows, 16);
       const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
           block(512);
       const size_t lds = dgrad4_lds(h, K);
-#define HGNN_DG4(HV, KV) \
-  hipLaunchKernelGGL((k_linear_dgrad_v4<HV, KV>), grid, block, lds, stream, a, tab, n16)
+      // v5 at H = 128 (K = 256: 5.06 vs 5.70 ms; K = 128: 3.22 vs 3.25 ms at N = 9M)
+      static const int dg_env = getenv("HGNN_K3_DGRAD") ? atoi(getenv("HGNN_K3_DGRAD")) : 0;
+      const int dg_ver = dg_env ? dg_env : (h == 128 ? 5 : 4);
+#define HGNN_DG4(HV, KV)                                                                        \
+  if (dg_ver == 4)                                                                              \
+    hipLaunchKernelGGL((k_linear_dgrad_v4<HV, KV>), grid, block, lds, stream, a, tab, n16);     \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_linear_dgrad_v5<HV, KV>), grid, block, lds, stream, a, tab, n16);
       switch (h * 1000 + K) {
         case 64064: HGNN_DG4(64, 64); break;
         case 64128: HGNN_DG4(64, 128); break;
@@ -1129,6 +1533,42 @@ int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
     }
     if (!(dw || db)) return HGNN_OK;
     if (!ws) return fail(HGNN_E_WS, "linear_bwd: weight gradients need the workspace");
+    if (a.dz_out && !fused) {   // the dgrad kernel wrote the masked dz: wgrad streams it alone
+      a.dout = a.dz_out;
+      a.out_act = nullptr;
+      a.dz_out = nullptr;
+    }
+    // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;
+    // v4 kept elsewhere (K = 256: v5 6.44 / 9.51 ms at T = 16 / 32 vs 5.65; H = 64 needs T >= 32,
+    // which measured slower than v4: 2.44 vs 1.94 ms)
+    static const int wg_env = getenv("HGNN_K3_WGRAD") ? atoi(getenv("HGNN_K3_WGRAD")) : 0;
+    const int wg_ver = wg_env ? wg_env : (h == 128 && K == 128 ? 5 : 4);
+    static const int wg_t = getenv("HGNN_K3_WGRAD_T") ? atoi(getenv("HGNN_K3_WGRAD_T")) : 16;
+    if (!fused && wg_ver == 5 && (h == 64 || h == 128) && (wg_t == 16 || wg_t == 32 || wg_t == 64) &&
+        (int64_t)wg_t * K / 4 >= 512 && (int64_t)wg_t * h / 4 >= 512 &&
+        wgrad5_lds(h, K, wg_t) <= 160 * 1024) {
+      const int64_t n_tiles = cdiv(n_rows, wg_t);
+      const size_t lds = wgrad5_lds(h, K, wg_t);
+      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+      const int G = (int)std::min<int64_t>(n_tiles, 256 * per_cu);
+      const size_t need = (size_t)G * h * (K + 1) * 4;
+      if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+      a.slab = static_cast<float*>(ws);
+      const dim3 grid(G), block(512);
+      switch (h * 1000 + K) {
+        case 64064: launch_wgrad5<64, 64>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+        case 64128: launch_wgrad5<64, 128>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+        case 64256: launch_wgrad5<64, 256>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+        case 128064: launch_wgrad5<128, 64>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+        case 128128: launch_wgrad5<128, 128>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+        default: launch_wgrad5<128, 256>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
+      }
+      if (int rc = check_launch("k_linear_wgrad_v5")) return rc;
+      const int64_t total = (int64_t)h * (K + 1);
+      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
+                         a.slab, (int64_t)G, h, K + 1, dw, db);
+      return check_launch("k_wgrad_reduce");
+    }
     const int T = v4_bwd_lds(h, K, fused, 64) <= 160 * 1024 ? 64 : 32;
     const int64_t n_tiles = cdiv(n_rows, T);
     const int G = (int)std::min<int64_t>(n_tiles, 256);

@@ -204,6 +204,7 @@ class HeteroSAGE(torch.nn.Module):
     def __init__(self, hidden_dim: int, relations: Sequence[Tuple[EdgeType, float]],
                  num_layers: int = 2, in_channels: int = -1):
         super().__init__()
+        self.hidden_dim = hidden_dim
         self.relations = [(tuple(et), float(w)) for et, w in relations]
         self.layers = torch.nn.ModuleList()
         for l in range(num_layers):
@@ -221,7 +222,9 @@ class HeteroSAGE(torch.nn.Module):
                 msgs = [("__".join(et), et, w) for et, w in self.relations if et[2] == dst]
                 rels = tuple((et[0], relation_csr(edge_index_dict[et], h[et[0]].shape[0],
                                                   h[dst].shape[0])) for _, et, _ in msgs)
-                groups.append(ops.DstGroup(dst, rels, True, True))
+                pre = tuple(ops.use_pre_projection(h[et[0]], h[dst], self.hidden_dim, True)
+                            for _, et, _ in msgs)
+                groups.append(ops.DstGroup(dst, rels, True, True, pre))
                 weights.append(_fused_weights(convs, msgs, h))
             out = ops.hetero_layer(ops.LayerSpec(types, tuple(groups)), h, weights)
             for t in h:

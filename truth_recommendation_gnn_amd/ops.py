@@ -99,15 +99,19 @@ def gather_compulsory_bytes(n_edges: int, n_rows: int, n_src: int, d: int, weigh
 
 
 # ----------------------------------------------------------------------------- raw kernel calls
-def gather_mean(x_src: torch.Tensor, csr: RelationCSR) -> torch.Tensor:
-    """K1: ``aggr[i] = mean_{(j->i)} x_src[j]`` (0 for an empty row)."""
+def gather_mean(x_src: torch.Tensor, csr: RelationCSR,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K1: ``aggr[i] = mean_{(j->i)} x_src[j]`` (0 for an empty row); added into ``out`` when
+    given."""
     x_src = _check_f32(x_src, "gather_mean")
     dev = N.require_device(x_src, csr.fwd.rowptr)
     if x_src.shape[0] != csr.n_src:
         raise ValueError(f"x_src has {x_src.shape[0]} rows, relation expects {csr.n_src}")
     d = int(x_src.shape[1])
-    out = torch.empty(csr.n_dst, d, dtype=torch.float32, device=dev)
-    _gather(x_src, csr.fwd, None, csr_mean=True, out=out, accumulate=False)
+    acc = out is not None
+    if out is None:
+        out = torch.empty(csr.n_dst, d, dtype=torch.float32, device=dev)
+    _gather(x_src, csr.fwd, None, csr_mean=True, out=out, accumulate=acc)
     return out
 
 
@@ -191,8 +195,8 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
 
 
 def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.Tensor],
-               relu: bool) -> torch.Tensor:
-    """K3/K4: ``act(sum_s segs[s] @ w[:, seg s]^T + b)``."""
+               relu: bool, add: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K3/K4: ``act(sum_s segs[s] @ w[:, seg s]^T + b (+ add))``."""
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
@@ -202,14 +206,16 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
     out = torch.empty(n, h, dtype=torch.float32, device=dev)
     k = sum(ks)
     with _timed(f"linear_fwd[{n}x{k}->{h}]", 4 * n * (k + h), flops=2 * n * k * h):
-        N.check(N.lib().hgnn_linear_fwd(len(segs), N.ptr_array(segs), N.int_array(ks), n,
-                                        N.ptr(w), h, N.ptr(b), 1 if relu else 0, N.ptr(out),
-                                        N.stream_ptr(dev)), "hgnn_linear_fwd")
+        N.check(N.lib().hgnn_linear_fwd_add(len(segs), N.ptr_array(segs), N.int_array(ks), n,
+                                            N.ptr(w), h, N.ptr(b), N.ptr(add),
+                                            1 if relu else 0, N.ptr(out), N.stream_ptr(dev)),
+                "hgnn_linear_fwd_add")
     return out
 
 
 def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], need_w: bool,
-               need_b: bool):
+               need_b: bool, dz_out: Optional[torch.Tensor] = None):
+    """K3 backward; ``dz_out`` (optional [n, h]) receives the masked dz as well."""
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
@@ -223,10 +229,10 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     nb = 4 * n * (2 * h + sum(ks) + k_dx)
     fl = 2 * n * h * k_dx + (2 * n * sum(ks) * h if need_w else 0)   # dgrad + wgrad
     with _timed(f"linear_bwd[{n}x{sum(ks)}->{h}]", nb, flops=fl):
-        N.check(N.lib().hgnn_linear_bwd(
+        N.check(N.lib().hgnn_linear_bwd_dz(
             len(segs), N.ptr_array(segs), N.int_array(ks), n, N.ptr(w), h, N.ptr(dout),
-            N.ptr(out_act), N.ptr_array(dxs), N.ptr(dw), N.ptr(db), N.ptr(ws),
-            0 if ws is None else ws.numel(), N.stream_ptr(dev)), "hgnn_linear_bwd")
+            N.ptr(out_act), N.ptr_array(dxs), N.ptr(dw), N.ptr(db), N.ptr(dz_out), N.ptr(ws),
+            0 if ws is None else ws.numel(), N.stream_ptr(dev)), "hgnn_linear_bwd_dz")
     return dw, db
 
 
@@ -237,6 +243,33 @@ class DstGroup:
     rels: Tuple[Tuple[str, RelationCSR], ...]   # (source type, relation structure)
     root: bool                                   # x_dst segment present (root_weight)
     relu: bool
+    # per relation: project the SOURCE table first (lin_l(mean x_j) == mean(lin_l x_j), bias
+    # kept in the destination update) — see use_pre_projection
+    pre: Tuple[bool, ...] = ()
+
+
+PRE_PROJECTION = os.environ.get("HGNN_PREPROJECT", "1") == "1"
+
+
+def use_pre_projection(x_src: torch.Tensor, x_dst: torch.Tensor, hidden: int,
+                       root: bool) -> bool:
+    """Whether a relation's lin_l should run on its source table before the mean gather.
+
+    The mean is linear, so ``W (mean_j x_j) = mean_j (W x_j)``: projecting the N_src source rows
+    and gathering the projected rows replaces the [N_dst x d_src] part of the destination
+    projection by an [N_src x d_src] one.  Worth it when the source table is at most half the
+    destination table (cfg4 layer 2: 1M posts -> 9M users halves the user-side K3 flops, forward
+    and backward) and the gathered rows do not widen (d_src >= hidden).  Only where the backward
+    needs the source gradient anyway (``x_src.requires_grad``) or there is no backward: the
+    projection's weight gradient is dP^T x_src with dP = the mean scatter's transpose of dz, a
+    K2 pass the aggregate-first order does not need when x_src is a static input (layer 1).
+    Rounding differs from the reference's order only at the fp32 ulp level.  HGNN_PREPROJECT=0
+    turns it off."""
+    if not (PRE_PROJECTION and root):
+        return False
+    if 2 * x_src.shape[0] > x_dst.shape[0] or x_src.shape[1] < hidden:
+        return False
+    return bool(x_src.requires_grad or not torch.is_grad_enabled())
 
 
 @dataclasses.dataclass(frozen=True)
@@ -294,10 +327,27 @@ class _HeteroLayer(torch.autograd.Function):
         for gi, g in enumerate(spec.groups):   # destination types are independent chains
             w, b = wb[2 * gi], wb[2 * gi + 1]
             with torch.cuda.stream(lanes.stream(gi)):
-                aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
-                segs = aggrs + ([xs[g.dst]] if g.root else [])
-                y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
-                               g.relu)
+                if any(g.pre):
+                    # pre-projected relations: P = x_src W_r^T, gathered (means summed into
+                    # one [N_dst, h] input) and added in the destination update's epilogue
+                    cols = _group_columns(g, xs)
+                    add, aggrs = None, []
+                    for (src, csr), pre, (o, k) in zip(g.rels, g.pre, cols):
+                        if pre:
+                            P = linear_fwd([xs[src]], w[:, o:o + k].contiguous(), None, False)
+                            add = gather_mean(P, csr, out=add)
+                            del P
+                        else:
+                            aggrs.append(gather_mean(xs[src], csr))
+                    segs = aggrs + ([xs[g.dst]] if g.root else [])
+                    y = linear_fwd(segs, _main_weight(g, w, cols),
+                                   None if b is None else b.contiguous(), g.relu, add=add)
+                    del add
+                else:
+                    aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
+                    segs = aggrs + ([xs[g.dst]] if g.root else [])
+                    y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
+                                   g.relu)
             lanes.escape(gi, y, *aggrs)
             outs[gi], aggrs_by_g[gi] = y, aggrs
         lanes.join()
@@ -321,7 +371,7 @@ class _HeteroLayer(torch.autograd.Function):
             if hb:
                 b = saved[pos]; pos += 1
             wbs.append((w, b))
-        aggrs_all = saved[pos:pos + sum(len(g.rels) for g in spec.groups)]
+        aggrs_all = saved[pos:pos + sum(_n_main_rels(g) for g in spec.groups)]
         pos += len(aggrs_all)
         outs = saved[pos:pos + ng]
         need = ctx.needs_input_grad[1:]
@@ -333,13 +383,17 @@ class _HeteroLayer(torch.autograd.Function):
         # allocated here on the main stream
         jobs = []
         ai = 0
+        pre_jobs = []
         for gi, g in enumerate(spec.groups):
-            aggrs = aggrs_all[ai:ai + len(g.rels)]
-            ai += len(g.rels)
+            aggrs = aggrs_all[ai:ai + _n_main_rels(g)]
+            ai += _n_main_rels(g)
             dout = douts[gi]
             w, b = wbs[gi]
             need_w, need_b = need[nt + 2 * gi], (b is not None and need[nt + 2 * gi + 1])
             if dout is None:
+                continue
+            if any(g.pre):
+                pre_jobs.append((gi, g, aggrs, w, dout.contiguous(), need_w, need_b))
                 continue
             dxs: List[Optional[torch.Tensor]] = []
             for (src, csr), a in zip(g.rels, aggrs):
@@ -366,6 +420,12 @@ class _HeteroLayer(torch.autograd.Function):
             lanes.escape(li, dw, db)
             gwb[2 * gi], gwb[2 * gi + 1] = dw, db
         lanes.join()
+        # groups with pre-projected relations (main stream): dz once, the destination update's
+        # backward on it, then per pre-projected relation the K2 of dz into the projected source
+        # rows and the projection's backward
+        for gi, g, aggrs, w, dout, need_w, need_b in pre_jobs:
+            gwb[2 * gi], gwb[2 * gi + 1] = _pre_group_backward(
+                g, xs, aggrs, w, dout, outs[gi], need_x, need_w, need_b, gx, pending)
         # phase 2: K2 per target type (different targets are independent chains)
         for t in pending:
             if gx[t] is None:
@@ -377,6 +437,98 @@ class _HeteroLayer(torch.autograd.Function):
                     scatter_mean_bwd(dA, csr, out=gx[t])
         lanes.join()
         return (None, *[gx[t] for t in spec.types], *gwb)
+
+
+def _group_columns(g: DstGroup, xs) -> List[Tuple[int, int]]:
+    """(offset, width) of each relation's lin_l block in the group's fused weight."""
+    cols, o = [], 0
+    for src, _ in g.rels:
+        k = int(xs[src].shape[1])
+        cols.append((o, k))
+        o += k
+    return cols
+
+
+def _n_main_rels(g: DstGroup) -> int:
+    return sum(1 for i in range(len(g.rels)) if not (g.pre and g.pre[i]))
+
+
+def _main_weight(g: DstGroup, w: torch.Tensor, cols) -> torch.Tensor:
+    """The fused weight without the pre-projected relations' lin_l blocks."""
+    keep = [w[:, o:o + k] for (o, k), pre in zip(cols, g.pre) if not pre]
+    if g.root:
+        keep.append(w[:, cols[-1][0] + cols[-1][1]:] if cols else w)
+    return torch.cat(keep, dim=1).contiguous()
+
+
+def relu_grad(dout: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """dz = dout * (out > 0): ReLU's backward from its output (one streaming pass)."""
+    dz = torch.empty_like(dout)
+    n = dout.numel()
+    with _timed("relu_grad", 12 * n):
+        N.check(N.lib().hgnn_hetero_epilogue_bwd(1, N.float_array([1.0]), n, 1, N.ptr(out),
+                                                 N.ptr(dout), N.ptr_array([dz]),
+                                                 N.stream_ptr(dout.device)),
+                "hgnn_hetero_epilogue_bwd")
+    return dz
+
+
+def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need_b, gx,
+                        pending):
+    """Backward of a destination group with pre-projected relations: returns (dW, db) in the
+    fused weight's column layout; source gradients go to ``gx`` / ``pending`` (K2 list)."""
+    cols = _group_columns(g, xs)
+    # the destination update's backward over the remaining segments also writes the masked dz
+    # that the pre-projected relations' K2 scatters (from the pass that masks it anyway)
+    dz = torch.empty_like(dout) if g.relu else dout
+    segs, seg_cols, dxs = [], [], []
+    ai = 0
+    for (src, csr), pre, c in zip(g.rels, g.pre, cols):
+        if pre:
+            continue
+        a = aggrs[ai]
+        ai += 1
+        segs.append(a)
+        seg_cols.append(c)
+        if need_x[src] and csr.num_edges > 0:
+            dA = torch.empty_like(a)
+            dxs.append(dA)
+            pending.setdefault(src, []).append((dA, csr))
+        else:
+            dxs.append(None)
+    if g.root:
+        segs.append(xs[g.dst])
+        o = cols[-1][0] + cols[-1][1] if cols else 0
+        seg_cols.append((o, int(w.shape[1]) - o))
+        if need_x[g.dst]:
+            d_root = torch.empty_like(xs[g.dst])
+            dxs.append(d_root)
+        else:
+            d_root = None
+            dxs.append(None)
+    dw = torch.empty_like(w) if need_w else None
+    dw_main, db = linear_bwd(segs, _main_weight(g, w, cols), dout, y if g.relu else None, dxs,
+                             need_w, need_b, dz_out=dz if g.relu else None)
+    if dw is not None:
+        o = 0
+        for (co, k) in seg_cols:
+            dw[:, co:co + k].copy_(dw_main[:, o:o + k])
+            o += k
+    if g.root and d_root is not None:
+        gx[g.dst] = d_root if gx[g.dst] is None else gx[g.dst].add_(d_root)
+    # pre-projected relations: dP = K2(dz) over the CSC, then P = x_src W_r^T's backward
+    for (src, csr), pre, (o, k) in zip(g.rels, g.pre, cols):
+        if not pre:
+            continue
+        x_src = xs[src]
+        dP = scatter_mean_bwd(dz, csr)
+        dxp = torch.empty_like(x_src) if need_x[src] else None
+        dwp, _ = linear_bwd([x_src], w[:, o:o + k].contiguous(), dP, None, [dxp], need_w, False)
+        if dw is not None:
+            dw[:, o:o + k].copy_(dwp)
+        if dxp is not None:
+            gx[src] = dxp if gx[src] is None else gx[src].add_(dxp)
+    return dw, db
 
 
 def hetero_layer(spec: LayerSpec, x_dict: Dict[str, torch.Tensor],
