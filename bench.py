@@ -485,14 +485,32 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     }
 
 
-def _roofline(kern, cfg, world):
+def _pool_shapes(kern):
+    """Mini-batch kernels change shape every batch: pool each kernel family over its launches
+    (row counts replaced by '*'; bytes, flops and time summed)."""
+    import re
+    out = {}
+    for k, v in kern.items():
+        key = re.sub(r"(?<=\[)\d+|(?<=<-)\d+", "*", k)
+        a = out.setdefault(key, {"launches": 0, "ms": 0.0, "bytes": 0, "cbytes": 0, "flops": 0})
+        for f in a:
+            a[f] += v[f]
+    return out
+
+
+def _roofline(kern, cfg, world, pooled=False):
     """The dominant HBM kernel: the K1 forward gather over the largest source table (the user
-    table; at N>1 the weighted post partial sums over the rank's own users)."""
+    table; at N>1 the weighted post partial sums over the rank's own users).  ``pooled``: the
+    mini-batch kernels pooled over their shapes — the forward gather family with the most
+    time."""
     fwd = {k: v for k, v in kern.items() if k.startswith(("gather_fwd", "gather_wfwd"))}
     if not fwd:
         return None
-    src_rows = lambda k: int(k.split("<-")[1].split("]")[0])
-    name = max(fwd, key=lambda k: (src_rows(k), fwd[k]["ms"]))
+    if pooled:
+        name = max(fwd, key=lambda k: fwd[k]["ms"])
+    else:
+        src_rows = lambda k: int(k.split("<-")[1].split("]")[0])
+        name = max(fwd, key=lambda k: (src_rows(k), fwd[k]["ms"]))
     r = fwd[name]
     per_launch_ms = r["ms"] / r["launches"]
     per_launch_bytes = r["bytes"] / r["launches"]
@@ -599,6 +617,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         kern = timer.summary()
     if rank != 0:
         return None
+    kern = _pool_shapes(kern)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
@@ -620,7 +639,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    "global_batch": 2 * nb * world,
                    "batches_per_s": round(world * args.steps / elapsed, 1),
                    "parallelism": f"data-parallel x{world}" if world > 1 else "single"},
-        "roofline": _roofline(kern, cfg, world), "projection": _projection(kern),
+        "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),
         "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"],
                         "ms_per_step": round(v["ms"] / args.timer_steps, 4),
