@@ -617,3 +617,62 @@ def test_integration_ctypes_snippet():
                                     n_dst, None, None, 0, 0, 2**30, None, p(aggr), stream) == 0
     close(aggr, sage_ref.mean_aggregate(g.x_dict["post"], g.edge_index_dict[synth.REV_ENGAGES],
                                         n_dst))
+
+
+# ----------------------------------------------------------------------------- pre-projection
+@pytest.mark.parametrize("d", [64, 128])
+def test_pre_projected_relation_matches_aggregate_first(monkeypatch, d):
+    """Layer 2's post -> user relation projected on the (smaller) post table before the gather
+    (ops.use_pre_projection) gives the aggregate-first result: outputs, fused loss and every
+    parameter gradient, against each other and against the CPU oracle."""
+    cfg = synth.dataclasses.replace(synth.scaled("cfg2", 0.002), dim=d, hidden=d)  # U=2000, P=200
+    g = synth.make_graph(cfg)
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+    x = {k: v.to(DEV) for k, v in g.x_dict.items()}
+    e = {k: v.to(DEV) for k, v in g.edge_index_dict.items()}
+    pos = e[synth.ENGAGES]
+    neg = synth.negative_posts(cfg.num_posts, pos.shape[1]).to(DEV)
+    pw = synth.interaction_weights(cfg.num_posts).to(DEV)[pos[1]]
+    torch.manual_seed(0)
+    base = HeteroSAGE(d, rels, num_layers=2, in_channels=d).to(DEV)
+    params = {k: v.detach().clone() for k, v in base.state_dict().items()}
+    res = {}
+    for pre in (False, True):
+        monkeypatch.setattr(ops, "PRE_PROJECTION", pre)
+        model = HeteroSAGE(d, rels, num_layers=2, in_channels=d).to(DEV)
+        model.load_state_dict(params)
+        out = model(x, e)
+        loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw)
+        loss.backward()
+        res[pre] = (out, loss.detach(), {n: p.grad.clone() for n, p in model.named_parameters()})
+    (o0, l0, g0), (o1, l1, g1) = res[False], res[True]
+    for t in ("user", "post"):
+        close(o1[t], o0[t], rtol=1e-5)
+    assert abs(float(l1) - float(l0)) <= 1e-6 * abs(float(l0))
+    for n in g0:
+        close(g1[n], g0[n], rtol=1e-5)
+    # and the oracle (the reference's aggregate-then-project order)
+    P = {k: v.cpu() for k, v in params.items()}
+    ref_out, ref_loss, ref_grads = sage_ref.train_step_grads(
+        P, lambda Q: sage_ref.hetero_sage(Q, g.x_dict, g.edge_index_dict, rels, 2),
+        g.edge_index_dict[synth.ENGAGES], neg.cpu(), pw.cpu())
+    for t in ("user", "post"):
+        close(o1[t], ref_out[t])
+    assert abs(float(l1) - float(ref_loss)) <= RTOL * abs(float(ref_loss))
+    for n, r in ref_grads.items():
+        close(g1[n], r)
+
+
+def test_pre_projection_used_at_layer_two_only():
+    """The rule on the bench's shapes: layer 1's static inputs keep aggregate-first (their
+    projection gradient would need an extra K2 pass); layer 2's post table is projected."""
+    x_post = torch.randn(100, 16, device=DEV)
+    x_user = torch.randn(1000, 16, device=DEV)
+    h_post = x_post.clone().requires_grad_()
+    assert not ops.use_pre_projection(x_post, x_user, 16, True)        # layer 1, training
+    assert ops.use_pre_projection(h_post, x_user, 16, True)            # layer 2
+    assert not ops.use_pre_projection(x_user, x_post, 16, True)        # user -> post: bigger src
+    assert not ops.use_pre_projection(h_post, x_user, 32, True)        # would widen the gather
+    assert not ops.use_pre_projection(h_post, x_user, 16, False)       # no root segment
+    with torch.no_grad():
+        assert ops.use_pre_projection(x_post, x_user, 16, True)        # inference: always
