@@ -14,6 +14,8 @@
 // partial sums go to a slab, then k_fixup adds them in chunk order.
 #include "hgnn_common.h"
 
+#include <stdlib.h>
+
 namespace hgnn {
 
 struct GatherArgs {
@@ -267,7 +269,12 @@ static int dispatch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) 
       return check_launch("k_gather");
     }
     // d = 128 (512-B rows): 8, 12 or 16 rows in flight measured the same on cfg3; 8 kept
-    if (nv <= 32) return launch_gather<32, 1, 4, 4>(a, has_w, stream);
+    if (nv <= 32) {
+      static const int u128 = getenv("HGNN_G128_U") ? atoi(getenv("HGNN_G128_U")) : 4;
+      if (u128 == 8) return launch_gather<32, 1, 4, 8>(a, has_w, stream);
+      if (u128 == 6) return launch_gather<32, 1, 4, 6>(a, has_w, stream);
+      return launch_gather<32, 1, 4, 4>(a, has_w, stream);
+    }
     if (nv <= 64) return launch_gather<64, 1, 4, 4>(a, has_w, stream);
     if (nv <= 128) return launch_gather<64, 2, 4, 2>(a, has_w, stream);
     if (nv <= 256) return launch_gather<64, 4, 4, 2>(a, has_w, stream);
