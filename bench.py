@@ -381,9 +381,13 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
         g = synth.make_graph(cfg, device=dev, device_gen=not on_cpu)
         pos_g = g.edge_index_dict[synth.ENGAGES]
         pw_g = synth.interaction_weights(cfg.num_posts).to(dev)[pos_g[1]]
+        # slice_inputs: every rank keeps the whole static input user table, so layer 1's post
+        # slice mean is computed locally (no partial sums, no reduce-scatter at layer 1)
         shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in rels}, cfg.num_users,
-                                   cfg.num_posts, env, impl=impl, pos_weights=pw_g)
+                                   cfg.num_posts, env, impl=impl, pos_weights=pw_g,
+                                   slice_inputs=True)
         x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
+        x_user_full = g.x_dict["user"]
         x_post = g.x_dict["post"]
         edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
         del g, pos_g, pw_g
@@ -391,7 +395,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
             torch.cuda.empty_cache()
         model = HeteroSAGE(cfg.hidden, rels, num_layers=cfg.layers, in_channels=cfg.dim).to(dev)
         with torch.no_grad():
-            shard.forward(model, x_user, x_post)
+            shard.forward(model, x_user, x_post, x_user_full=x_user_full)
         for p in model.parameters():
             dist.broadcast(p.data, 0)
 
@@ -403,7 +407,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
 
         def loss_fn():
             # the post table's last all-gather stays in flight under the negatives draw + sort
-            h_u, h_p = shard.forward(model, x_user, x_post, wait=False)
+            h_u, h_p = shard.forward(model, x_user, x_post, wait=False, x_user_full=x_user_full)
             return shard.loss(h_u, h_p, negatives(), neg_order="user")
 
     # the reference's optimizer (train_gnn.py:207, Adam lr 0.001); on the GPU torch's fused
@@ -415,7 +419,8 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
         if sharded and not args.autograd_sharded:
             # explicit schedule: each collective issued when its input is complete and waited
             # for by its consumer only (parallel.UserShard.step; same kernels and gradients)
-            loss = shard.step(model, x_user, x_post, negatives(), neg_order="user")
+            loss = shard.step(model, x_user, x_post, negatives(), neg_order="user",
+                              x_user_full=x_user_full)
         else:
             loss = loss_fn()
             loss.backward()

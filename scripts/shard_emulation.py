@@ -51,6 +51,8 @@ def main():
     ap.add_argument("--world", type=int, default=8)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--no-slice-inputs", action="store_true",
+                    help="layer 1's post side through partial sums + reduce-scatter (round 1)")
     ap.add_argument("--strong", action="store_true",
                     help="partition the config's own graph (e.g. cfg4 over 8 ranks), not N x it")
     args = ap.parse_args()
@@ -61,22 +63,24 @@ def main():
     pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
     env = EmulEnv(world=args.world, rank=0)
     shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in RELATIONS},
-                               gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g)
+                               gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g,
+                               slice_inputs=not args.no_slice_inputs)
     x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
+    x_full = None if args.no_slice_inputs else g.x_dict["user"]
     x_post = g.x_dict["post"]
     edges_local = sum(int(r.csr.num_edges) for r in shard.rels.values()) * gcfg.layers
     del g, pos_g, pw_g
     torch.cuda.empty_cache()
     model = HeteroSAGE(gcfg.hidden, RELATIONS, num_layers=gcfg.layers).to(dev)
     with torch.no_grad():
-        shard.forward(model, x_user, x_post)
+        shard.forward(model, x_user, x_post, x_user_full=x_full)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     gen = torch.Generator(device=dev).manual_seed(3)
 
     def step():
         opt.zero_grad(set_to_none=True)
         neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
-        shard.step(model, x_user, x_post, neg, neg_order="user")
+        shard.step(model, x_user, x_post, neg, neg_order="user", x_user_full=x_full)
         opt.step()
 
     for _ in range(3):

@@ -28,7 +28,7 @@ def _maxabs(t):
     return float(t.abs().max()) if t.numel() else 0.0
 
 
-def _worker(rank, world, port, q, kind="engage2"):
+def _worker(rank, world, port, q, kind="engage2", slice_inputs=False):
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
     from dist_torch_impl import TorchImpl
@@ -44,9 +44,11 @@ def _worker(rank, world, port, q, kind="engage2"):
         pw = synth.interaction_weights(cfg.num_posts)[pos[1]]
         model.load_state_dict(params)
         shard = UserShard(edges, cfg.num_users, cfg.num_posts, env, impl=TorchImpl(),
-                          pos_weights=pw)
+                          pos_weights=pw, slice_inputs=slice_inputs)
+        full = g.x_dict["user"] if slice_inputs else None
         lo, hi = user_range(cfg.num_users, world, rank)
-        h_u, h_p = shard.forward(model, g.x_dict["user"][lo:hi], g.x_dict["post"], wait=False)
+        h_u, h_p = shard.forward(model, g.x_dict["user"][lo:hi], g.x_dict["post"], wait=False,
+                                 x_user_full=full)
         loss = shard.loss(h_u, h_p, shard.local_edges_of(neg))
         loss.backward()
         sync_grads(model, env)
@@ -56,7 +58,7 @@ def _worker(rank, world, port, q, kind="engage2"):
         for p in model.parameters():
             p.grad = None
         step_loss = shard.step(model, g.x_dict["user"][lo:hi], g.x_dict["post"],
-                               shard.local_edges_of(neg))
+                               shard.local_edges_of(neg), x_user_full=full)
         sync_grads(model, env)
         step_total = env.all_reduce_(step_loss.clone())
         step_grads = {n: p.grad.clone() for n, p in model.named_parameters()}
@@ -82,15 +84,18 @@ def _worker(rank, world, port, q, kind="engage2"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "engage2"), (3, "engage2"), (2, "rgcn"),
-                                        (3, "rgcn"), (2, "rel4"), (3, "rel4"),
-                                        (4, "rel4"), (3, "tiny_rgcn"), (3, "tiny4"),
-                                        (8, "tiny4")])
-def test_user_sharded_step_matches_single_process_oracle(world, kind):
+@pytest.mark.parametrize("world,kind,slice_inputs", [
+    (2, "engage2", False), (3, "engage2", False), (2, "rgcn", False), (3, "rgcn", False),
+    (2, "rel4", False), (3, "rel4", False), (4, "rel4", False), (3, "tiny_rgcn", False),
+    (3, "tiny4", False), (8, "tiny4", False),
+    # layer 1's post slice from the whole static user table (no reduce-scatter at layer 1)
+    (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True)])
+def test_user_sharded_step_matches_single_process_oracle(world, kind, slice_inputs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind, slice_inputs))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]

@@ -394,6 +394,10 @@ class _Rel:
     csr: object
     w_fwd: Optional[torch.Tensor] = None
     w_bwd: Optional[torch.Tensor] = None
+    # user->post only, with ``UserShard(slice_inputs=True)``: every edge INTO the owned post slice
+    # (global user ids).  Layer 1 reads the static input user table, which each rank can hold
+    # whole: the slice's mean is then computed locally, with no partial sums to reduce-scatter.
+    slice_csr: object = None
 
 
 @dataclasses.dataclass
@@ -429,9 +433,10 @@ class UserShard:
     """
 
     def __init__(self, edges, n_users: int, n_posts: int, env: DistEnv, impl=None,
-                 pos_weights: Optional[torch.Tensor] = None):
+                 pos_weights: Optional[torch.Tensor] = None, slice_inputs: bool = False):
         impl = impl or HipImpl()
         self.env, self.impl = env, impl
+        self.slice_inputs = slice_inputs
         if torch.is_tensor(edges):
             edges = {ENGAGES: edges, REV_ENGAGES: edges.flip(0)}
         self.n_users, self.n_posts = n_users, n_posts
@@ -502,7 +507,13 @@ class UserShard:
             rel = impl.relation(local, self.n_own, self.n_posts_pad)
             if et == ENGAGES:
                 self.mask, self.pos_local = m, local
-            return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv))
+            slice_rel = None
+            if self.slice_inputs:
+                ms = (dst >= self.p_lo) & (dst < self.p_hi)
+                sl = torch.stack([src[ms], dst[ms] - self.p_lo]).contiguous()
+                slice_rel = impl.relation(sl, self.n_users, self.post_rows)
+            return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv),
+                        slice_rel)
         # post -> post: edges into the owned slice of the post table
         m = (dst >= self.p_lo) & (dst < self.p_hi)
         local = torch.stack([src[m], dst[m] - self.p_lo]).contiguous()
@@ -541,11 +552,13 @@ class UserShard:
         return recv, pend
 
     def forward(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor,
-                wait: bool = True):
+                wait: bool = True, x_user_full: Optional[torch.Tensor] = None):
         """Partitioned forward of ``model`` (``HeteroSAGE`` or a ``WeightedRGCN`` layout);
         returns (owned user embeddings, post embeddings of the whole padded table — rows >=
         n_posts are padding).  ``wait=False`` leaves the last all-gather of the post table in
-        flight for :meth:`loss`, which waits on it only after enqueueing the negatives sort."""
+        flight for :meth:`loss`, which waits on it only after enqueueing the negatives sort.
+        ``x_user_full`` (the whole input user table, with ``slice_inputs=True``): layer 1's
+        user->post means of the owned post slice are computed locally (no reduce-scatter)."""
         impl, env = self.impl, self.env
         if x_post.shape[0] != self.n_posts_pad:
             x_post = torch.nn.functional.pad(x_post, (0, 0, 0, self.n_posts_pad - x_post.shape[0]))
@@ -569,6 +582,9 @@ class UserShard:
             for _, et, _ in pmsgs:
                 r = self.rels[et]
                 if r.kind[0] == "user":
+                    if li == 0 and x_user_full is not None and r.slice_csr is not None:
+                        a_post[et] = (impl.mean_gather(x_user_full, r.slice_csr), Pending())
+                        continue
                     s = impl.weighted_gather(h_u, r.csr, r.w_fwd, r.w_bwd)
                     pend = Pending()
                     a_post[et] = ((_ReduceScatter.apply(s, env, pend, defer), pend)
@@ -618,7 +634,8 @@ class UserShard:
         return h_u, h_p
 
     def step(self, model, x_user_own: torch.Tensor, x_post: torch.Tensor,
-             neg_local: torch.Tensor, neg_order: str = "edge") -> torch.Tensor:
+             neg_local: torch.Tensor, neg_order: str = "edge",
+             x_user_full: Optional[torch.Tensor] = None) -> torch.Tensor:
         """One training step's forward, loss and backward for this rank, with an explicit
         schedule instead of autograd's: the same kernels, and the parameter gradients
         ``forward`` + ``loss`` + ``backward()`` give (accumulated into ``.grad``); returns the
@@ -637,7 +654,7 @@ class UserShard:
         if self.cscale is None:
             raise ValueError("UserShard built without pos_weights")
         with torch.no_grad():
-            return _step(self, model, x_user_own, x_post, neg_local, neg_order)
+            return _step(self, model, x_user_own, x_post, neg_local, neg_order, x_user_full)
 
     def loss(self, h_u_own, h_p, neg_local, neg_order="edge"):
         """This rank's additive share of the reference loss."""
@@ -659,7 +676,7 @@ def _k2_into(impl, buf, g, csr):
     return buf
 
 
-def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
+def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x_user_full=None):
     """UserShard.step: forward, loss and backward with every collective issued as early as its
     input exists and waited as late as its consumer allows (see the method docstring)."""
     impl, env = shard.impl, shard.env
@@ -691,6 +708,10 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order):
         for _, et, _ in pm:
             r = shard.rels[et]
             if r.kind[0] == "user":
+                if li == 0 and x_user_full is not None and r.slice_csr is not None:
+                    # static inputs held whole: the owned slice's mean, no partial sums to reduce
+                    rs[et] = (impl.gather_mean_raw(x_user_full, r.slice_csr), _Done())
+                    continue
                 part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd)
                 rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
         if ag is not None:                      # F3 the previous layer's post table
