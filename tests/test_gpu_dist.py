@@ -98,7 +98,8 @@ def _case_worker(rank, world, port, q, kind, slice_inputs=False):
         model = model.to(dev)
         env = parallel.DistEnv.from_torch()
         env.side_adjoint = True      # the RCCL-path adjoints (side stream + deferred hand-off)
-        ed = {k: v.to(dev) for k, v in edges.items()}
+        # a case's edges: the engages tensor alone ("engage2") or an edge_index_dict
+        ed = edges.to(dev) if torch.is_tensor(edges) else {k: v.to(dev) for k, v in edges.items()}
         shard = parallel.UserShard(ed, cfg.num_users, cfg.num_posts, env,
                                    pos_weights=pw.to(dev), slice_inputs=slice_inputs)
         full = g.x_dict["user"].to(dev) if slice_inputs else None
