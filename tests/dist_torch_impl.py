@@ -35,8 +35,10 @@ class TorchImpl:
         return out.index_add(0, ei[1], x[ei[0]] * w_fwd[:, None])
 
     @staticmethod
-    def fused_linear(segs, w, b, relu):
+    def fused_linear(segs, w, b, relu, add=None):
         y = F.linear(torch.cat(segs, 1), w, b)
+        if add is not None:
+            y = y + add
         return F.relu(y) if relu else y
 
     @staticmethod
@@ -75,8 +77,10 @@ class TorchImpl:
     linear_fwd_raw = fused_linear
 
     @staticmethod
-    def linear_bwd_raw(segs, w, dout, out_act, dxs, need_w, need_b):
+    def linear_bwd_raw(segs, w, dout, out_act, dxs, need_w, need_b, dz_out=None):
         dz = dout * (out_act > 0) if out_act is not None else dout
+        if dz_out is not None:
+            dz_out.copy_(dz)
         x = torch.cat(segs, 1)
         dx = dz @ w
         o = 0

@@ -74,6 +74,7 @@ def _worker(rank, world, port, q, kind="engage2", slice_inputs=False):
                "step_grad_err": max(float((step_grads[n] - ref_grads[n]).abs().max()) /
                                     max(float(ref_grads[n].abs().max()), 1e-12)
                                     for n in step_grads),
+               "pre_layers": shard.pre_layers,
                "n_local": int(shard.pos_local.shape[1]), "n_total": int(pos.shape[1]),
                "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
         q.put(res)
@@ -89,7 +90,8 @@ def _worker(rank, world, port, q, kind="engage2", slice_inputs=False):
     (2, "rel4", False), (3, "rel4", False), (4, "rel4", False), (3, "tiny_rgcn", False),
     (3, "tiny4", False), (8, "tiny4", False),
     # layer 1's post slice from the whole static user table (no reduce-scatter at layer 1)
-    (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True)])
+    (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True), (2, "engage3", True),
+    (3, "soc2", True), (1, "engage2", True)])
 def test_user_sharded_step_matches_single_process_oracle(world, kind, slice_inputs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -107,7 +109,10 @@ def test_user_sharded_step_matches_single_process_oracle(world, kind, slice_inpu
     assert sum(r["n_local"] for r in res) == res[0]["n_total"]
     if kind in ("rgcn", "rel4"):     # the social relation really crosses ranks
         assert all(r["n_halo"] > 0 for r in res), res
+    # UserShard.step's sliced pre-projection of the post -> user relation (parallel._pre_rel)
+    want_pre = {"engage2": [1], "engage3": [1, 2], "soc2": [1]}.get(kind, [])
     for r in res:
+        assert r["pre_layers"] == want_pre, r
         assert r["loss_err"] < 1e-5, r
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
         assert r["grad_err"] < 1e-4, r

@@ -133,7 +133,8 @@ def _case_worker(rank, world, port, q, kind, slice_inputs=False):
                                  / out["post"].abs().max()),
                "grad_err": max(float((grads[n] - ref_grads[n]).abs().max()) /
                                max(float(ref_grads[n].abs().max()), 1e-12) for n in grads),
-               "n_halo": shard.halo.n_halo if shard.halo is not None else 0}
+               "n_halo": shard.halo.n_halo if shard.halo is not None else 0,
+               "pre_layers": shard.pre_layers}
         q.put(res)
     except Exception as e:   # surface worker failures in the parent
         q.put({"rank": rank, "error": repr(e)})
@@ -144,7 +145,8 @@ def _case_worker(rank, world, port, q, kind, slice_inputs=False):
 
 @pytest.mark.parametrize("world,kind,slice_inputs", [
     (2, "rgcn", False), (3, "rel4", False), (3, "tiny_rgcn", False), (3, "tiny4", False),
-    (8, "tiny4", False), (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True)])
+    (8, "tiny4", False), (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True),
+    (2, "engage3", True), (3, "soc2", True)])
 def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind, slice_inputs):
     """The reference WeightedRGCN (social relation through the halo all-to-all) and the
     4-relation cfg5 graph on the HIP kernels, world 2/3 on one device (gloo over device
@@ -165,7 +167,9 @@ def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind, slice_i
         p.join(timeout=120)
     errs = [r["error"] for r in res if "error" in r]
     assert not errs, errs
+    want_pre = {"engage2": [1], "engage3": [1, 2], "soc2": [1]}.get(kind, [])
     for r in res:
+        assert r["pre_layers"] == want_pre, r      # parallel._pre_rel on the HIP kernels
         if kind in ("rgcn", "rel4"):
             assert r["n_halo"] > 0, r
         assert r["loss_err"] < 1e-4, r

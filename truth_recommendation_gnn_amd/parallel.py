@@ -676,6 +676,55 @@ def _k2_into(impl, buf, g, csr):
     return buf
 
 
+def _pre_rel(shard: "UserShard", layers, li: int) -> Optional[int]:
+    """Index (into layer ``li``'s user-side relations) of the post -> user relation whose lin_l
+    runs on the post SLICE before the previous layer's all-gather, or None.
+
+    ``W (mean_j x_j) = mean_j (W x_j)`` (``ops.use_pre_projection``): each rank projects its
+    S = n_posts / world slice rows (y_p_own W_l^T, S x H), the all-gather carries the projected
+    rows instead of y_p, and the user-side update loses its [n_own x d] lin_l block — K = 2d ->
+    d for the forward, and the backward's dgrad of that block (the relation's K2 scatters the
+    masked dz itself).  The adjoint: the reduce-scatter brings the slice's dP, whose projection
+    backward (S rows) gives d y_p_own and the block's weight gradient.  Applies when the
+    all-gathered table has no other reader: layer li > 0 (layer 0 reads the static inputs), a
+    post side in layers li-1 and li (li's post table is not passed through), exactly one
+    post -> user relation and no post -> post relation at layer li.  ``HGNN_PREPROJECT=0``
+    turns it off (``ops.PRE_PROJECTION``)."""
+    if li == 0 or not ops.PRE_PROJECTION or not getattr(shard.impl, "pre_projection", True):
+        return None
+    _, prev_layout = layers[li - 1]
+    _, layout = layers[li]
+    um, pm = layout.get("user", []), layout.get("post", [])
+    if not prev_layout.get("post") or not pm:
+        return None
+    if any(shard.rels[et].kind[0] == "post" for _, et, _ in pm):
+        return None
+    js = [j for j, (_, et, _) in enumerate(um) if shard.rels[et].kind[0] == "post"]
+    return js[0] if len(js) == 1 else None
+
+
+def _block_cols(um, widths: Dict[str, int]) -> List[Tuple[int, int]]:
+    """(offset, width) of each user-side relation's lin_l block in the fused weight
+    ``[w_1 W_l,1 | ... | w_R W_l,R | root]`` (``nn._fused_weights``)."""
+    cols, o = [], 0
+    for _, et, _ in um:
+        k = widths[et[0]]
+        cols.append((o, k))
+        o += k
+    return cols
+
+
+def _without_block(W: torch.Tensor, col: Tuple[int, int]) -> torch.Tensor:
+    o, k = col
+    return torch.cat([W[:, :o], W[:, o + k:]], dim=1).contiguous()
+
+
+def _lin_fwd(impl, segs, W, b, add):
+    if add is None:
+        return impl.linear_fwd_raw(segs, W, b, True)
+    return impl.linear_fwd_raw(segs, W, b, True, add=add)
+
+
 def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x_user_full=None):
     """UserShard.step: forward, loss and backward with every collective issued as early as its
     input exists and waited as late as its consumer allows (see the method docstring)."""
@@ -684,20 +733,35 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
     if x_post.shape[0] != shard.n_posts_pad:
         x_post = torch.nn.functional.pad(x_post, (0, 0, 0, shard.n_posts_pad - x_post.shape[0]))
     layers = model_layers(model)
+    L = len(layers)
     for convs, _ in layers:
         if any(c.lin_r is None for c in convs.values()):
             raise NotImplementedError("UserShard.step expects SAGEConv(root_weight=True) layers")
+    pre = [_pre_rel(shard, layers, li) for li in range(L)]
+    fused: Dict[int, tuple] = {}
+
+    def weights_of(li, shapes):
+        if li not in fused:
+            convs, layout = layers[li]
+            um, pm = layout.get("user", []), layout.get("post", [])
+            fused[li] = (_fused_weights(convs, um, shapes) if um else (None, None),
+                         _fused_weights(convs, pm, shapes) if pm else (None, None))
+        return fused[li]
+
     h_u, h_p, h_p_own = x_user_own, x_post, x_post[shard.p_lo:shard.p_hi]
     ag = None                                   # in-flight all-gather of h_p
+    proj = [None] * L                           # layer li's pre-projection: (block, cols)
     saved = []
     for li, (convs, layout) in enumerate(layers):
         um, pm = layout.get("user", []), layout.get("post", [])
         for _, et, _ in um + pm:
             if et not in shard.rels:
                 raise KeyError(f"relation {et} is not in the sharded graph")
-        shapes = {"user": h_u, "post": h_p}
-        Wu, bu = _fused_weights(convs, um, shapes) if um else (None, None)
-        Wp, bp = _fused_weights(convs, pm, shapes) if pm else (None, None)
+        # h_p is None when this layer reads the projected table (pre[li]); the slice has its width
+        shapes = {"user": h_u, "post": h_p_own}
+        (Wu, bu), (Wp, bp) = weights_of(li, shapes)
+        jp = pre[li] if proj[li] is not None else None
+        col_pre = proj[li][1] if jp is not None else None
         # F1 halo rows out; F2 post partial sums -> reduce-scatter (both in flight from here)
         halo, halo_w = None, _Done()
         if multi and shard.halo is not None and any(et[0] == "user" for _, et, _ in um):
@@ -717,23 +781,27 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         if ag is not None:                      # F3 the previous layer's post table
             ag.wait()
             ag = None
-        # F4 user side
-        a_u, x_ext = [], None
-        for _, et, _ in um:
+        # F4 user side (a pre-projected relation's mean of projected rows enters the epilogue)
+        a_u, x_ext, add = [], None, None
+        for j, (_, et, _) in enumerate(um):
             r = shard.rels[et]
-            if r.kind[0] == "post":
+            if j == jp:
+                add = impl.gather_mean_raw(h_p, r.csr)
+            elif r.kind[0] == "post":
                 a_u.append(impl.gather_mean_raw(h_p, r.csr))
             else:
                 if x_ext is None:
                     halo_w.wait()
                     x_ext = h_u if halo is None else torch.cat([h_u, halo])
                 a_u.append(impl.gather_mean_raw(x_ext, r.csr))
+        Wu_main = _without_block(Wu, col_pre) if jp is not None else Wu
         # the last layer's user projection waits until the post table's all-gather is issued: the
         # loss needs that table at once, so the projection and the negatives sort both run under
         # the collective (the reduce-scatter still has the user-side gathers under it)
-        late_u = multi and bool(pm) and bool(um) and li == len(layers) - 1
-        y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True) if um and not late_u else h_u
-        # F5 post side on the owned slice, then its all-gather
+        late_u = multi and bool(pm) and bool(um) and li == L - 1
+        y_u = _lin_fwd(impl, a_u + [h_u], Wu_main, bu, add) if um and not late_u else h_u
+        # F5 post side on the owned slice, then its all-gather (of the next layer's projected
+        # rows when that layer pre-projects)
         a_p = []
         for _, et, _ in pm:
             r = shard.rels[et]
@@ -745,33 +813,56 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                 a_p.append(a)
         if pm:
             y_p_own = impl.linear_fwd_raw(a_p + [h_p_own], Wp, bp, True)
-            y_p, ag = env.all_gather_async(y_p_own) if multi else (y_p_own, None)
+            table = y_p_own
+            nxt = li + 1
+            if nxt < L and pre[nxt] is not None:
+                (Wu_n, _), _ = weights_of(nxt, {"user": y_u, "post": y_p_own})
+                um_n = layers[nxt][1]["user"]
+                cols = _block_cols(um_n, {"user": int(y_u.shape[1]),
+                                                 "post": int(y_p_own.shape[1])})
+                o, k = cols[pre[nxt]]
+                if k >= Wu_n.shape[0]:          # the projected rows are no wider than y_p
+                    block = Wu_n[:, o:o + k].contiguous()
+                    table = impl.linear_fwd_raw([y_p_own], block, None, False)
+                    proj[nxt] = (block, (o, k))
+            y_p, ag = env.all_gather_async(table) if multi else (table, None)
         else:
             y_p_own, y_p = h_p_own, h_p
         if late_u:
-            y_u = impl.linear_fwd_raw(a_u + [h_u], Wu, bu, True)
-        saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu, Wp,
-                      bu is not None, bp is not None))
+            y_u = _lin_fwd(impl, a_u + [h_u], Wu_main, bu, add)
+        saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu_main,
+                      Wp, bu is not None, bp is not None, jp, col_pre))
         h_u, h_p, h_p_own = y_u, y_p, y_p_own
+    shard.pre_layers = [li for li in range(L) if proj[li] is not None]   # (for tests)
     # loss: the negatives sort runs while the last all-gather lands
     loss, G_u, G_full = impl.edge_bce_loss_raw(h_u, h_p, shard.pos_local, neg_local,
                                                shard.num_edges_global, shard.cscale, neg_order,
                                                ag.wait if ag is not None else None)
     G_own = None
     R = None                                    # reduce-scatter of G_full, once issued
-    for li in reversed(range(len(layers))):
-        (convs, um, pm, hu, hp, hpo, x_ext, a_u, a_p, yu, ypo, Wu, Wp, has_bu, has_bp) = saved[li]
+    R_proj = None                               # (block, cols, grads to finish) if R carries dP
+    for li in reversed(range(L)):
+        (convs, um, pm, hu, hp, hpo, x_ext, a_u, a_p, yu, ypo, Wu, Wp, has_bu, has_bp, jp,
+         col_pre) = saved[li]
         need_x = li > 0                         # layer 0's inputs are the (fixed) features
         if pm and R is None:                    # B1 adjoint of the post-table all-gather
-            g = G_full if G_full is not None else torch.zeros_like(hp)
+            g = G_full if G_full is not None else ypo.new_zeros(shard.n_posts_pad, ypo.shape[1])
             R = env.reduce_scatter_async(g) if multi else (g, _Done())
-        # B2a user-side projection backward
-        dxu = []
+        # B2a user-side projection backward (a pre-projected relation: dz as a side output)
+        dxu, dz = [], None
+        pending_w = None
         if um:
             dxu = [torch.empty_like(a) if need_x else None for a in a_u]
             dxu.append(torch.empty_like(hu) if need_x else None)
-            dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True, has_bu)
-            _grads_to_params(convs, um, dW, db)
+            if jp is not None:
+                dz = torch.empty_like(G_u)
+                dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True,
+                                             has_bu, dz_out=dz)
+                pending_w = (convs, um, dW, db, col_pre)  # the block's gradient comes with dP
+            else:
+                dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True,
+                                             has_bu)
+                _grads_to_params(convs, um, dW, db)
             d_hu = dxu[-1]
         else:
             d_hu = G_u if need_x else None
@@ -782,6 +873,17 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             r_slice, r_w = R
             r_w.wait()
             R = None
+            if R_proj is not None:
+                # the reduce-scatter brought the next layer's dP slice: the projection's backward
+                # (S rows) gives this layer's output-slice gradient and the block's gradient
+                block, (o, k), (n_convs, n_um, n_dW, n_db, _) = R_proj
+                R_proj = None
+                g_y = torch.empty_like(ypo)
+                dblock, _ = impl.linear_bwd_raw([ypo], block, r_slice.contiguous(), None, [g_y],
+                                                True, False)
+                dW_full = torch.cat([n_dW[:, :o], dblock, n_dW[:, o:]], dim=1)
+                _grads_to_params(n_convs, n_um, dW_full, n_db)
+                r_slice = g_y
             g_slice = r_slice if G_own is None else r_slice + G_own
             dxp = [torch.empty_like(a) if need_x else None for a in a_p]
             dxp.append(torch.empty_like(hpo) if need_x else None)
@@ -796,16 +898,22 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         for j, (_, et, _) in enumerate(pm):
             if shard.rels[et].kind[0] == "user":
                 gath[et] = env.all_gather_async(dxp[j]) if multi else (dxp[j], _Done())
-        # B2b gradients into the previous layer's post table and the halo (a layer without a
-        # post side passes the table through: its gradient flows on unchanged)
+        # B2b gradients into the previous layer's post table (of its projected rows when this
+        # layer pre-projects: the K2 of dz) and the halo (a layer without a post side passes the
+        # table through: its gradient flows on unchanged)
         G_prev = None if pm else G_full
         d_xext = None
+        ai = 0
         for j, (_, et, _) in enumerate(um):
             r = shard.rels[et]
+            if j == jp:
+                G_prev = _k2_into(impl, G_prev, dz, r.csr)
+                continue
             if r.kind[0] == "post":
-                G_prev = _k2_into(impl, G_prev, dxu[j], r.csr)
+                G_prev = _k2_into(impl, G_prev, dxu[ai], r.csr)
             else:
-                d_xext = _k2_into(impl, d_xext, dxu[j], r.csr)
+                d_xext = _k2_into(impl, d_xext, dxu[ai], r.csr)
+            ai += 1
         for j, (_, et, _) in enumerate(pm):
             r = shard.rels[et]
             if r.kind[0] == "post":
@@ -823,8 +931,10 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         # the previous layer's post-table gradient is complete: its reduce-scatter starts now
         prev_pm = saved[li - 1][2]
         if prev_pm:
-            g = G_prev if G_prev is not None else torch.zeros_like(hp)
+            g = G_prev if G_prev is not None else hpo.new_zeros(shard.n_posts_pad, hpo.shape[1])
             R = env.reduce_scatter_async(g) if multi else (g, _Done())
+            if jp is not None:
+                R_proj = (proj[li][0], col_pre, pending_w)
         # B5 user rows' share of the post partial sums, then the halo rows' gradients
         for et, (full, w) in gath.items():
             w.wait()
