@@ -370,7 +370,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
 
         def loss_fn():
             out = model(g.x_dict, g.edge_index_dict)
-            neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
+            neg = ops.draw_negatives(pos, cfg.num_posts, generator=gen)
             return ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
                                      check=False, cscale=cscale)
     else:
@@ -403,7 +403,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
             if on_cpu:
                 return torch.randint(0, cfg.num_posts, (shard.pos_local.shape[1],),
                                      generator=gen, device=dev)
-            return ops.sample_negatives(shard.pos_local, cfg.num_posts, generator=gen)
+            return ops.draw_negatives(shard.pos_local, cfg.num_posts, generator=gen)
 
         def loss_fn():
             # the post table's last all-gather stays in flight under the negatives draw + sort

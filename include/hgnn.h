@@ -70,6 +70,16 @@ int hgnn_sort_pairs_i64(const int64_t* keys, const int32_t* a, const int32_t* b,
                         int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
                         int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* The loss's negatives drawn and grouped in one call: exactly hgnn_uniform_i32(d_seed, E, n_keys,
+ * neg_out) followed by hgnn_sort_pairs_i32(neg_out, a, NULL, E, n_keys, rowptr, a_sorted, NULL,
+ * NULL, ...), with the draws computed inside the sort's first pass instead of being written and
+ * read back (neg_out, E int32 in position order, may be NULL).  Replaces the reference's
+ * torch.randint negatives (train_gnn.py:272) plus the grouping the fused dP gather needs.
+ * Workspace: hgnn_sort_pairs_ws_bytes(E, n_keys). */
+int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E, int64_t n_keys,
+                             int32_t* neg_out, int32_t* rowptr, int32_t* a_sorted, void* ws,
+                             size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- degree-skew plan ----------------------------------------------------------------------
  * Rows with more than `chunk` edges are split into ceil(deg/chunk) chunks, each summed by its own
  * wave into a partial slot, then reduced in chunk order (deterministic).  Two phases so the host

@@ -1,8 +1,17 @@
 #!/bin/bash
-# Quick GPU pass: selected tests (-k expr in $1), then bench at N=1 (extra args after $1).
+# Targeted GPU tests (-k expression in $K) then the default bench (cfg4), no CPU baseline.
+# usage: K="expr" [TESTS="tests/x.py ..."] bash scripts/gpu_quick.sh [bench args...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-K="$1"; shift
-timeout -k 10 400 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests -m gpu -k "$K" > gpurun_out/quick_tests.log 2>&1; rc=$?; tail -4 gpurun_out/quick_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > gpurun_out/quick_bench.log 2>&1; rc=$?; tail -1 gpurun_out/quick_bench.log | head -c 700; echo; exit $rc
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread -k "$K" > gpurun_out/gpu_quick_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/gpu_quick_tests.log | tail -8; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --no-cpu-baseline "$@" > gpurun_out/bench_quick.log 2>&1
+rc=$?; echo "bench rc=$rc"; python - <<'PY'
+import json
+for l in open("gpurun_out/bench_quick.log"):
+    if l.startswith("{"):
+        d = json.loads(l)
+        print(d["value"], d["ms_per_step"], {k: v["ms_per_step"] for k, v in d["kernels"].items()})
+PY
+exit $rc

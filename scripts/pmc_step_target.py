@@ -32,7 +32,7 @@ gen = torch.Generator(device=dev).manual_seed(synth.NEG_SEED)
 def step():
     opt.zero_grad(set_to_none=True)
     out = model(g.x_dict, e)
-    neg = ops.sample_negatives(pos, cfg.num_posts, generator=gen)
+    neg = ops.draw_negatives(pos, cfg.num_posts, generator=gen)
     loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw, neg_order="user",
                              check=False, cscale=cscale)
     loss.backward()

@@ -461,6 +461,74 @@ def test_sample_negatives_uniform_and_seeded():
     assert abs(float(lag.mean())) / (1000 ** 2 / 12) < 0.01
 
 
+@pytest.mark.parametrize("E,n_keys", [(0, 7), (1, 1), (1000, 1), (5000, 37),
+                                      (300_000, 100_000), (2_000_000, 1_000_000),
+                                      (1_000_003, 2**21 + 5)])
+def test_draw_sort_negatives_is_draw_then_sort(E, n_keys):
+    """hgnn_draw_sort_negatives (draws computed inside the sort's first pass) is bit for bit
+    hgnn_uniform_i32 followed by hgnn_sort_pairs_i32, and a stable sort (numpy) of the draws."""
+    from truth_recommendation_gnn_amd import _native as Nn
+    lib, s = Nn.lib(), Nn.stream_ptr(torch.device(DEV))
+    seed = torch.tensor([0x1234_5678_9ABC_DEF], dtype=torch.int64, device=DEV)
+    uop = torch.sort(torch.randint(0, 1 << 24, (E,), device=DEV, dtype=torch.int32))[0]
+    ws = Nn.workspace(lib.hgnn_sort_pairs_ws_bytes(E, n_keys), torch.device(DEV))
+    neg = torch.full((E,), -1, dtype=torch.int32, device=DEV)
+    rp = torch.empty(n_keys + 1, dtype=torch.int32, device=DEV)
+    us = torch.empty(E, dtype=torch.int32, device=DEV)
+    Nn.check(lib.hgnn_draw_sort_negatives(Nn.ptr(seed), Nn.ptr(uop), E, n_keys, Nn.ptr(neg),
+                                          Nn.ptr(rp), Nn.ptr(us), Nn.ptr(ws), ws.numel(), s),
+             "hgnn_draw_sort_negatives")
+    neg2 = torch.empty(E, dtype=torch.int32, device=DEV)
+    rp2 = torch.empty(n_keys + 1, dtype=torch.int32, device=DEV)
+    us2 = torch.empty(E, dtype=torch.int32, device=DEV)
+    if E:
+        Nn.check(lib.hgnn_uniform_i32(Nn.ptr(seed), E, n_keys, Nn.ptr(neg2), s), "uniform")
+    Nn.check(lib.hgnn_sort_pairs_i32(Nn.ptr(neg2), Nn.ptr(uop), None, E, n_keys, Nn.ptr(rp2),
+                                     Nn.ptr(us2), None, None, Nn.ptr(ws), ws.numel(), s), "sort")
+    torch.cuda.synchronize()
+    assert torch.equal(neg, neg2) and torch.equal(rp, rp2) and torch.equal(us, us2)
+    k = neg.cpu().numpy().astype(np.int64)
+    order = np.argsort(k, kind="stable")
+    np.testing.assert_array_equal(us.cpu().numpy(), uop.cpu().numpy()[order])
+    np.testing.assert_array_equal(rp.cpu().numpy(),
+                                  np.searchsorted(k[order], np.arange(n_keys + 1), side="left"))
+
+
+def test_fused_loss_negative_draw_equals_materialised():
+    """edge_bce_loss with a NegativeDraw (draw + grouping in one call) gives bitwise the loss and
+    gradients of the same draws materialised first (NegativeDraw.tensor())."""
+    z, x, e, params = _fixture_cfg1()
+    model = WeightedRGCN(hidden_dim=64).to(DEV)
+    model.load_state_dict(params)
+    with torch.no_grad():
+        out = model(x, e)
+    pos = e[synth.ENGAGES]
+    pw = torch.from_numpy(z["pos_weights"]).to(DEV)
+    dr = ops.draw_negatives(pos, out["post"].shape[0],
+                            generator=torch.Generator(device=DEV).manual_seed(11))
+    csr = ops.relation_csr_for_loss(pos, out["user"].shape[0], out["post"].shape[0])
+    res = []
+    for n in (dr, dr.tensor()):
+        U, P = out["user"].clone().requires_grad_(), out["post"].clone().requires_grad_()
+        loss = ops.edge_bce_loss(U, P, pos, n, pw, neg_order="user")
+        loss.backward()
+        res.append((loss.detach(), U.grad, P.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    # and the torch reference on the same draws, put back in COO edge order
+    neg_user = dr.tensor().long()
+    neg_edge = torch.empty_like(neg_user)
+    neg_edge[csr.bwd.perm.long()] = neg_user
+    U, P = out["user"].clone().requires_grad_(), out["post"].clone().requires_grad_()
+    ref = ops.link_loss(U, P, pos, neg_edge, pw)
+    ref.backward()
+    close(res[0][0], ref.detach())
+    close(res[0][1], U.grad)
+    close(res[0][2], P.grad)
+    with pytest.raises(ValueError):
+        ops.edge_bce_loss(out["user"], out["post"], pos, dr, pw, neg_order="edge")
+
+
 def test_weighted_rgcn_fused_loss_step_matches_golden():
     z, x, e, params = _fixture_cfg1()
     model = WeightedRGCN(hidden_dim=64).to(DEV)

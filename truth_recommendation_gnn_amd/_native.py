@@ -51,6 +51,7 @@ _SIGS = {
                                     _p, _c_sz, _p]),
     "hgnn_sort_pairs_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
     "hgnn_sort_pairs_i32": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_draw_sort_negatives": (_c_i32, [_p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_sort_pairs_i64": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_score_gather": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _c_i64, _c_i32, _p,
                                    ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p,

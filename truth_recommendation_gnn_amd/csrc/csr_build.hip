@@ -169,18 +169,27 @@ __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const 
 
 // counts[digit * nblocks + block] for this block's tile (RADIX = 1 << BITS digits).  Every key of
 // the tile is loaded before the first LDS atomic, so all RR loads per thread are in flight.
-template <int BITS, int RR = kSortRounds>
+// GEN: the keys are the uniform draws uniform_draw(*gen.seed, i, gen.hi) (the negatives sort),
+// computed in place of the key load.
+struct KeyGen {
+  const uint64_t* seed;
+  uint32_t hi;
+};
+
+template <int BITS, int RR = kSortRounds, bool GEN = false>
 __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
-                                                               int shift, int32_t* counts) {
+                                                               int shift, int32_t* counts,
+                                                               KeyGen gen = KeyGen{nullptr, 0}) {
   constexpr int R = 1 << BITS;
   __shared__ int hist[R];
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) hist[dd] = 0;
   const int64_t base = (int64_t)blockIdx.x * (kSortThreads * RR);
   int k[RR];
+  const uint64_t seed = GEN ? *gen.seed : 0;
 #pragma unroll
   for (int r = 0; r < RR; ++r) {
     const int64_t i = base + (int64_t)r * kSortThreads + threadIdx.x;
-    k[r] = i < E ? keys[i] : -1;
+    k[r] = i < E ? (GEN ? uniform_draw(seed, i, gen.hi) : keys[i]) : -1;
   }
   __syncthreads();
 #pragma unroll
@@ -207,10 +216,11 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
   return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-template <int BITS, bool HAS_B, int RR = kSortRounds>
+template <int BITS, bool HAS_B, int RR = kSortRounds, bool GEN = false>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
-    const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a) {
+    const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a,
+    KeyGen gen = KeyGen{nullptr, 0}, int32_t* gen_out = nullptr) {
   constexpr int R = 1 << BITS;
   constexpr int NW = kSortThreads / 64;
   constexpr int TILE = kSortThreads * RR;
@@ -232,13 +242,19 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   const int64_t tile0 = tile * TILE;
   const int64_t wave0 = tile0 + (int64_t)wid * PER_WAVE;
   int key[RR], rank[RR], va[RR], vb[RR];
+  const uint64_t seed = GEN ? *gen.seed : 0;
   // every load of the tile issued before the ranking: the wave barriers and LDS traffic of the
   // ranking loop would otherwise keep the compiler from hoisting them, one HBM latency per round
 #pragma unroll
   for (int r = 0; r < RR; ++r) {
     const int64_t i = wave0 + r * 64 + lane;
     const bool valid = i < E;
-    key[r] = valid ? keys_in[i] : 0;
+    if (GEN) {
+      key[r] = valid ? uniform_draw(seed, i, gen.hi) : 0;
+      if (valid && gen_out) gen_out[i] = key[r];   // the draws in position order (coalesced)
+    } else {
+      key[r] = valid ? keys_in[i] : 0;
+    }
     va[r] = valid ? (identity_a ? (int)i : a_in[i]) : 0;
     vb[r] = (HAS_B && valid) ? b_in[i] : 0;
   }
@@ -431,7 +447,8 @@ static size_t sort_ws_bytes(int64_t E) {
 static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t n_keys,
                             const int32_t* a_in, const int32_t* b_in, int32_t* a_out,
                             int32_t* b_out, Workspace& w, hipStream_t stream,
-                            const int32_t** k_sorted) {
+                            const int32_t** k_sorted, KeyGen gen = KeyGen{nullptr, 0},
+                            int32_t* gen_out = nullptr) {
   int32_t* kb = w.take<int32_t>(E);
   int32_t* ta = w.take<int32_t>(E);
   int32_t* tb = b_in ? w.take<int32_t>(E) : nullptr;
@@ -455,8 +472,12 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
     int32_t* aout = to_out ? a_out : ta;
     int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
     const int ident = (p == 0 && a_in == nullptr) ? 1 : 0;
-#define HGNN_COUNTS(BV) \
-  hipLaunchKernelGGL(k_digit_counts<BV>, dim3(nb), dim3(kSortThreads), 0, stream, kin, E, shift, counts)
+    const bool g0 = p == 0 && gen.seed != nullptr;   // first pass: keys drawn, not loaded
+#define HGNN_COUNTS(BV)                                                                           \
+  if (g0) hipLaunchKernelGGL((k_digit_counts<BV, kSortRounds, true>), dim3(nb), dim3(kSortThreads), \
+                             0, stream, kin, E, shift, counts, gen);                              \
+  else hipLaunchKernelGGL((k_digit_counts<BV>), dim3(nb), dim3(kSortThreads), 0, stream, kin, E,  \
+                          shift, counts, KeyGen{nullptr, 0})
     HGNN_BITS_SWITCH(bits, HGNN_COUNTS)
 #undef HGNN_COUNTS
     if (int rc = check_launch("k_digit_counts")) return rc;
@@ -464,8 +485,12 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
 #define HGNN_SCATTER(BV, HB)                                                                 \
   hipLaunchKernelGGL((k_digit_scatter<BV, HB>), dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, \
                      bin, E, shift, offs, kout, aout, bout, ident)
-#define HGNN_SCATTER_B(BV) \
-  if (b_in) { HGNN_SCATTER(BV, true); } else { HGNN_SCATTER(BV, false); }
+#define HGNN_SCATTER_B(BV)                                                                    \
+  if (g0) {                                                                                   \
+    hipLaunchKernelGGL((k_digit_scatter<BV, false, kSortRounds, true>), dim3(nb),              \
+                       dim3(kSortThreads), 0, stream, kin, ain, bin, E, shift, offs, kout, aout, \
+                       bout, ident, gen, gen_out);                                            \
+  } else if (b_in) { HGNN_SCATTER(BV, true); } else { HGNN_SCATTER(BV, false); }
     HGNN_BITS_SWITCH(bits, HGNN_SCATTER_B)
 #undef HGNN_SCATTER_B
 #undef HGNN_SCATTER
@@ -561,6 +586,33 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   }
   const int32_t* sk = nullptr;
   if (int rc = radix_sort_pairs(kin, ka, E, n_keys, a, b, a_sorted, b_sorted, w, stream, &sk))
+    return rc;
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
+                     n_keys, rowptr);
+  return check_launch("k_rowptr_from_sorted");
+}
+
+int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E, int64_t n_keys,
+                             int32_t* neg_out, int32_t* rowptr, int32_t* a_sorted, void* ws,
+                             size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_keys < 1 || n_keys >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "draw_sort_negatives: E=%lld n_keys=%lld out of range", (long long)E,
+                (long long)n_keys);
+  if (!rowptr || (E > 0 && (!d_seed || !a || !a_sorted)))
+    return fail(HGNN_E_ARG, "draw_sort_negatives: null pointer");
+  if (E == 0) {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, rowptr,
+                       n_keys + 1, 0);
+    return check_launch("draw_sort_negatives(empty)");
+  }
+  if (ws_bytes < sort_ws_bytes(E))
+    return fail(HGNN_E_WS, "draw_sort_negatives: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* ka = w.take<int32_t>(E);
+  const int32_t* sk = nullptr;
+  if (int rc = radix_sort_pairs(nullptr, ka, E, n_keys, a, nullptr, a_sorted, nullptr, w, stream,
+                                &sk, KeyGen{d_seed, (uint32_t)n_keys}, neg_out))
     return rc;
   hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
                      n_keys, rowptr);

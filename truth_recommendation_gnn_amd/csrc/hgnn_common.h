@@ -123,6 +123,16 @@ __device__ __forceinline__ float sigmoid_t(float x, float t) {
   return x >= 0.f ? r : t * r;
 }
 
+// Uniform int32 in [0, hi) of draw i: splitmix64 of seed + i * golden ratio, then the high 32 bits
+// scaled by hi (hgnn_uniform_i32; the negatives sort regenerates the same draws in its first pass).
+__device__ __forceinline__ int32_t uniform_draw(uint64_t seed, int64_t i, uint32_t hi) {
+  uint64_t x = seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (int32_t)(((x >> 32) * (uint64_t)hi) >> 32);
+}
+
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t* ws_bytes,
                        hipStream_t stream);
 

@@ -314,11 +314,7 @@ int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n
 __global__ void k_uniform_i32(const uint64_t* seed, int64_t n, uint32_t hi, int32_t* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint64_t x = *seed + (uint64_t)i * 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  out[i] = (int32_t)(((x >> 32) * (uint64_t)hi) >> 32);
+  out[i] = uniform_draw(*seed, i, hi);
 }
 
 // x *= *s in place, skipped entirely when *s == 1 (read on the device: no host sync).  The

@@ -585,7 +585,8 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP)."""
     U = _check_f32(U, "edge_bce_loss user_emb")
     P = _check_f32(P, "edge_bce_loss post_emb")
-    dev = N.require_device(U, P, neg_u_order)
+    draw = neg_u_order if isinstance(neg_u_order, NegativeDraw) else None
+    dev = N.require_device(U, P, draw.seed if draw is not None else neg_u_order)
     lib, s = N.lib(), N.stream_ptr(dev)
     nu, np_, d, E = U.shape[0], P.shape[0], int(U.shape[1]), csr.num_edges
     if P.shape[1] != d or nu != csr.n_src or np_ != csr.n_dst:
@@ -606,8 +607,13 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     c = cscale.to(torch.float32).reshape(()).contiguous()
     inv_e = 1.0 / n_total if n_total > 0 else 0.0
     uop = _user_of_pos(csr)
-    neg32 = neg_u_order.dtype == torch.int32          # sample_negatives' draws
-    neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
+    neg32 = neg_u_order.dtype == torch.int32          # sample_negatives' / draw_negatives' draws
+    if draw is not None:
+        if draw.n != E or draw.num_posts != np_:
+            raise ValueError("edge_bce_loss: the NegativeDraw does not match the positive edges")
+        neg = torch.empty(E, dtype=torch.int32, device=dev)   # written by the sort's first pass
+    else:
+        neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
     rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
     nu_s = torch.empty(E, dtype=torch.int32, device=dev)
     dP = torch.empty_like(P)
@@ -617,7 +623,14 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     lanes = _Lanes(dev, 2)
     with torch.cuda.stream(lanes.stream(1)):
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-        if neg32:
+        if draw is not None:
+            # draws computed in the sort's first pass; `neg` (position order) for the scoring pass
+            with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
+                N.check(lib.hgnn_draw_sort_negatives(
+                    N.ptr(draw.seed), N.ptr(uop), E, np_, N.ptr(neg), N.ptr(rowptr_n),
+                    N.ptr(nu_s), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                    "hgnn_draw_sort_negatives")
+        elif neg32:
             # int32 keys: no validation pass (the scoring pass below counts out-of-range
             # negatives; the sort only misplaces such a key, never dereferences it)
             with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
@@ -631,6 +644,8 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
                     N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
                     None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
                     "hgnn_sort_pairs_i64")
+    if draw is not None and lanes.side is not None:
+        lanes.main.wait_stream(lanes.side)    # the scoring pass reads the sort's `neg`
     if ready is not None:
         # P is still arriving (parallel.py's all-gather of the post table): the sort above
         # needs only the edges, so it ran ahead; every kernel below reads P
@@ -705,7 +720,7 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     if neg_p.shape[0] != csr.num_edges:
         raise ValueError("one negative per positive edge is required (train_gnn.py:272)")
-    neg_u = negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
+    neg_u = _negatives_user_order(csr, neg_p, neg_order)
     if cscale is None:
         cscale = pos_weights.to(torch.float32).mean()
     n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
@@ -718,13 +733,53 @@ def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges:
     """:func:`edge_bce_loss` outside autograd: (loss, dL/dU, dL/dP) from the same kernels, for
     callers that run their own backward schedule (``parallel.UserShard.step``)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
-    neg_u = negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
+    neg_u = _negatives_user_order(csr, neg_p, neg_order)
     return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready)
+
+
+def _negatives_user_order(csr, neg_p, neg_order):
+    if isinstance(neg_p, NegativeDraw):
+        if neg_order != "user":
+            raise ValueError("a NegativeDraw is drawn in the user-grouped order (neg_order='user')")
+        return neg_p
+    return negatives_in_user_order(csr, neg_p) if neg_order == "edge" else neg_p.contiguous()
 
 
 def relation_csr_for_loss(pos_edges, n_users, n_posts) -> RelationCSR:
     from .graph import relation_csr
     return relation_csr(pos_edges, n_users, n_posts)
+
+
+class NegativeDraw:
+    """One uniform negative post per positive edge, not yet materialised: the device seed of a
+    counter-based draw (:func:`draw_negatives`).  The fused loss draws and groups them by post in
+    one call (``hgnn_draw_sort_negatives``: the draws are computed inside the sort's first pass,
+    not written by one kernel and read back by two); :meth:`tensor` gives the same int32 values
+    as :func:`sample_negatives` would for the same seed."""
+
+    def __init__(self, seed: torch.Tensor, n: int, num_posts: int):
+        self.seed, self.n, self.num_posts = seed, int(n), int(num_posts)
+        self.shape = (self.n,)
+        self.dtype = torch.int32
+        self.device = seed.device
+
+    def tensor(self) -> torch.Tensor:
+        out = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        if self.n:
+            N.check(N.lib().hgnn_uniform_i32(N.ptr(self.seed), self.n, self.num_posts, N.ptr(out),
+                                             N.stream_ptr(self.device)), "hgnn_uniform_i32")
+        return out
+
+
+def draw_negatives(pos_edges: torch.Tensor, num_posts: int,
+                   generator: Optional[torch.Generator] = None) -> NegativeDraw:
+    """:func:`sample_negatives` without the materialised array: the seed only (one tiny device
+    draw from ``generator``, no host sync).  ``edge_bce_loss(..., neg_order='user')`` takes it."""
+    dev = N.require_device(pos_edges)
+    if num_posts < 1 or num_posts >= 2**31:
+        raise ValueError(f"num_posts={num_posts} out of range")
+    seed = torch.randint(0, 2**62, (1,), device=dev, dtype=torch.int64, generator=generator)
+    return NegativeDraw(seed, int(pos_edges.shape[1]), num_posts)
 
 
 def sample_negatives(pos_edges: torch.Tensor, num_posts: int,
