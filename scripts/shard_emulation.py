@@ -79,7 +79,7 @@ def main():
 
     def step():
         opt.zero_grad(set_to_none=True)
-        neg = ops.sample_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
+        neg = ops.draw_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
         shard.step(model, x_user, x_post, neg, neg_order="user", x_user_full=x_full)
         opt.step()
 

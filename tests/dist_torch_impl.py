@@ -90,11 +90,14 @@ class TorchImpl:
             o += s.shape[1]
         return (dz.T @ x if need_w else None), (dz.sum(0) if need_b else None)
 
-    def edge_bce_loss_raw(self, U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None):
+    def edge_bce_loss_raw(self, U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None,
+                          on_dP=None):
         if ready is not None:
             ready()
         U2, P2 = U.detach().requires_grad_(), P.detach().requires_grad_()
         with torch.enable_grad():
             loss = self.edge_bce_loss(U2, P2, pos, neg, n_total, cscale)
             dU, dP = torch.autograd.grad(loss, (U2, P2))
+        if on_dP is not None:
+            on_dP(dP)
         return loss.detach(), dU, dP

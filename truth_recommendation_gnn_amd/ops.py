@@ -581,8 +581,10 @@ def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tens
 
 
 def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
-              ready=None):
-    """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP)."""
+              ready=None, on_dP=None):
+    """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP).  ``on_dP(dP)``,
+    if given, is called once dP's kernels are enqueued and before the scoring pass (dU, the loss)
+    is: the sharded step starts dP's reduce-scatter there, under the scoring pass."""
     U = _check_f32(U, "edge_bce_loss user_emb")
     P = _check_f32(P, "edge_bce_loss post_emb")
     draw = neg_u_order if isinstance(neg_u_order, NegativeDraw) else None
@@ -660,6 +662,8 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
         else:
             _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
             _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
+        if on_dP is not None:
+            on_dP(dP)
     with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
         if neg32:
             N.check(lib.hgnn_edge_score_fwd_i32(
@@ -729,12 +733,14 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
 
 def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
                       neg_p: torch.Tensor, n_edges_total: int, cscale: torch.Tensor,
-                      neg_order: str = "user", ready=None):
+                      neg_order: str = "user", ready=None, on_dP=None):
     """:func:`edge_bce_loss` outside autograd: (loss, dL/dU, dL/dP) from the same kernels, for
-    callers that run their own backward schedule (``parallel.UserShard.step``)."""
+    callers that run their own backward schedule (``parallel.UserShard.step``; ``on_dP``: see
+    ``_edge_bce``)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     neg_u = _negatives_user_order(csr, neg_p, neg_order)
-    return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready)
+    return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready,
+                     on_dP)
 
 
 def _negatives_user_order(csr, neg_p, neg_order):

@@ -768,7 +768,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             hl = shard.halo
             halo, halo_w = env.all_to_all_async(impl.gather_mean_raw(h_u, hl.rel_send),
                                                 hl.send_splits, hl.recv_splits)
-        rs = {}
+        rs, rs_issued = {}, False
         for _, et, _ in pm:
             r = shard.rels[et]
             if r.kind[0] == "user":
@@ -778,68 +778,102 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     continue
                 part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd)
                 rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
+                rs_issued = True
         if ag is not None:                      # F3 the previous layer's post table
             ag.wait()
             ag = None
-        # F4 user side (a pre-projected relation's mean of projected rows enters the epilogue)
-        a_u, x_ext, add = [], None, None
-        for j, (_, et, _) in enumerate(um):
-            r = shard.rels[et]
-            if j == jp:
-                add = impl.gather_mean_raw(h_p, r.csr)
-            elif r.kind[0] == "post":
-                a_u.append(impl.gather_mean_raw(h_p, r.csr))
-            else:
-                if x_ext is None:
-                    halo_w.wait()
-                    x_ext = h_u if halo is None else torch.cat([h_u, halo])
-                a_u.append(impl.gather_mean_raw(x_ext, r.csr))
         Wu_main = _without_block(Wu, col_pre) if jp is not None else Wu
-        # the last layer's user projection waits until the post table's all-gather is issued: the
-        # loss needs that table at once, so the projection and the negatives sort both run under
-        # the collective (the reduce-scatter still has the user-side gathers under it)
-        late_u = multi and bool(pm) and bool(um) and li == L - 1
-        y_u = _lin_fwd(impl, a_u + [h_u], Wu_main, bu, add) if um and not late_u else h_u
-        # F5 post side on the owned slice, then its all-gather (of the next layer's projected
-        # rows when that layer pre-projects)
-        a_p = []
-        for _, et, _ in pm:
-            r = shard.rels[et]
-            if r.kind[0] == "post":
-                a_p.append(impl.gather_mean_raw(h_p, r.csr))
-            else:
-                a, w = rs[et]
-                w.wait()
-                a_p.append(a)
-        if pm:
-            y_p_own = impl.linear_fwd_raw(a_p + [h_p_own], Wp, bp, True)
+        st = {"x_ext": None, "a_u": [], "add": None, "y_u": h_u, "a_p": [],
+              "y_p_own": h_p_own, "y_p": h_p}
+
+        def user_gathers():
+            # F4 user side (a pre-projected relation's mean of projected rows enters the epilogue)
+            for j, (_, et, _) in enumerate(um):
+                r = shard.rels[et]
+                if j == jp:
+                    st["add"] = impl.gather_mean_raw(h_p, r.csr)
+                elif r.kind[0] == "post":
+                    st["a_u"].append(impl.gather_mean_raw(h_p, r.csr))
+                else:
+                    if st["x_ext"] is None:
+                        halo_w.wait()
+                        st["x_ext"] = h_u if halo is None else torch.cat([h_u, halo])
+                    st["a_u"].append(impl.gather_mean_raw(st["x_ext"], r.csr))
+
+        def user_projection():
+            if um:
+                st["y_u"] = _lin_fwd(impl, st["a_u"] + [h_u], Wu_main, bu, st["add"])
+
+        def post_side():
+            # F5 post side on the owned slice, then its all-gather (of the next layer's projected
+            # rows when that layer pre-projects)
+            nonlocal ag
+            for _, et, _ in pm:
+                r = shard.rels[et]
+                if r.kind[0] == "post":
+                    st["a_p"].append(impl.gather_mean_raw(h_p, r.csr))
+                else:
+                    a, w = rs[et]
+                    w.wait()
+                    st["a_p"].append(a)
+            if not pm:
+                return
+            y_p_own = impl.linear_fwd_raw(st["a_p"] + [h_p_own], Wp, bp, True)
             table = y_p_own
             nxt = li + 1
             if nxt < L and pre[nxt] is not None:
-                (Wu_n, _), _ = weights_of(nxt, {"user": y_u, "post": y_p_own})
-                um_n = layers[nxt][1]["user"]
-                cols = _block_cols(um_n, {"user": int(y_u.shape[1]),
-                                                 "post": int(y_p_own.shape[1])})
-                o, k = cols[pre[nxt]]
+                wu = int(Wu.shape[0]) if um else int(h_u.shape[1])   # the next layer's input widths
+                wp = int(y_p_own.shape[1])
+                stand_in = {"user": h_u.new_empty((0, wu)), "post": h_u.new_empty((0, wp))}
+                (Wu_n, _), _ = weights_of(nxt, stand_in)
+                o, k = _block_cols(layers[nxt][1]["user"], {"user": wu, "post": wp})[pre[nxt]]
                 if k >= Wu_n.shape[0]:          # the projected rows are no wider than y_p
                     block = Wu_n[:, o:o + k].contiguous()
                     table = impl.linear_fwd_raw([y_p_own], block, None, False)
                     proj[nxt] = (block, (o, k))
-            y_p, ag = env.all_gather_async(table) if multi else (table, None)
+            st["y_p_own"] = y_p_own
+            st["y_p"], ag = env.all_gather_async(table) if multi else (table, None)
+
+        if multi and pm and not rs_issued:
+            # no reduce-scatter to wait for (layer 1 with the static inputs held whole): the post
+            # side first, so its all-gather runs under this layer's user side and the next
+            # layer's partial sums
+            post_side()
+            user_gathers()
+            user_projection()
         else:
-            y_p_own, y_p = h_p_own, h_p
-        if late_u:
-            y_u = _lin_fwd(impl, a_u + [h_u], Wu_main, bu, add)
+            user_gathers()
+            # the last layer's user projection waits until the post table's all-gather is
+            # issued: the loss needs that table at once, so the projection and the negatives
+            # sort both run under the collective (the reduce-scatter still has the user-side
+            # gathers under it)
+            late_u = multi and bool(pm) and bool(um) and li == L - 1
+            if not late_u:
+                user_projection()
+            post_side()
+            if late_u:
+                user_projection()
+        x_ext, a_u, add, y_u = st["x_ext"], st["a_u"], st["add"], st["y_u"]
+        a_p, y_p_own, y_p = st["a_p"], st["y_p_own"], st["y_p"]
         saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu_main,
                       Wp, bu is not None, bp is not None, jp, col_pre))
         h_u, h_p, h_p_own = y_u, y_p, y_p_own
     shard.pre_layers = [li for li in range(L) if proj[li] is not None]   # (for tests)
-    # loss: the negatives sort runs while the last all-gather lands
+    # loss: the negatives sort runs while the last all-gather lands; dP's reduce-scatter (the
+    # all-gather's adjoint, B1) is issued as soon as dP is enqueued and runs under the scoring
+    # pass and the user-side projection backward
+    R = None                                    # reduce-scatter of G_full, once issued
+
+    def issue_b1(dP):
+        nonlocal R
+        if multi and layers[-1][1].get("post"):
+            R = env.reduce_scatter_async(dP)
+
     loss, G_u, G_full = impl.edge_bce_loss_raw(h_u, h_p, shard.pos_local, neg_local,
                                                shard.num_edges_global, shard.cscale, neg_order,
-                                               ag.wait if ag is not None else None)
+                                               ag.wait if ag is not None else None,
+                                               on_dP=issue_b1)
     G_own = None
-    R = None                                    # reduce-scatter of G_full, once issued
     R_proj = None                               # (block, cols, grads to finish) if R carries dP
     for li in reversed(range(L)):
         (convs, um, pm, hu, hp, hpo, x_ext, a_u, a_p, yu, ypo, Wu, Wp, has_bu, has_bp, jp,
