@@ -15,13 +15,19 @@ import json
 import sys
 
 
-def rows(d, counter):
-    out = collections.defaultdict(list)      # (kernel, grid) -> [values in dispatch order]
+def rows(d, counter, marker=None):
+    """(kernel, grid) -> [values in dispatch order]; with ``marker``, only the dispatches after
+    the last dispatch whose kernel name contains it (the profiled steps)."""
+    out = collections.defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         recs = list(csv.DictReader(open(f)))
         key = "Dispatch_Id" if recs and "Dispatch_Id" in recs[0] else None
         if key:
             recs.sort(key=lambda r: int(r[key]))
+        if marker and key:
+            ids = [int(r[key]) for r in recs if marker in r["Kernel_Name"]]
+            if ids:
+                recs = [r for r in recs if int(r[key]) > max(ids)]
         for r in recs:
             if r["Counter_Name"] == counter:
                 out[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
@@ -39,7 +45,8 @@ def main():
     for line in open(log):
         if line.startswith("PMC_TARGET "):
             info = json.loads(line[len("PMC_TARGET "):])
-    fetch, write = rows(fetch_dir, "FETCH_SIZE"), rows(write_dir, "WRITE_SIZE")
+    mk = info.get("marker")
+    fetch, write = rows(fetch_dir, "FETCH_SIZE", mk), rows(write_dir, "WRITE_SIZE", mk)
     cfg, steps = info["config"], info["steps"]
     out = {"counters": "FETCH_SIZE, WRITE_SIZE (KiB): separate rocprofv3 --kernel-trace --pmc passes "
                        "of scripts/pmc_step_target.py",
