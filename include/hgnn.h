@@ -135,6 +135,15 @@ int hgnn_linear_fwd_add(int32_t n_seg, const float* const* xs, const int32_t* ks
                         const float* w, int32_t h, const float* bias, const float* add,
                         int32_t relu, float* out, hgnn_stream_t stream);
 
+/* hgnn_linear_fwd_add that also writes the ReLU mask of `out` as bits (relu != 0, h % 32 == 0):
+ * bit c % 32 of mask[row * (h / 32) + c / 32] = out[row][c] > 0, 16-B aligned.  The backward
+ * (hgnn_linear_bwd_mask) reads h/8 bytes per row instead of out's 4h: autograd's saved ReLU
+ * output is only ever used for that mask (train_gnn.py:198's activation). */
+int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* ks,
+                         int64_t n_rows, const float* w, int32_t h, const float* bias,
+                         const float* add, int32_t relu, float* out, uint32_t* mask,
+                         hgnn_stream_t stream);
+
 /* Backward of hgnn_linear_fwd.  dz = dout * (out > 0) when out != NULL (ReLU), else dout.
  *   dxs[s] = dz @ w[:, seg s]           (skipped for NULL entries)
  *   dw     = dz^T @ [xs...]             (NULL: skipped; same for db = colsum(dz))
@@ -147,6 +156,13 @@ int hgnn_linear_bwd_dz(int32_t n_seg, const float* const* xs, const int32_t* ks,
                        const float* w, int32_t h, const float* dout, const float* out,
                        float* const* dxs, float* dw, float* db, float* dz_out, void* ws,
                        size_t ws_bytes, hgnn_stream_t stream);
+/* hgnn_linear_bwd_dz with the ReLU mask also given as the bits of hgnn_linear_fwd_mask: the
+ * persistent backward kernels read the bits, the others `out` (both required). */
+int hgnn_linear_bwd_mask(int32_t n_seg, const float* const* xs, const int32_t* ks,
+                         int64_t n_rows, const float* w, int32_t h, const float* dout,
+                         const float* out, const uint32_t* mask, float* const* dxs, float* dw,
+                         float* db, float* dz_out, void* ws, size_t ws_bytes,
+                         hgnn_stream_t stream);
 int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,

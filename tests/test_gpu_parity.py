@@ -229,6 +229,49 @@ def test_linear_bwd_variants(ks, h, mode):
         close(db, ref_db)
 
 
+def _unpack_relu_bits(mask, n, h):
+    """The lane layout of hgnn_linear_fwd_mask as a dense [n, h] bool: word row*4 + g, bit 4c + e
+    is column 16c + 4g + e."""
+    m = mask.cpu().view(torch.int32).numpy().astype(np.uint32).reshape(n, 4)
+    out = np.zeros((n, h), dtype=bool)
+    for g in range(4):
+        for c in range(h // 16):
+            for e in range(4):
+                out[:, 16 * c + 4 * g + e] = (m[:, g] >> np.uint32(4 * c + e)) & 1
+    return out
+
+
+@pytest.mark.parametrize("ks,h", [([128, 128], 128), ([128], 128), ([64, 64], 64),
+                                  ([64, 64, 128], 128), ([16, 48], 128), ([64], 48),
+                                  ([64, 64], 112)])
+@pytest.mark.parametrize("mode", ["all", "wgrad_only", "dz_out"])
+def test_linear_relu_bits_equal_float_mask(ks, h, mode):
+    """hgnn_linear_fwd_mask writes out > 0 as bits (persistent kernels, or k_relu_mask for other
+    shapes: h = 48, 112) and hgnn_linear_bwd_mask with those bits gives bitwise the gradients of
+    the float-mask backward (hgnn_linear_bwd_dz), dz side output included."""
+    n = 64 * 300 + 17
+    gen = torch.Generator().manual_seed(3 * h + len(ks))
+    segs = [torch.randn(n, k, generator=gen).to(DEV) for k in ks]
+    w = (torch.randn(h, sum(ks), generator=gen) * 0.2).to(DEV)
+    b = torch.randn(h, generator=gen).to(DEV)
+    dout = torch.randn(n, h, generator=gen).to(DEV)
+    mk = ops.relu_mask_for(n, h, True, torch.device(DEV))
+    assert mk is not None
+    out = ops.linear_fwd(segs, w, b, relu=True, mask_out=mk)
+    ref = ops.linear_fwd(segs, w, b, relu=True)
+    assert torch.equal(out, ref)
+    np.testing.assert_array_equal(_unpack_relu_bits(mk, n, h), (out > 0).cpu().numpy())
+    res = []
+    for m in (None, mk):
+        dxs = [None] * len(ks) if mode == "wgrad_only" else [torch.empty_like(x) for x in segs]
+        dz = torch.empty_like(dout) if mode == "dz_out" else None
+        dw, db = ops.linear_bwd(segs, w, dout, out, dxs, True, True, dz_out=dz, mask=m)
+        res.append([dw, db, dz] + dxs)
+    for a, c in zip(*res):
+        if a is not None:
+            assert torch.equal(a, c)
+
+
 # ----------------------------------------------------------------------------- models
 def _fixture_cfg1():
     z = np.load(GOLD / "cfg1_weighted_rgcn.npz")

@@ -44,6 +44,10 @@ _SIGS = {
     "hgnn_linear_fwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _c_i32, _p, _p]),
     "hgnn_linear_fwd_add": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _c_i32, _p,
                                      _p]),
+    "hgnn_linear_fwd_mask": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _c_i32, _p,
+                                      _p, _p]),
+    "hgnn_linear_bwd_mask": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p,
+                                      _p, _p, _p, _c_sz, _p]),
     "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
                                  _c_sz, _p]),

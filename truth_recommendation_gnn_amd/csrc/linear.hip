@@ -35,6 +35,8 @@ struct LinArgs {
   const float* bias;
   const float* dout;
   const float* out_act;   // ReLU output for the backward mask (nullable)
+  const uint32_t* mask_in;  // backward: the same mask as bits (hgnn_linear_fwd_mask; nullable)
+  uint32_t* mask_out;       // forward: write the ReLU mask as bits (nullable)
   const float* add;       // forward: [n, h] rows added before the activation (nullable)
   float* dz_out;          // backward: the masked dz written out as well (nullable; dgrad kernels)
   float* out;
@@ -47,6 +49,23 @@ struct LinArgs {
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ReLU mask as bits (hgnn_linear_fwd_mask), in the lane layout the persistent kernels share:
+// the lane (i, g) that holds columns 16 c + 4 g .. +3 (c = 0 .. H/16 - 1) of row i finds them in
+// word row * 4 + g, bits 4 c .. 4 c + 3 (H <= 128, a multiple of 16): one 4-B word per lane per
+// row, no cross-lane exchange in the forward, 16 B per row instead of the output's 4 H.
+__device__ __forceinline__ float4 mask4(float4 v, uint32_t word, int shift) {
+  v.x = (word >> shift) & 1u ? v.x : 0.f;
+  v.y = (word >> (shift + 1)) & 1u ? v.y : 0.f;
+  v.z = (word >> (shift + 2)) & 1u ? v.z : 0.f;
+  v.w = (word >> (shift + 3)) & 1u ? v.w : 0.f;
+  return v;
+}
+
+__device__ __forceinline__ uint32_t relu_bits(float4 v, int shift) {
+  return ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+          (v.w > 0.f ? 8u : 0u)) << shift;
 }
 
 template <bool VEC>
@@ -658,6 +677,7 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
       }
     const int64_t row = t * 16 + i;
     if (row < a.n) {
+      uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         // bias re-read per tile (L1-resident) rather than held in 4*NT VGPRs for the whole loop
@@ -672,8 +692,10 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
         if (a.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
+        mbits |= relu_bits(v, 4 * tt);
         *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
       }
+      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
     }
 #pragma unroll
     for (int c = 0; c < KC; ++c) av[c] = an[c];
@@ -747,6 +769,7 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
     }
     const int64_t row = t * 16 + i;
     if (row < a.n) {
+      uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
@@ -760,8 +783,10 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
         if (a.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
+        mbits |= relu_bits(v, 4 * tt);
         *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
       }
+      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
     }
   }
 }
@@ -804,12 +829,15 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
   if (zrole) {
     auto load_dz = [&](int64_t it, float4 (&z)[HC]) {
       const int64_t row = (blockIdx.x + it * gridDim.x) * T + zrow * 16 + i;
+      const uint32_t mk = a.mask_in && it < n_my && row < a.n ? a.mask_in[row * 4 + g] : 0u;
 #pragma unroll
       for (int c = 0; c < HC; ++c) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (it < n_my && row < a.n && c >= zcol0 && c < zcol0 + ZC) {
           v = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
-          if (a.out_act) {
+          if (a.mask_in) {
+            v = mask4(v, mk, 4 * c);
+          } else if (a.out_act) {
             const float4 m =
                 *reinterpret_cast<const float4*>(a.out_act + row * H + c * 16 + 4 * g);
             v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
@@ -995,16 +1023,20 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
   const int xc = xk4 / 4;
   const float* xseg = tab.x[xc] + tab.col[xc] + 4 * (xk4 % 4);
   const int xld = tab.ld[xc];
-  const bool masked = a.out_act != nullptr;
+  const bool bits = a.mask_in != nullptr;
+  const bool masked = !bits && a.out_act != nullptr;
   const int64_t n_my = (n_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
   const int64_t last = a.n - 1;
   float4 zp[ZQ], mp[ZQ], xp[XQ];
+  uint32_t bp[ZQ];
+  const int bshift = 4 * (zc4 >> 2);        // columns 4 zc4 .. +3: chunk zc4/4, lane group zc4%4
   auto issue = [&](int64_t it) {
     const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
 #pragma unroll
     for (int q = 0; q < ZQ; ++q) {
       const int64_t row = min<int64_t>(r0 + zr0 + q * ZR, last);
       zp[q] = *reinterpret_cast<const float4*>(a.dout + row * H + 4 * zc4);
+      if (bits) bp[q] = a.mask_in[row * 4 + (zc4 & 3)];
       if (masked) mp[q] = *reinterpret_cast<const float4*>(a.out_act + row * H + 4 * zc4);
     }
 #pragma unroll
@@ -1029,6 +1061,7 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
     for (int q = 0; q < ZQ; ++q) {
       const int r = zr0 + q * ZR;
       float4 v = zp[q];
+      if (bits) v = mask4(v, bp[q], bshift);
       if (masked) {
         v.x = mp[q].x > 0.f ? v.x : 0.f; v.y = mp[q].y > 0.f ? v.y : 0.f;
         v.z = mp[q].z > 0.f ? v.z : 0.f; v.w = mp[q].w > 0.f ? v.w : 0.f;
@@ -1134,12 +1167,15 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
   const int64_t nw = (int64_t)gridDim.x * 8;
   auto load_dz = [&](int64_t t, float4 (&z)[HC]) {
     const int64_t row = t * 16 + i;
+    const uint32_t mk = a.mask_in && row < a.n ? a.mask_in[row * 4 + g] : 0u;
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (row < a.n) {
         v = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
-        if (a.out_act) {
+        if (a.mask_in) {
+          v = mask4(v, mk, 4 * c);
+        } else if (a.out_act) {
           const float4 m = *reinterpret_cast<const float4*>(a.out_act + row * H + c * 16 + 4 * g);
           v.x = m.x > 0.f ? v.x : 0.f; v.y = m.y > 0.f ? v.y : 0.f;
           v.z = m.z > 0.f ? v.z : 0.f; v.w = m.w > 0.f ? v.w : 0.f;
@@ -1215,10 +1251,13 @@ __global__ void __launch_bounds__(512, 2) k_linear_dgrad_v5(const LinArgs a, con
   const int i = lane & 15, g = lane >> 4;
   const int64_t nw = (int64_t)gridDim.x * 8;
   const int64_t last = a.n - 1;
-  const bool masked = a.out_act != nullptr;
+  const bool bits = a.mask_in != nullptr;
+  const bool masked = !bits && a.out_act != nullptr;
   float4 zr[HC], mr[HC];
+  uint32_t mk = 0u;
   auto issue = [&](int64_t t) {
     const int64_t row = min<int64_t>(t * 16 + i, last);
+    if (bits) mk = a.mask_in[row * 4 + g];
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
       zr[c] = *reinterpret_cast<const float4*>(a.dout + row * H + c * 16 + 4 * g);
@@ -1234,6 +1273,7 @@ __global__ void __launch_bounds__(512, 2) k_linear_dgrad_v5(const LinArgs a, con
 #pragma unroll
     for (int c = 0; c < HC; ++c) {
       zc[c] = zr[c];
+      if (bits) zc[c] = mask4(zc[c], mk, 4 * c);
       if (masked) {
         zc[c].x = mr[c].x > 0.f ? zc[c].x : 0.f; zc[c].y = mr[c].y > 0.f ? zc[c].y : 0.f;
         zc[c].z = mr[c].z > 0.f ? zc[c].z : 0.f; zc[c].w = mr[c].w > 0.f ? zc[c].w : 0.f;
@@ -1289,6 +1329,21 @@ __global__ void __launch_bounds__(512, 2) k_linear_dgrad_v5(const LinArgs a, con
 }
 
 
+
+// ReLU mask bits from a finished output (forward shapes without a persistent kernel), in the
+// lane layout of mask4: one thread per (row, lane group g).
+__global__ void k_relu_mask(const float* out, int64_t n, int32_t h, uint32_t* mask) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n * 4) return;
+  const int64_t row = idx >> 2;
+  const int g = (int)(idx & 3);
+  uint32_t m = 0;
+  for (int c = 0; c < h / 16; ++c)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      m |= (out[row * h + 16 * c + 4 * g + e] > 0.f ? 1u : 0u) << (4 * c + e);
+  mask[idx] = m;
+}
 
 // the persistent forward also takes K = 256 (W: H*(K+8)*4 <= 135 KB of LDS, one block per CU)
 static bool fwd4_ok(const LinArgs& a, bool vec) {
@@ -1352,11 +1407,32 @@ int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, in
 int hgnn_linear_fwd_add(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                         const float* w, int32_t h, const float* bias, const float* add,
                         int32_t relu, float* out, hgnn_stream_t stream_) {
+  return hgnn_linear_fwd_mask(n_seg, xs, ks, n_rows, w, h, bias, add, relu, out, nullptr,
+                              stream_);
+}
+
+int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                         const float* w, int32_t h, const float* bias, const float* add,
+                         int32_t relu, float* out, uint32_t* mask, hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   LinArgs a{};
   bool vec;
   if (int rc = fill_args(a, n_seg, xs, ks, nullptr, n_rows, w, h, &vec)) return rc;
+  if (mask && (!relu || h % 16 != 0 || h > 128))
+    return fail(HGNN_E_ARG, "linear_fwd_mask: the bit mask needs relu, h %% 16 == 0, h <= 128 (h=%d)",
+                h);
   if (n_rows == 0) return HGNN_OK;
+  if (mask && !(fwd4_ok(a, vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                        reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&
+                        reinterpret_cast<uintptr_t>(add) % 16 == 0))) {
+    // no persistent kernel for this shape: the output first, then its mask from the output
+    if (int rc = hgnn_linear_fwd_add(n_seg, xs, ks, n_rows, w, h, bias, add, relu, out, stream_))
+      return rc;
+    hipLaunchKernelGGL(k_relu_mask, dim3((unsigned)cdiv(n_rows * 4, 256)), dim3(256), 0, stream,
+                       out, n_rows, h, mask);
+    return check_launch("k_relu_mask");
+  }
+  a.mask_out = mask;
   if (!out) return fail(HGNN_E_ARG, "linear_fwd: out is null");
   vec = vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
         reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&
@@ -1466,13 +1542,25 @@ int hgnn_linear_bwd_dz(int32_t n_seg, const float* const* xs, const int32_t* ks,
                        const float* w, int32_t h, const float* dout, const float* out,
                        float* const* dxs, float* dw, float* db, float* dz_out, void* ws,
                        size_t ws_bytes, hgnn_stream_t stream_) {
+  return hgnn_linear_bwd_mask(n_seg, xs, ks, n_rows, w, h, dout, out, nullptr, dxs, dw, db,
+                              dz_out, ws, ws_bytes, stream_);
+}
+
+int hgnn_linear_bwd_mask(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                         const float* w, int32_t h, const float* dout, const float* out,
+                         const uint32_t* mask, float* const* dxs, float* dw, float* db,
+                         float* dz_out, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   LinArgs a{};
   bool vec;
   if (int rc = fill_args(a, n_seg, xs, ks, dxs, n_rows, w, h, &vec)) return rc;
   if (!dout && n_rows > 0) return fail(HGNN_E_ARG, "linear_bwd: dout is null");
+  if (mask && (!out || h % 16 != 0 || h > 128))
+    return fail(HGNN_E_ARG, "linear_bwd_mask: the bit mask needs `out` too, h %% 16 == 0, h <= 128");
   a.dout = dout;
   a.out_act = out;
+  // the persistent kernels read the bits; the others (and the streaming dz pass) read `out`
+  a.mask_in = mask;
   vec = vec && reinterpret_cast<uintptr_t>(dout) % 16 == 0 &&
         (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
         reinterpret_cast<uintptr_t>(dz_out) % 16 == 0;
@@ -1536,6 +1624,7 @@ int hgnn_linear_bwd_dz(int32_t n_seg, const float* const* xs, const int32_t* ks,
     if (a.dz_out && !fused) {   // the dgrad kernel wrote the masked dz: wgrad streams it alone
       a.dout = a.dz_out;
       a.out_act = nullptr;
+      a.mask_in = nullptr;
       a.dz_out = nullptr;
     }
     // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;

@@ -194,9 +194,23 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
     return out
 
 
+def relu_mask_for(n: int, h: int, relu: bool, dev) -> Optional[torch.Tensor]:
+    """The bit form of a K3 output's ReLU mask (``hgnn_linear_fwd_mask``: 16 B per row, the
+    backward reads it instead of the 4h-byte output), or None where the kernels have no bit form
+    (no ReLU, h not a multiple of 16 or above 128, or ``HGNN_RELU_BITS=0``)."""
+    if not (RELU_BITS and relu and h % 16 == 0 and h <= 128):
+        return None
+    return torch.empty((n, 4), dtype=torch.int32, device=dev)
+
+
+RELU_BITS = os.environ.get("HGNN_RELU_BITS", "1") == "1"
+
+
 def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.Tensor],
-               relu: bool, add: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """K3/K4: ``act(sum_s segs[s] @ w[:, seg s]^T + b (+ add))``."""
+               relu: bool, add: Optional[torch.Tensor] = None,
+               mask_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K3/K4: ``act(sum_s segs[s] @ w[:, seg s]^T + b (+ add))``; ``mask_out`` (from
+    :func:`relu_mask_for`) also receives the ReLU mask as bits."""
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
@@ -206,16 +220,18 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
     out = torch.empty(n, h, dtype=torch.float32, device=dev)
     k = sum(ks)
     with _timed(f"linear_fwd[{n}x{k}->{h}]", 4 * n * (k + h), flops=2 * n * k * h):
-        N.check(N.lib().hgnn_linear_fwd_add(len(segs), N.ptr_array(segs), N.int_array(ks), n,
-                                            N.ptr(w), h, N.ptr(b), N.ptr(add),
-                                            1 if relu else 0, N.ptr(out), N.stream_ptr(dev)),
-                "hgnn_linear_fwd_add")
+        N.check(N.lib().hgnn_linear_fwd_mask(len(segs), N.ptr_array(segs), N.int_array(ks), n,
+                                             N.ptr(w), h, N.ptr(b), N.ptr(add),
+                                             1 if relu else 0, N.ptr(out), N.ptr(mask_out),
+                                             N.stream_ptr(dev)), "hgnn_linear_fwd_mask")
     return out
 
 
 def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], need_w: bool,
-               need_b: bool, dz_out: Optional[torch.Tensor] = None):
-    """K3 backward; ``dz_out`` (optional [n, h]) receives the masked dz as well."""
+               need_b: bool, dz_out: Optional[torch.Tensor] = None,
+               mask: Optional[torch.Tensor] = None):
+    """K3 backward; ``dz_out`` (optional [n, h]) receives the masked dz as well; ``mask``: the
+    forward's ReLU bits (read instead of ``out_act`` by the persistent kernels)."""
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
@@ -226,13 +242,16 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     if need_w or need_b:
         ws = N.workspace(N.lib().hgnn_linear_bwd_ws_bytes(n, sum(ks), h), dev)
     k_dx = sum(k for k, dx in zip(ks, dxs) if dx is not None)
-    nb = 4 * n * (2 * h + sum(ks) + k_dx)
+    bits = mask is not None and out_act is not None
+    nb = 4 * n * (h + (h if out_act is not None and not bits else 0) + sum(ks) + k_dx) + \
+        (16 * n if bits else 0)
     fl = 2 * n * h * k_dx + (2 * n * sum(ks) * h if need_w else 0)   # dgrad + wgrad
     with _timed(f"linear_bwd[{n}x{sum(ks)}->{h}]", nb, flops=fl):
-        N.check(N.lib().hgnn_linear_bwd_dz(
+        N.check(N.lib().hgnn_linear_bwd_mask(
             len(segs), N.ptr_array(segs), N.int_array(ks), n, N.ptr(w), h, N.ptr(dout),
-            N.ptr(out_act), N.ptr_array(dxs), N.ptr(dw), N.ptr(db), N.ptr(dz_out), N.ptr(ws),
-            0 if ws is None else ws.numel(), N.stream_ptr(dev)), "hgnn_linear_bwd_dz")
+            N.ptr(out_act), N.ptr(mask if out_act is not None else None), N.ptr_array(dxs),
+            N.ptr(dw), N.ptr(db), N.ptr(dz_out), N.ptr(ws), 0 if ws is None else ws.numel(),
+            N.stream_ptr(dev)), "hgnn_linear_bwd_mask")
     return dw, db
 
 
@@ -321,7 +340,7 @@ class _HeteroLayer(torch.autograd.Function):
         xs = dict(zip(spec.types, flat[:nt]))
         wb = flat[nt:]
         ng = len(spec.groups)
-        outs, aggrs_by_g = [None] * ng, [None] * ng
+        outs, aggrs_by_g, masks = [None] * ng, [None] * ng, [None] * ng
         dev = flat[0].device
         lanes = _Lanes(dev, ng)
         for gi, g in enumerate(spec.groups):   # destination types are independent chains
@@ -340,19 +359,23 @@ class _HeteroLayer(torch.autograd.Function):
                         else:
                             aggrs.append(gather_mean(xs[src], csr))
                     segs = aggrs + ([xs[g.dst]] if g.root else [])
+                    mk = relu_mask_for(xs[g.dst].shape[0], int(w.shape[0]), g.relu, dev)
                     y = linear_fwd(segs, _main_weight(g, w, cols),
-                                   None if b is None else b.contiguous(), g.relu, add=add)
+                                   None if b is None else b.contiguous(), g.relu, add=add,
+                                   mask_out=mk)
                     del add
                 else:
                     aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
                     segs = aggrs + ([xs[g.dst]] if g.root else [])
+                    mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev)
                     y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
-                                   g.relu)
-            lanes.escape(gi, y, *aggrs)
-            outs[gi], aggrs_by_g[gi] = y, aggrs
+                                   g.relu, mask_out=mk)
+            lanes.escape(gi, y, mk, *aggrs)
+            outs[gi], aggrs_by_g[gi], masks[gi] = y, aggrs, mk
         lanes.join()
         aggrs_all = [a for aggrs in aggrs_by_g for a in aggrs]
         ctx.spec = spec
+        ctx.masks = masks          # ReLU bits of each output (None where there is no bit form)
         ctx.has_b = [b is not None for b in wb[1::2]]
         ctx.save_for_backward(*flat[:nt], *[t for t in wb if t is not None], *aggrs_all, *outs)
         return tuple(outs)
@@ -393,7 +416,8 @@ class _HeteroLayer(torch.autograd.Function):
             if dout is None:
                 continue
             if any(g.pre):
-                pre_jobs.append((gi, g, aggrs, w, dout.contiguous(), need_w, need_b))
+                pre_jobs.append((gi, g, aggrs, w, dout.contiguous(), need_w, need_b,
+                                 ctx.masks[gi]))
                 continue
             dxs: List[Optional[torch.Tensor]] = []
             for (src, csr), a in zip(g.rels, aggrs):
@@ -416,16 +440,16 @@ class _HeteroLayer(torch.autograd.Function):
         for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
             with torch.cuda.stream(lanes.stream(li)):
                 dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w,
-                                    need_b)
+                                    need_b, mask=ctx.masks[gi])
             lanes.escape(li, dw, db)
             gwb[2 * gi], gwb[2 * gi + 1] = dw, db
         lanes.join()
         # groups with pre-projected relations (main stream): dz once, the destination update's
         # backward on it, then per pre-projected relation the K2 of dz into the projected source
         # rows and the projection's backward
-        for gi, g, aggrs, w, dout, need_w, need_b in pre_jobs:
+        for gi, g, aggrs, w, dout, need_w, need_b, mk in pre_jobs:
             gwb[2 * gi], gwb[2 * gi + 1] = _pre_group_backward(
-                g, xs, aggrs, w, dout, outs[gi], need_x, need_w, need_b, gx, pending)
+                g, xs, aggrs, w, dout, outs[gi], need_x, need_w, need_b, gx, pending, mk)
         # phase 2: K2 per target type (different targets are independent chains)
         for t in pending:
             if gx[t] is None:
@@ -474,7 +498,7 @@ def relu_grad(dout: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
 
 
 def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need_b, gx,
-                        pending):
+                        pending, mask=None):
     """Backward of a destination group with pre-projected relations: returns (dW, db) in the
     fused weight's column layout; source gradients go to ``gx`` / ``pending`` (K2 list)."""
     cols = _group_columns(g, xs)
@@ -508,7 +532,7 @@ def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need
             dxs.append(None)
     dw = torch.empty_like(w) if need_w else None
     dw_main, db = linear_bwd(segs, _main_weight(g, w, cols), dout, y if g.relu else None, dxs,
-                             need_w, need_b, dz_out=dz if g.relu else None)
+                             need_w, need_b, dz_out=dz if g.relu else None, mask=mask)
     if dw is not None:
         o = 0
         for (co, k) in seg_cols:

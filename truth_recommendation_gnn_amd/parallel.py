@@ -314,6 +314,8 @@ class HipImpl:
 
     # weighted_gather's backward awaits a gradient whose all-reduce is still in flight
     defer_grad = True
+    # linear_fwd_raw / linear_bwd_raw take the ReLU mask in bit form (mask_out= / mask=)
+    relu_masks = True
 
     def relation(self, edge_index, n_src, n_dst):
         return relation_csr(edge_index, n_src, n_dst)   # cached: the loss finds the same one
@@ -719,10 +721,24 @@ def _without_block(W: torch.Tensor, col: Tuple[int, int]) -> torch.Tensor:
     return torch.cat([W[:, :o], W[:, o + k:]], dim=1).contiguous()
 
 
-def _lin_fwd(impl, segs, W, b, add):
-    if add is None:
-        return impl.linear_fwd_raw(segs, W, b, True)
-    return impl.linear_fwd_raw(segs, W, b, True, add=add)
+def _lin_fwd(impl, segs, W, b, add, mask=None):
+    kw = {} if add is None else {"add": add}
+    if mask is not None:
+        kw["mask_out"] = mask
+    return impl.linear_fwd_raw(segs, W, b, True, **kw)
+
+
+def _relu_mask(impl, n, h, like):
+    """The bit form of a ReLU output's mask for the backward (HIP kernels only), or None."""
+    if not getattr(impl, "relu_masks", False):
+        return None
+    return ops.relu_mask_for(int(n), int(h), True, like.device)
+
+
+def _lin_bwd(impl, segs, W, dout, y, dxs, need_b, mask, **kw):
+    if mask is not None:
+        kw["mask"] = mask
+    return impl.linear_bwd_raw(segs, W, dout, y, dxs, True, need_b, **kw)
 
 
 def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x_user_full=None):
@@ -784,7 +800,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             ag = None
         Wu_main = _without_block(Wu, col_pre) if jp is not None else Wu
         st = {"x_ext": None, "a_u": [], "add": None, "y_u": h_u, "a_p": [],
-              "y_p_own": h_p_own, "y_p": h_p}
+              "y_p_own": h_p_own, "y_p": h_p, "m_u": None, "m_p": None}
 
         def user_gathers():
             # F4 user side (a pre-projected relation's mean of projected rows enters the epilogue)
@@ -802,7 +818,8 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
 
         def user_projection():
             if um:
-                st["y_u"] = _lin_fwd(impl, st["a_u"] + [h_u], Wu_main, bu, st["add"])
+                st["m_u"] = _relu_mask(impl, h_u.shape[0], Wu_main.shape[0], h_u)
+                st["y_u"] = _lin_fwd(impl, st["a_u"] + [h_u], Wu_main, bu, st["add"], st["m_u"])
 
         def post_side():
             # F5 post side on the owned slice, then its all-gather (of the next layer's projected
@@ -818,7 +835,8 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     st["a_p"].append(a)
             if not pm:
                 return
-            y_p_own = impl.linear_fwd_raw(st["a_p"] + [h_p_own], Wp, bp, True)
+            st["m_p"] = _relu_mask(impl, h_p_own.shape[0], Wp.shape[0], h_p_own)
+            y_p_own = _lin_fwd(impl, st["a_p"] + [h_p_own], Wp, bp, None, st["m_p"])
             table = y_p_own
             nxt = li + 1
             if nxt < L and pre[nxt] is not None:
@@ -855,8 +873,9 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                 user_projection()
         x_ext, a_u, add, y_u = st["x_ext"], st["a_u"], st["add"], st["y_u"]
         a_p, y_p_own, y_p = st["a_p"], st["y_p_own"], st["y_p"]
+        masks = (st["m_u"], st["m_p"])
         saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu_main,
-                      Wp, bu is not None, bp is not None, jp, col_pre))
+                      Wp, bu is not None, bp is not None, jp, col_pre, masks))
         h_u, h_p, h_p_own = y_u, y_p, y_p_own
     shard.pre_layers = [li for li in range(L) if proj[li] is not None]   # (for tests)
     # loss: the negatives sort runs while the last all-gather lands; dP's reduce-scatter (the
@@ -877,7 +896,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
     R_proj = None                               # (block, cols, grads to finish) if R carries dP
     for li in reversed(range(L)):
         (convs, um, pm, hu, hp, hpo, x_ext, a_u, a_p, yu, ypo, Wu, Wp, has_bu, has_bp, jp,
-         col_pre) = saved[li]
+         col_pre, (m_u, m_p)) = saved[li]
         need_x = li > 0                         # layer 0's inputs are the (fixed) features
         if pm and R is None:                    # B1 adjoint of the post-table all-gather
             g = G_full if G_full is not None else ypo.new_zeros(shard.n_posts_pad, ypo.shape[1])
@@ -890,12 +909,11 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             dxu.append(torch.empty_like(hu) if need_x else None)
             if jp is not None:
                 dz = torch.empty_like(G_u)
-                dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True,
-                                             has_bu, dz_out=dz)
+                dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu, m_u,
+                                  dz_out=dz)
                 pending_w = (convs, um, dW, db, col_pre)  # the block's gradient comes with dP
             else:
-                dW, db = impl.linear_bwd_raw(a_u + [hu], Wu, G_u.contiguous(), yu, dxu, True,
-                                             has_bu)
+                dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu, m_u)
                 _grads_to_params(convs, um, dW, db)
             d_hu = dxu[-1]
         else:
@@ -921,8 +939,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             g_slice = r_slice if G_own is None else r_slice + G_own
             dxp = [torch.empty_like(a) if need_x else None for a in a_p]
             dxp.append(torch.empty_like(hpo) if need_x else None)
-            dW, db = impl.linear_bwd_raw(a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, True,
-                                         has_bp)
+            dW, db = _lin_bwd(impl, a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, has_bp, m_p)
             _grads_to_params(convs, pm, dW, db)
             d_hpo = dxp[-1]
         if not need_x:
