@@ -773,7 +773,8 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         for _, et, _ in um + pm:
             if et not in shard.rels:
                 raise KeyError(f"relation {et} is not in the sharded graph")
-        # h_p is None when this layer reads the projected table (pre[li]); the slice has its width
+        # h_p is the projected table when this layer pre-projects (proj[li]); the own slice has
+        # the width of the previous post output, which the weight shapes need
         shapes = {"user": h_u, "post": h_p_own}
         (Wu, bu), (Wp, bp) = weights_of(li, shapes)
         jp = pre[li] if proj[li] is not None else None
