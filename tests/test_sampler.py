@@ -172,6 +172,46 @@ def test_sampled_minibatch_forward_backward_match_torch_on_blocks():
         torch.testing.assert_close(p.grad.cpu(), r, rtol=1e-4, atol=1e-5 * float(r.abs().max()))
 
 
+def test_sampled_blocks_with_hot_sources_backward_matches_torch():
+    """A source drawn by more sampled edges than the default split chunk (64): the blocks carry
+    no skew plan, so such a CSC row must be summed whole (a hot post under many seed users: at
+    cfg5 700+ of one block's rev_engages edges).  Regression: it was skipped as 'heavy'."""
+    from truth_recommendation_gnn_amd import HeteroSAGE, sampler, synth
+    rng = np.random.default_rng(4)
+    n_u, n_p = 600, 12
+    users = np.concatenate([np.arange(n_u), rng.integers(0, n_u, 900)])
+    posts = np.concatenate([np.zeros(n_u, dtype=np.int64), rng.integers(1, n_p, 900)])
+    eng = torch.from_numpy(np.stack([users, posts]).astype(np.int64))
+    ei = {synth.ENGAGES: eng.to(DEV), synth.REV_ENGAGES: eng.flip(0).contiguous().to(DEV)}
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+    names = []
+    for l in range(2):
+        for et, _ in rels:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (16, 16)), (f"{p}.lin_l.bias", (16,)),
+                      (f"{p}.lin_r.weight", (16, 16))]
+    params = sage_ref.init_params(names)
+    model = HeteroSAGE(16, rels, num_layers=2).to(DEV)
+    model.load_state_dict(params)
+    s = sampler.NeighborSampler({"user": n_u, "post": n_p}, ei, [et for et, _ in rels], [8, 8])
+    seeds = {"user": torch.arange(0, n_u, 2), "post": torch.arange(0, n_p)}
+    mb = s.sample(seeds, seed=2)
+    hot = int(torch.bincount(mb.blocks[-1].csr[synth.REV_ENGAGES].edge_index[0]).max())
+    assert hot > 64
+    gen = torch.Generator().manual_seed(3)
+    x = {"user": torch.randn(n_u, 16, generator=gen), "post": torch.randn(n_p, 16, generator=gen)}
+    got = sampler.forward_blocks(model, mb, {t: v.to(DEV) for t, v in x.items()})
+    ref_params = {k: v.clone().requires_grad_() for k, v in params.items()}
+    ref = _torch_blocks(ref_params, rels, mb, x)
+    wts = {t: torch.randn(ref[t].shape, generator=gen) for t in ref}
+    sum((got[t] * wts[t].to(DEV)).sum() for t in got).backward()
+    sum((ref[t] * wts[t]).sum() for t in ref).backward()
+    for name, p in model.named_parameters():
+        r = ref_params[name].grad
+        torch.testing.assert_close(p.grad.cpu(), r, rtol=1e-4,
+                                   atol=1e-5 * float(r.abs().max()), msg=name)
+
+
 def test_relabel_edge_cases_and_seed_checks():
     from truth_recommendation_gnn_amd import sampler
     ei = torch.tensor([[0, 1, 2], [1, 2, 0]], device=DEV)

@@ -108,6 +108,11 @@ def default_chunk(num_edges: int) -> int:
     return int(min(max(c, 64), 1024))
 
 
+# chunk of a plan without heavy rows when the rows were not counted: no row is ever split (the
+# gather kernels skip a row longer than the chunk in its light pass, leaving it to the heavy list)
+NO_SPLIT = 1 << 30
+
+
 @dataclasses.dataclass
 class Plan:
     chunk: int
@@ -203,7 +208,8 @@ class RelationCSR:
         dev = col.device
         perm = torch.arange(self.num_edges, dtype=torch.int32, device=dev)
         c = default_chunk(self.num_edges)
-        plan = _plan(rowptr, self.n_dst, c) if may_have_heavy_rows else Plan(c, 0, 0, None, None)
+        plan = (_plan(rowptr, self.n_dst, c) if may_have_heavy_rows
+                else Plan(NO_SPLIT, 0, 0, None, None))
         self.fwd = GroupedEdges(rowptr, col, perm, plan, self.n_dst)
         self.inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=dev)
         N.check(N.lib().hgnn_inv_degree(N.ptr(rowptr), self.n_dst, N.ptr(self.inv_deg),
@@ -240,7 +246,9 @@ class RelationCSR:
     def _bwd_from_csr(self) -> GroupedEdges:
         """CSC of a relation built ``from_csr`` (sampled blocks): its ids were produced on the
         device and are valid by construction, so the sort runs on the int32 CSR directly with no
-        validation pass and no host sync; no skew plan (block rows are short)."""
+        validation pass and no host sync.  No skew plan (it needs a host sync to size): a
+        source row is summed by one wave however long it is — a hot post drawn by many sampled
+        edges included (at cfg5, 700+ of one block's 15k rev_engages edges)."""
         g, E = self.fwd, self.num_edges
         dev = g.col.device
         rowptr = torch.empty(self.n_src + 1, dtype=torch.int32, device=dev)
@@ -252,8 +260,7 @@ class RelationCSR:
                                         N.ptr(g.perm), E, self.n_src, N.ptr(rowptr), N.ptr(col),
                                         N.ptr(perm), None, N.ptr(ws), ws.numel(),
                                         N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
-        return GroupedEdges(rowptr, col, perm, Plan(default_chunk(E), 0, 0, None, None),
-                            self.n_src)
+        return GroupedEdges(rowptr, col, perm, Plan(NO_SPLIT, 0, 0, None, None), self.n_src)
 
     @property
     def bwd_weights(self) -> torch.Tensor:

@@ -679,8 +679,8 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
         if lanes.side is not None:
             lanes.side.wait_stream(lanes.main)
     with torch.cuda.stream(lanes.stream(1)):
-        from .graph import GroupedEdges, Plan
-        negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(1 << 30, 0, 0, None, None), np_)
+        from .graph import NO_SPLIT, GroupedEdges, Plan
+        negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(NO_SPLIT, 0, 0, None, None), np_)
         if _SCORE2:
             _score_gather2(U, P, pf, negs, c, inv_e, dP)
         else:
