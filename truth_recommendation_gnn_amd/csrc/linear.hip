@@ -854,7 +854,10 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
     const float* wt_r = wt + i * LWT + 4 * g;
     for (int64_t it = 0; it <= n_my; ++it) {
       if (it < n_my) {
-        float* dz_w = dzb + (it & 1) * T * LZ + (zrow * 16 + i) * LZ + 4 * g;
+        // dz tile element (r, c) lives at r * LZ + (c ^ (((r >> 2) & 3) << 2)): the float4 writes
+        // here (lane (i, g): row 16 zrow + i, 16-B slot g of each chunk) and the b32 column reads of
+        // the X waves (lane (i, g): row 4 s + g, column 16 J + i) both hit 64 distinct banks
+        float* dz_w = dzb + (it & 1) * T * LZ + (zrow * 16 + i) * LZ + 4 * (g ^ ((i >> 2) & 3));
         if (a.dz_out) {
           const int64_t row = (blockIdx.x + it * gridDim.x) * T + zrow * 16 + i;
           if (row < a.n) {
@@ -950,13 +953,14 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
       }
       if (it >= 1) {   // wgrad of tile it-1 (its dz / X buffers were completed last barrier)
         const int b = (it - 1) & 1;
-        const float* dz_r = dzb + b * T * LZ + g * LZ + (w4 * JT) * 16 + i;
+        const float* dz_r = dzb + b * T * LZ + g * LZ + (w4 * JT) * 16;
         const float* xs_r = xsb + b * T * LX + g * LX + i;
 #pragma unroll 4
         for (int s4 = 0; s4 < T / 4; ++s4) {
           float az[JT];
 #pragma unroll
-          for (int jt = 0; jt < JT; ++jt) az[jt] = dz_r[s4 * 4 * LZ + jt * 16];
+          for (int jt = 0; jt < JT; ++jt)
+            az[jt] = dz_r[s4 * 4 * LZ + jt * 16 + (i ^ ((s4 & 3) << 2))];   // swizzled (above)
 #pragma unroll
           for (int kt = 0; kt < KC; ++kt) {
             const float bx = xs_r[s4 * 4 * LX + kt * 16];
