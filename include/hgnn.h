@@ -135,6 +135,23 @@ int hgnn_linear_fwd_add(int32_t n_seg, const float* const* xs, const int32_t* ks
                         const float* w, int32_t h, const float* bias, const float* add,
                         int32_t relu, float* out, hgnn_stream_t stream);
 
+/* The relation-weighted fused weight of one destination update (WeightedRGCN's
+ * relu(w_direct * conv_a + w_social * conv_b), train_gnn.py:187-198, folded into one K3):
+ *   w_out = [s_1 wl_1 | ... | s_R wl_R | sum_r s_r wr_r]   ([h, sum_r k_r + k_root], row-major)
+ *   b_out = sum_r s_r bl_r                                 (nullable; needs some bl_r)
+ * wl[r]: [h, k_r]; wr[r]: [h, k_root] or NULL (no lin_r; k_root = 0 when every wr is NULL);
+ * bl[r]: [h] or NULL.  n_rel <= HGNN_MAX_SEG - 1.  Bitwise the torch expression (products and sums
+ * rounded separately, in relation order).  Replaces the per-step cat/mul/add chain. */
+int hgnn_fuse_weights(int32_t n_rel, const float* const* wl, const int32_t* k,
+                      const float* const* wr, int32_t k_root, const float* const* bl,
+                      const float* scale, int32_t h, float* w_out, float* b_out,
+                      hgnn_stream_t stream);
+/* Its adjoint: dwl[r] = s_r dw[:, block r], dwr[r] = s_r dw[:, root block], dbl[r] = s_r db
+ * (every output array and entry nullable). */
+int hgnn_split_weight_grads(int32_t n_rel, const float* dw, const float* db, const int32_t* k,
+                            int32_t k_root, const float* scale, int32_t h, float* const* dwl,
+                            float* const* dwr, float* const* dbl, hgnn_stream_t stream);
+
 /* hgnn_linear_fwd_add that also writes the ReLU mask of `out` as bits (relu != 0, h % 32 == 0):
  * bit c % 32 of mask[row * (h / 32) + c / 32] = out[row][c] > 0, 16-B aligned.  The backward
  * (hgnn_linear_bwd_mask) reads h/8 bytes per row instead of out's 4h: autograd's saved ReLU

@@ -7,7 +7,51 @@ import torch.nn.functional as F
 from oracle import sage_ref
 
 
+def _torch_fused_weights(convs, msgs, x_dict):
+    """[w_1 W_l,1 | ... | w_R W_l,R | sum_r w_r W_r,r] and sum_r w_r b_r with torch ops
+    (autograd-tracked): the CPU stand-in of nn._fused_weights."""
+    w_ls, w_root, b = [], None, None
+    for name, et, wt in msgs:
+        conv = convs[name]
+        conv.materialize(x_dict[et[0]].shape[1], x_dict[et[2]].shape[1])
+        scale = (lambda t: t) if wt == 1.0 else (lambda t: t * wt)
+        w_ls.append(scale(conv.lin_l.weight))
+        if conv.lin_r is not None:
+            r = scale(conv.lin_r.weight)
+            w_root = r if w_root is None else w_root + r
+        if conv.lin_l.bias is not None:
+            bb = scale(conv.lin_l.bias)
+            b = bb if b is None else b + bb
+    parts = w_ls + ([w_root] if w_root is not None else [])
+    return torch.cat(parts, dim=1), b
+
+
+def _torch_grads_to_params(convs, msgs, dW, db):
+    """The adjoint of _torch_fused_weights, accumulated into each parameter's .grad."""
+    def acc(p, g):
+        if p.grad is None:
+            p.grad = g
+        else:
+            p.grad.add_(g)
+    off = 0
+    for name, _, wt in msgs:
+        conv = convs[name]
+        k = conv.lin_l.weight.shape[1]
+        acc(conv.lin_l.weight, (dW[:, off:off + k] * wt).contiguous())
+        if conv.lin_l.bias is not None and db is not None:
+            acc(conv.lin_l.bias, db * wt)
+        off += k
+    root = dW[:, off:]
+    for name, _, wt in msgs:
+        conv = convs[name]
+        if conv.lin_r is not None:
+            acc(conv.lin_r.weight, (root * wt).contiguous())
+
+
 class TorchImpl:
+    fused_weights = staticmethod(_torch_fused_weights)
+    grads_to_params = staticmethod(_torch_grads_to_params)
+
     def relation(self, edge_index, n_src, n_dst):
         return (edge_index, n_src, n_dst)
 

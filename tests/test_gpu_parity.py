@@ -229,6 +229,45 @@ def test_linear_bwd_variants(ks, h, mode):
         close(db, ref_db)
 
 
+@pytest.mark.parametrize("case", ["rgcn", "author", "no_root", "no_bias", "single"])
+def test_fuse_weights_bitwise_equals_torch_expression(case):
+    """hgnn_fuse_weights / hgnn_split_weight_grads against the torch expression they replace
+    ([s_1 Wl_1 | ... | s_R Wl_R | sum_r s_r Wr_r], sum_r s_r bl_r): outputs and every parameter
+    gradient bitwise equal."""
+    gen = torch.Generator().manual_seed(len(case))
+    scales = {"rgcn": [1.0, 0.75], "author": [1.75, 0.7, 0.3], "no_root": [1.0, 0.5],
+              "no_bias": [0.75, 1.0], "single": [1.0]}[case]
+    R, h = len(scales), 48
+    ks = [64, 32, 64][:R]
+    wl = [torch.randn(h, k, generator=gen).to(DEV).requires_grad_() for k in ks]
+    wr = [None if (case == "no_root" and r == 1) else
+          torch.randn(h, 64, generator=gen).to(DEV).requires_grad_() for r in range(R)]
+    bl = [None if case == "no_bias" else torch.randn(h, generator=gen).to(DEV).requires_grad_()
+          for _ in range(R)]
+    W, b = ops.fuse_weights(wl, wr, bl, scales)
+    # the torch expression (nn._fused_weights before round 2)
+    w_ls, w_root, b_ref = [], None, None
+    for r, s in enumerate(scales):
+        sc = (lambda t: t) if s == 1.0 else (lambda t, s=s: t * s)
+        w_ls.append(sc(wl[r]))
+        if wr[r] is not None:
+            w_root = sc(wr[r]) if w_root is None else w_root + sc(wr[r])
+        if bl[r] is not None:
+            b_ref = sc(bl[r]) if b_ref is None else b_ref + sc(bl[r])
+    W_ref = torch.cat(w_ls + [w_root], 1)
+    assert torch.equal(W, W_ref)
+    assert (b is None and b_ref is None) or torch.equal(b, b_ref)
+    params = [t for t in wl + wr + bl if t is not None]
+    gW = torch.randn(W.shape, generator=gen).to(DEV)
+    gb = torch.randn(h, generator=gen).to(DEV)
+    loss = (W * gW).sum() + ((b * gb).sum() if b is not None else 0)
+    got = torch.autograd.grad(loss, params)
+    loss_ref = (W_ref * gW).sum() + ((b_ref * gb).sum() if b_ref is not None else 0)
+    ref = torch.autograd.grad(loss_ref, params)
+    for a, c in zip(got, ref):
+        assert torch.equal(a, c)
+
+
 def _unpack_relu_bits(mask, n, h):
     """The lane layout of hgnn_linear_fwd_mask as a dense [n, h] bool: word row*4 + g, bit 4c + e
     is column 16c + 4g + e."""

@@ -48,6 +48,9 @@ _SIGS = {
                                       _p, _p]),
     "hgnn_linear_bwd_mask": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p,
                                       _p, _p, _p, _c_sz, _p]),
+    "hgnn_fuse_weights": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _p, _c_i32, _p, _p, _p]),
+    "hgnn_split_weight_grads": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _c_i32, _p, _p, _p,
+                                         _p]),
     "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
                                  _c_sz, _p]),

@@ -106,23 +106,17 @@ Layout = Dict[str, List[Tuple[str, EdgeType, float]]]
 
 def _fused_weights(convs: Dict[str, SAGEConv], msgs, x_dict) -> Tuple[torch.Tensor,
                                                                         Optional[torch.Tensor]]:
-    """[w_1 W_l,1 | ... | w_R W_l,R | sum_r w_r W_r,r] and sum_r w_r b_r (autograd-tracked)."""
-    w_ls, w_root, b = [], None, None
+    """[w_1 W_l,1 | ... | w_R W_l,R | sum_r w_r W_r,r] and sum_r w_r b_r (autograd-tracked),
+    built by one HIP launch from the per-conv parameters (``ops.fuse_weights``)."""
+    wl, wr, bl, scales = [], [], [], []
     for name, et, wt in msgs:
         conv = convs[name]
-        d_src = x_dict[et[0]].shape[1]
-        d_dst = x_dict[et[2]].shape[1]
-        conv.materialize(d_src, d_dst)
-        scale = (lambda t: t) if wt == 1.0 else (lambda t: t * wt)   # no kernel for weight 1
-        w_ls.append(scale(conv.lin_l.weight))
-        if conv.lin_r is not None:
-            r = scale(conv.lin_r.weight)
-            w_root = r if w_root is None else w_root + r
-        if conv.lin_l.bias is not None:
-            bb = scale(conv.lin_l.bias)
-            b = bb if b is None else b + bb
-    parts = w_ls + ([w_root] if w_root is not None else [])
-    return torch.cat(parts, dim=1), b
+        conv.materialize(x_dict[et[0]].shape[1], x_dict[et[2]].shape[1])
+        wl.append(conv.lin_l.weight)
+        wr.append(conv.lin_r.weight if conv.lin_r is not None else None)
+        bl.append(conv.lin_l.bias)
+        scales.append(wt)
+    return ops.fuse_weights(wl, wr, bl, scales)
 
 
 class _LayoutModel(torch.nn.Module):

@@ -255,6 +255,80 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     return dw, db
 
 
+# ----------------------------------------------------------------------------- fused weights
+def split_weight_grads(dW: torch.Tensor, db: Optional[torch.Tensor], ks: Sequence[int],
+                       k_root: int, scales: Sequence[float],
+                       dwl: Sequence[Optional[torch.Tensor]], dwr: Sequence[Optional[torch.Tensor]],
+                       dbl: Sequence[Optional[torch.Tensor]]) -> None:
+    """Adjoint of :func:`fuse_weights` into the given gradient buffers (entries may be None):
+    dwl[r] = s_r dW[:, block r], dwr[r] = s_r dW[:, root], dbl[r] = s_r db (one launch)."""
+    dev = dW.device
+    N.check(N.lib().hgnn_split_weight_grads(
+        len(ks), N.ptr(dW.contiguous()), N.ptr(None if db is None else db.contiguous()),
+        N.int_array(ks), int(k_root), N.float_array(scales), int(dW.shape[0]),
+        N.ptr_array(dwl), N.ptr_array(dwr), N.ptr_array(dbl), N.stream_ptr(dev)),
+        "hgnn_split_weight_grads")
+
+
+class _FuseWeights(torch.autograd.Function):
+    """``[s_1 Wl_1 | ... | s_R Wl_R | sum_r s_r Wr_r]`` and ``sum_r s_r bl_r`` in one launch
+    (``hgnn_fuse_weights``); backward: every parameter's gradient in one launch."""
+
+    @staticmethod
+    def forward(ctx, meta, *ts):
+        ks, k_root, scales, has_r, has_b = meta
+        R = len(ks)
+        wl, it = list(ts[:R]), iter(ts[R:])
+        wr = [next(it) if hr else None for hr in has_r]
+        bl = [next(it) if hb else None for hb in has_b]
+        h, dev = int(wl[0].shape[0]), wl[0].device
+        W = torch.empty(h, sum(ks) + k_root, dtype=torch.float32, device=dev)
+        b = torch.empty(h, dtype=torch.float32, device=dev) if any(has_b) else None
+        N.check(N.lib().hgnn_fuse_weights(
+            R, N.ptr_array([t.contiguous() for t in wl]), N.int_array(ks),
+            N.ptr_array([None if t is None else t.contiguous() for t in wr]), int(k_root),
+            N.ptr_array([None if t is None else t.contiguous() for t in bl]),
+            N.float_array(scales), h, N.ptr(W), N.ptr(b), N.stream_ptr(dev)),
+            "hgnn_fuse_weights")
+        ctx.meta, ctx.h, ctx.dev = meta, h, dev
+        return (W, b) if b is not None else W
+
+    @staticmethod
+    def backward(ctx, dW, db=None):
+        ks, k_root, scales, has_r, has_b = ctx.meta
+        R = len(ks)
+        need = ctx.needs_input_grad[1:]
+        new = lambda shape, i: (torch.empty(shape, dtype=torch.float32, device=ctx.dev)
+                                if need[i] else None)
+        dwl = [new((ctx.h, k), r) for r, k in enumerate(ks)]
+        i = R
+        dwr, dbl = [], []
+        for hr in has_r:
+            dwr.append(new((ctx.h, k_root), i) if hr else None)
+            i += hr
+        for hb in has_b:
+            dbl.append(new((ctx.h,), i) if hb else None)
+            i += hb
+        if dW is None:
+            dW = torch.zeros(ctx.h, sum(ks) + k_root, dtype=torch.float32, device=ctx.dev)
+        split_weight_grads(dW, db if any(has_b) else None, ks, k_root, scales, dwl, dwr, dbl)
+        return (None, *dwl, *[t for t, hr in zip(dwr, has_r) if hr],
+                *[t for t, hb in zip(dbl, has_b) if hb])
+
+
+def fuse_weights(wl: Sequence[torch.Tensor], wr: Sequence[Optional[torch.Tensor]],
+                 bl: Sequence[Optional[torch.Tensor]], scales: Sequence[float]
+                 ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Differentiable fused weight of a destination update (see ``hgnn_fuse_weights``)."""
+    ks = tuple(int(t.shape[1]) for t in wl)
+    roots = [t for t in wr if t is not None]
+    k_root = int(roots[0].shape[1]) if roots else 0
+    meta = (ks, k_root, tuple(float(x) for x in scales), tuple(t is not None for t in wr),
+            tuple(t is not None for t in bl))
+    out = _FuseWeights.apply(meta, *wl, *roots, *[t for t in bl if t is not None])
+    return out if isinstance(out, tuple) else (out, None)
+
+
 # ----------------------------------------------------------------------------- layer spec
 @dataclasses.dataclass(frozen=True)
 class DstGroup:

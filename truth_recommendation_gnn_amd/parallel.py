@@ -316,6 +316,12 @@ class HipImpl:
     defer_grad = True
     # linear_fwd_raw / linear_bwd_raw take the ReLU mask in bit form (mask_out= / mask=)
     relu_masks = True
+    # the fused weight of a destination update and its adjoint: one launch each
+    fused_weights = staticmethod(_fused_weights)
+
+    @staticmethod
+    def grads_to_params(convs, msgs, dW, db):
+        _grads_to_params(convs, msgs, dW, db)
 
     def relation(self, edge_index, n_src, n_dst):
         return relation_csr(edge_index, n_src, n_dst)   # cached: the loss finds the same one
@@ -353,25 +359,29 @@ class HipImpl:
 
 def _grads_to_params(convs, msgs, dW: torch.Tensor, db: Optional[torch.Tensor]) -> None:
     """Adjoint of ``nn._fused_weights``: W = [w_1 W_l,1 | ... | w_R W_l,R | sum_r w_r W_r,r],
-    b = sum_r w_r b_r.  Accumulates into each parameter's ``.grad``."""
-    def acc(p, g):                              # g is always a fresh tensor
-        if p.grad is None:
-            p.grad = g
-        else:
-            p.grad.add_(g)
-    off = 0
+    b = sum_r w_r b_r, split back into every parameter's gradient by one launch
+    (``ops.split_weight_grads``) and accumulated into its ``.grad``."""
+    ks, scales, dwl, dwr, dbl = [], [], [], [], []
     for name, _, wt in msgs:
         conv = convs[name]
-        k = conv.lin_l.weight.shape[1]
-        acc(conv.lin_l.weight, (dW[:, off:off + k] * wt).contiguous())
-        if conv.lin_l.bias is not None and db is not None:
-            acc(conv.lin_l.bias, db * wt)
-        off += k
-    root = dW[:, off:]
-    for name, _, wt in msgs:
+        ks.append(int(conv.lin_l.weight.shape[1]))
+        scales.append(wt)
+        dwl.append(torch.empty_like(conv.lin_l.weight))
+        dwr.append(torch.empty_like(conv.lin_r.weight) if conv.lin_r is not None else None)
+        dbl.append(torch.empty_like(conv.lin_l.bias)
+                   if conv.lin_l.bias is not None and db is not None else None)
+    k_root = int(dW.shape[1]) - sum(ks)
+    ops.split_weight_grads(dW, db, ks, k_root, scales, dwl, dwr, dbl)
+    for (name, _, _), gl, gr, gb in zip(msgs, dwl, dwr, dbl):
         conv = convs[name]
-        if conv.lin_r is not None:
-            acc(conv.lin_r.weight, (root * wt).contiguous())
+        for p, g in ((conv.lin_l.weight, gl), (conv.lin_r.weight if conv.lin_r is not None
+                                                 else None, gr), (conv.lin_l.bias, gb)):
+            if p is None or g is None:
+                continue
+            if p.grad is None:
+                p.grad = g
+            else:
+                p.grad.add_(g)
 
 
 def model_layers(model) -> List[Tuple[Dict[str, torch.nn.Module], Layout]]:
@@ -596,7 +606,7 @@ class UserShard:
                 gathered = None
             h_u_next = h_u
             if umsgs:
-                Wu, bu = _fused_weights(convs, umsgs, shapes)
+                Wu, bu = impl.fused_weights(convs, umsgs, shapes)
                 segs, x_ext = [], None
                 for _, et, _ in umsgs:
                     r = self.rels[et]
@@ -609,7 +619,7 @@ class UserShard:
                         segs.append(impl.mean_gather(x_ext, r.csr))
                 h_u_next = impl.fused_linear(segs + [h_u], Wu, bu, True)
             if pmsgs:
-                Wp, bp = _fused_weights(convs, pmsgs, shapes)
+                Wp, bp = impl.fused_weights(convs, pmsgs, shapes)
                 segs = []
                 for _, et, _ in pmsgs:
                     r = self.rels[et]
@@ -760,8 +770,8 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         if li not in fused:
             convs, layout = layers[li]
             um, pm = layout.get("user", []), layout.get("post", [])
-            fused[li] = (_fused_weights(convs, um, shapes) if um else (None, None),
-                         _fused_weights(convs, pm, shapes) if pm else (None, None))
+            fused[li] = (impl.fused_weights(convs, um, shapes) if um else (None, None),
+                         impl.fused_weights(convs, pm, shapes) if pm else (None, None))
         return fused[li]
 
     h_u, h_p, h_p_own = x_user_own, x_post, x_post[shard.p_lo:shard.p_hi]
@@ -915,7 +925,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                 pending_w = (convs, um, dW, db, col_pre)  # the block's gradient comes with dP
             else:
                 dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu, m_u)
-                _grads_to_params(convs, um, dW, db)
+                impl.grads_to_params(convs, um, dW, db)
             d_hu = dxu[-1]
         else:
             d_hu = G_u if need_x else None
@@ -935,13 +945,13 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                 dblock, _ = impl.linear_bwd_raw([ypo], block, r_slice.contiguous(), None, [g_y],
                                                 True, False)
                 dW_full = torch.cat([n_dW[:, :o], dblock, n_dW[:, o:]], dim=1)
-                _grads_to_params(n_convs, n_um, dW_full, n_db)
+                impl.grads_to_params(n_convs, n_um, dW_full, n_db)
                 r_slice = g_y
             g_slice = r_slice if G_own is None else r_slice + G_own
             dxp = [torch.empty_like(a) if need_x else None for a in a_p]
             dxp.append(torch.empty_like(hpo) if need_x else None)
             dW, db = _lin_bwd(impl, a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, has_bp, m_p)
-            _grads_to_params(convs, pm, dW, db)
+            impl.grads_to_params(convs, pm, dW, db)
             d_hpo = dxp[-1]
         if not need_x:
             break
