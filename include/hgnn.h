@@ -70,6 +70,15 @@ int hgnn_sort_pairs_i64(const int64_t* keys, const int32_t* a, const int32_t* b,
                         int64_t n_keys, int32_t* rowptr, int32_t* a_sorted, int32_t* b_sorted,
                         int32_t* d_invalid, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* Transpose of a CSR (rowptr[n_rows+1] / col[E], columns in [0, n_cols) — not re-validated)
+ * into its CSC: t_rowptr[n_cols+1], t_col[E] = the row of each entry, t_perm[E] = its CSR
+ * position, stable (rows ascending within a column); t_w (nullable) = 1/deg(row) per entry, the
+ * weight of the mean's backward.  One call instead of COO -> sort for the backward of a relation
+ * whose edges come grouped by destination (sampled blocks).  ws: hgnn_sort_pairs_ws_bytes(E, n_cols). */
+int hgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, int64_t n_rows, int64_t E,
+                       int64_t n_cols, int32_t* t_rowptr, int32_t* t_col, int32_t* t_perm,
+                       float* t_w, void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* The loss's negatives drawn and grouped in one call: exactly hgnn_uniform_i32(d_seed, E, n_keys,
  * neg_out) followed by hgnn_sort_pairs_i32(neg_out, a, NULL, E, n_keys, rowptr, a_sorted, NULL,
  * NULL, ...), with the draws computed inside the sort's first pass instead of being written and
@@ -280,6 +289,12 @@ int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_r
                           const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
                           int32_t* out_rowptr, int32_t* out_col, void* ws, size_t ws_bytes,
                           hgnn_stream_t stream);
+/* The fill phase alone, for an out_rowptr an earlier count-only hgnn_sample_neighbors call made
+ * (same rowptr, dst_ids, fanout): one launch.  Destination ids outside [0, n_rows) have no
+ * neighbours in either phase (never dereferenced). */
+int hgnn_sample_fill(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                     const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
+                     const int32_t* out_rowptr, int32_t* out_col, hgnn_stream_t stream);
 /* Next layer's node set of one type: nodes_out = [prefix (order kept), then every item id not in
  * prefix, once, in order of first appearance in items]; local_out[k] = position of items[k] in
  * nodes_out; *d_count = total.  Prefix ids distinct; ids are non-negative int32.  nodes_out holds

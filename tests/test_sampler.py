@@ -229,3 +229,28 @@ def test_relabel_edge_cases_and_seed_checks():
         s.sample({"a": torch.tensor([3])})
     mb = s.sample({"a": torch.tensor([1])}, seed=1)
     assert mb.nodes[-1]["a"].tolist() == [1]
+    with pytest.raises(ValueError):      # far outside the table: counted as degree 0, no read
+        s.sample({"a": torch.tensor([1, 10**6])})
+    with pytest.raises(ValueError):
+        s.sample({"a": torch.tensor([-1])})
+
+
+@pytest.mark.parametrize("n_src,n_dst,E", [(1, 1, 1), (37, 11, 500), (5000, 300, 60000),
+                                           (300, 5000, 7000)])
+def test_csr_transpose_equals_coo_grouping(n_src, n_dst, E):
+    """hgnn_csr_transpose (a from_csr relation's CSC, sampled blocks) against the CSC that
+    group_edges builds from the COO: same rowptr, rows and positions (stable), and 1/deg(row)
+    per entry equal to inv_deg[row]."""
+    from truth_recommendation_gnn_amd import graph
+    rng = np.random.default_rng(n_src + E)
+    ei = _rand_csr_graph(rng, n_src, n_dst, E).to(DEV)
+    full = graph.RelationCSR(ei, n_src, n_dst)
+    blk = graph.RelationCSR.from_csr(full.fwd.rowptr, full.fwd.col, n_src, n_dst,
+                                     may_have_heavy_rows=False)
+    want = graph.group_edges(full.fwd.col.long(), blk._dst_of_positions(torch.int64), n_src,
+                             n_dst)
+    got = blk.bwd
+    assert torch.equal(got.rowptr, want.rowptr)
+    assert torch.equal(got.col, want.col)
+    assert torch.equal(got.perm, want.perm)
+    assert torch.equal(blk.bwd_weights, full.inv_deg[got.col.long()])

@@ -66,6 +66,10 @@ _SIGS = {
     "hgnn_score_gather2": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _c_i64, _p,
                                     ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_sample_fill": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p, _p,
+                                  _p]),
+    "hgnn_csr_transpose": (_c_i32, [_p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz,
+                                    _p]),
     "hgnn_sample_neighbors": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p,
                                        _p, _p, _c_sz, _p]),
     "hgnn_relabel_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
@@ -137,7 +141,17 @@ def ptr(t: Optional[torch.Tensor]):
     return None if t is None else _p(t.data_ptr())
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device: torch.device):
+    """The device's current HIP stream as a raw pointer.  torch's own raw accessor (the one its
+    generated code uses) costs well under a microsecond; ``torch.cuda.current_stream`` builds a
+    Stream object per call (~5 us), which at a few hundred calls per sampled mini-batch step was
+    a visible share of the host time."""
+    if _raw_stream is not None:
+        i = device.index
+        return _p(_raw_stream(torch.cuda.current_device() if i is None else i))
     return _p(torch.cuda.current_stream(device).cuda_stream)
 
 

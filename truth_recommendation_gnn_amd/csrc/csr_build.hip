@@ -592,6 +592,59 @@ int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b,
   return check_launch("k_rowptr_from_sorted");
 }
 
+}  // extern "C"
+
+namespace hgnn {
+// CSC entry i of a CSR: its row (binary search of the CSR position t_perm[i] in rowptr) and, if
+// asked, 1/deg of that row — the weight K2 streams (graph.RelationCSR.bwd_weights).
+__global__ void k_transpose_finish(const int32_t* rowptr, int64_t n_rows, const int32_t* t_perm,
+                                   int64_t E, int32_t* t_col, float* t_w) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  const int32_t pos = t_perm[i];
+  int64_t lo = 0, hi = n_rows;   // rowptr[lo] <= pos < rowptr[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] <= pos) lo = mid; else hi = mid;
+  }
+  t_col[i] = (int32_t)lo;
+  if (t_w) t_w[i] = 1.f / (float)(rowptr[lo + 1] - rowptr[lo]);
+}
+}  // namespace hgnn
+
+extern "C" {
+
+int hgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, int64_t n_rows, int64_t E,
+                       int64_t n_cols, int32_t* t_rowptr, int32_t* t_col, int32_t* t_perm,
+                       float* t_w, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (E < 0 || E >= (int64_t(1) << 31) - 1 || n_rows < 0 || n_cols < 0 ||
+      n_cols >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "csr_transpose: E=%lld n_rows=%lld n_cols=%lld out of range",
+                (long long)E, (long long)n_rows, (long long)n_cols);
+  if (!t_rowptr || (E > 0 && (!rowptr || !col || !t_col || !t_perm)))
+    return fail(HGNN_E_ARG, "csr_transpose: null pointer");
+  if (E == 0 || n_cols == 0) {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(n_cols + 1, 256)), dim3(256), 0, stream, t_rowptr,
+                       n_cols + 1, 0);
+    return check_launch("csr_transpose(empty)");
+  }
+  if (ws_bytes < sort_ws_bytes(E)) return fail(HGNN_E_WS, "csr_transpose: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* ka = w.take<int32_t>(E);
+  const int32_t* sk = nullptr;
+  // payload: the CSR position itself (identity on the first pass), no key validation pass
+  if (int rc = radix_sort_pairs(col, ka, E, n_cols, nullptr, nullptr, t_perm, nullptr, w, stream,
+                                &sk))
+    return rc;
+  hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_cols + 1, 256)), dim3(256), 0, stream, sk,
+                     E, n_cols, t_rowptr);
+  if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
+  hipLaunchKernelGGL(k_transpose_finish, dim3(cdiv(E, 256)), dim3(256), 0, stream, rowptr, n_rows,
+                     t_perm, E, t_col, t_w);
+  return check_launch("k_transpose_finish");
+}
+
 int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E, int64_t n_keys,
                              int32_t* neg_out, int32_t* rowptr, int32_t* a_sorted, void* ws,
                              size_t ws_bytes, hgnn_stream_t stream_) {

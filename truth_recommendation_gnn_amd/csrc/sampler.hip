@@ -36,24 +36,31 @@ __device__ __forceinline__ uint32_t draw(uint64_t seed, int32_t node, int r, uin
   return (uint32_t)(((h >> 32) * (uint64_t)m) >> 32);
 }
 
-__global__ void k_sample_count(const int32_t* rowptr, const int32_t* dst_ids, int64_t n,
-                               int32_t fanout, int32_t* counts) {
+// A destination id outside [0, n_rows) has no neighbours (count 0): the caller validates the ids
+// it was given with the first read-back it makes anyway, and nothing is read out of bounds.
+__global__ void k_sample_count(const int32_t* rowptr, int64_t n_rows, const int32_t* dst_ids,
+                               int64_t n, int32_t fanout, int32_t* counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t d = dst_ids[i];
+  if (d < 0 || d >= n_rows) {
+    counts[i] = 0;
+    return;
+  }
   const int32_t deg = rowptr[d + 1] - rowptr[d];
   counts[i] = (fanout < 0 || deg <= fanout) ? deg : fanout;
 }
 
 __global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, const int32_t* col,
-                                                     const int32_t* dst_ids, int64_t n,
-                                                     int32_t fanout, uint64_t seed,
+                                                     int64_t n_rows, const int32_t* dst_ids,
+                                                     int64_t n, int32_t fanout, uint64_t seed,
                                                      const int32_t* out_rowptr,
                                                      int32_t* out_col) {
   const int lane = threadIdx.x & 63;
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= n) return;
   const int32_t d = dst_ids[w];
+  if (d < 0 || d >= n_rows) return;   // counted 0 by k_sample_count
   const int32_t beg = rowptr[d], deg = rowptr[d + 1] - beg;
   int32_t* out = out_col + out_rowptr[w];
   if (fanout < 0 || deg <= fanout) {   // keep every neighbour, in CSR order
@@ -185,12 +192,26 @@ int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_r
   int32_t* counts = w.take<int32_t>(n_dst);
   void* scan_ws = w.take<char>(scan_b);
   hipLaunchKernelGGL(k_sample_count, dim3((unsigned)cdiv(n_dst, 256)), dim3(256), 0, stream,
-                     rowptr, dst_ids, n_dst, fanout, counts);
+                     rowptr, n_rows, dst_ids, n_dst, fanout, counts);
   if (int rc = check_launch("k_sample_count")) return rc;
   if (int rc = exclusive_scan_i32(counts, out_rowptr, n_dst, scan_ws, &scan_b, stream)) return rc;
   if (!out_col) return HGNN_OK;   // count-only call
-  hipLaunchKernelGGL(k_sample_fill, dim3((unsigned)cdiv(n_dst, 4)), dim3(256), 0, stream, rowptr,
-                     col, dst_ids, n_dst, fanout, seed, out_rowptr, out_col);
+  return hgnn_sample_fill(rowptr, col, n_rows, dst_ids, n_dst, fanout, seed, out_rowptr, out_col,
+                          stream_);
+}
+
+int hgnn_sample_fill(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                     const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
+                     const int32_t* out_rowptr, int32_t* out_col, hgnn_stream_t stream) {
+  if (n_rows < 0 || n_dst < 0 || fanout == 0 || fanout > 64)
+    return fail(HGNN_E_ARG, "sample_fill: n_rows=%lld n_dst=%lld fanout=%d (1..64 or <0)",
+                (long long)n_rows, (long long)n_dst, fanout);
+  if (n_dst == 0) return HGNN_OK;
+  if (!rowptr || !dst_ids || !out_rowptr || !out_col)
+    return fail(HGNN_E_ARG, "sample_fill: null pointer");
+  hipLaunchKernelGGL(k_sample_fill, dim3((unsigned)cdiv(n_dst, 4)), dim3(256), 0,
+                     as_stream(stream), rowptr, col, n_rows, dst_ids, n_dst, fanout, seed,
+                     out_rowptr, out_col);
   return check_launch("k_sample_fill");
 }
 

@@ -126,7 +126,8 @@ class Plan:
 class GroupedEdges:
     rowptr: torch.Tensor     # int32 [n_rows+1]
     col: torch.Tensor        # int32 [E]
-    perm: torch.Tensor       # int32 [E] original edge id of each CSR position
+    perm: Optional[torch.Tensor]   # int32 [E] original edge id of each CSR position (None: the
+    #                                identity, for edges that came grouped — RelationCSR.from_csr)
     plan: Plan
     n_rows: int
 
@@ -189,10 +190,19 @@ class RelationCSR:
         self.chunk = chunk
         self._ei = edge_index
         self.fwd = group_edges(edge_index[1], edge_index[0], self.n_dst, self.n_src, chunk)
-        self.inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=edge_index.device)
-        N.check(N.lib().hgnn_inv_degree(N.ptr(self.fwd.rowptr), self.n_dst, N.ptr(self.inv_deg),
-                                        N.stream_ptr(edge_index.device)), "hgnn_inv_degree")
+        self._inv_deg: Optional[torch.Tensor] = None
         self._bwd: Optional[GroupedEdges] = None
+
+    @property
+    def inv_deg(self) -> torch.Tensor:
+        """1/deg per destination row (0 for an empty row), on first use."""
+        if self._inv_deg is None:
+            dev = self.fwd.rowptr.device
+            self._inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=dev)
+            N.check(N.lib().hgnn_inv_degree(N.ptr(self.fwd.rowptr), self.n_dst,
+                                            N.ptr(self._inv_deg), N.stream_ptr(dev)),
+                    "hgnn_inv_degree")
+        return self._inv_deg
 
     @classmethod
     def from_csr(cls, rowptr: torch.Tensor, col: torch.Tensor, n_src: int, n_dst: int,
@@ -205,15 +215,13 @@ class RelationCSR:
         self.n_src, self.n_dst = int(n_src), int(n_dst)
         self.num_edges = int(col.numel())
         self.chunk = None
-        dev = col.device
-        perm = torch.arange(self.num_edges, dtype=torch.int32, device=dev)
         c = default_chunk(self.num_edges)
         plan = (_plan(rowptr, self.n_dst, c) if may_have_heavy_rows
                 else Plan(NO_SPLIT, 0, 0, None, None))
-        self.fwd = GroupedEdges(rowptr, col, perm, plan, self.n_dst)
-        self.inv_deg = torch.empty(self.n_dst, dtype=torch.float32, device=dev)
-        N.check(N.lib().hgnn_inv_degree(N.ptr(rowptr), self.n_dst, N.ptr(self.inv_deg),
-                                        N.stream_ptr(dev)), "hgnn_inv_degree")
+        # nothing else is launched here: a sampled mini-batch builds eight of these per step, and
+        # 1/deg and the CSC are needed only by the backward (layers whose input has a gradient)
+        self.fwd = GroupedEdges(rowptr, col, None, plan, self.n_dst)
+        self._inv_deg = None
         self._ei = None
         self._bwd = None
         self._from_csr = True
@@ -244,22 +252,25 @@ class RelationCSR:
         return self._bwd
 
     def _bwd_from_csr(self) -> GroupedEdges:
-        """CSC of a relation built ``from_csr`` (sampled blocks): its ids were produced on the
-        device and are valid by construction, so the sort runs on the int32 CSR directly with no
-        validation pass and no host sync.  No skew plan (it needs a host sync to size): a
-        source row is summed by one wave however long it is — a hot post drawn by many sampled
-        edges included (at cfg5, 700+ of one block's 15k rev_engages edges)."""
+        """CSC of a relation built ``from_csr`` (sampled blocks), in one call
+        (``hgnn_csr_transpose``): the ids were produced on the device and are valid by
+        construction, so there is no validation pass and no host sync, and the same call writes
+        the per-position 1/deg that K2 streams (``bwd_weights``).  No skew plan (it needs a host
+        sync to size): a source row is summed by one wave however long it is — a hot post drawn
+        by many sampled edges included (at cfg5, 700+ of one block's 15k rev_engages edges)."""
         g, E = self.fwd, self.num_edges
         dev = g.col.device
         rowptr = torch.empty(self.n_src + 1, dtype=torch.int32, device=dev)
         col = torch.empty(E, dtype=torch.int32, device=dev)
         perm = torch.empty(E, dtype=torch.int32, device=dev)
+        w = torch.empty(E, dtype=torch.float32, device=dev)
         lib = N.lib()
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, self.n_src), dev)
-        N.check(lib.hgnn_sort_pairs_i32(N.ptr(g.col), N.ptr(self._dst_of_positions(torch.int32)),
-                                        N.ptr(g.perm), E, self.n_src, N.ptr(rowptr), N.ptr(col),
-                                        N.ptr(perm), None, N.ptr(ws), ws.numel(),
-                                        N.stream_ptr(dev)), "hgnn_sort_pairs_i32")
+        N.check(lib.hgnn_csr_transpose(N.ptr(g.rowptr), N.ptr(g.col), self.n_dst, E, self.n_src,
+                                       N.ptr(rowptr), N.ptr(col), N.ptr(perm), N.ptr(w),
+                                       N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                "hgnn_csr_transpose")
+        self._bwd_w = w
         return GroupedEdges(rowptr, col, perm, Plan(NO_SPLIT, 0, 0, None, None), self.n_src)
 
     @property
@@ -268,7 +279,9 @@ class RelationCSR:
         lookup of inv_deg[dst] per edge."""
         w = getattr(self, "_bwd_w", None)
         if w is None:
-            g = self.bwd
+            g = self.bwd                  # (a from_csr relation's CSC build sets _bwd_w too)
+            w = getattr(self, "_bwd_w", None)
+        if w is None:
             w = self.inv_deg[g.col.long()].contiguous() if self.num_edges else \
                 torch.empty(0, dtype=torch.float32, device=self.inv_deg.device)
             self._bwd_w = w

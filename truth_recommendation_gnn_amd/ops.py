@@ -14,6 +14,7 @@ gradient sums the reference's autograd would do with separate add kernels happen
 """
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -339,6 +340,26 @@ class DstGroup:
     # per relation: project the SOURCE table first (lin_l(mean x_j) == mean(lin_l x_j), bias
     # kept in the destination update) — see use_pre_projection
     pre: Tuple[bool, ...] = ()
+    # destinations = the first n_root rows of the dst type's table (a sampled block: the next
+    # layer's nodes lead the current ones); None: the whole table
+    n_root: Optional[int] = None
+
+
+def _root(g: DstGroup, xs) -> torch.Tensor:
+    """The destination rows' own features (the root segment): a prefix view in a block."""
+    x = xs[g.dst]
+    return x if g.n_root is None else x[:g.n_root]
+
+
+def _root_grad_buffer(g: DstGroup, xs, gx) -> torch.Tensor:
+    """Allocates gx[dst] and returns the view the root segment's dgrad writes (a block's prefix;
+    the rows after it are zero until the K2s add into them)."""
+    x = xs[g.dst]
+    if g.n_root is None:
+        gx[g.dst] = torch.empty_like(x)
+        return gx[g.dst]
+    gx[g.dst] = torch.zeros_like(x)
+    return gx[g.dst][:g.n_root]
 
 
 PRE_PROJECTION = os.environ.get("HGNN_PREPROJECT", "1") == "1"
@@ -385,16 +406,20 @@ class _Lanes:
     enabled = os.environ.get("HGNN_STREAMS", "0") == "1"
 
     def __init__(self, dev: torch.device, n_chains: int, force: bool = False):
-        self.main = torch.cuda.current_stream(dev)
-        self.side = None
+        self.main = self.side = None
         if (self.enabled or force) and n_chains > 1:
+            self.main = torch.cuda.current_stream(dev)
             self.side = _Lanes._side.get(dev)
             if self.side is None:
                 self.side = _Lanes._side[dev] = torch.cuda.Stream(dev)
             self.side.wait_stream(self.main)
 
-    def stream(self, i: int):
-        return self.side if (self.side is not None and i % 2 == 1) else self.main
+    def ctx(self, i: int):
+        """The stream context of chain i: a no-op with one lane (no Stream objects built — at a
+        few hundred per sampled mini-batch step they were a visible share of its host time)."""
+        if self.side is None:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.side if i % 2 == 1 else self.main)
 
     def escape(self, i: int, *tensors):
         if self.side is not None and i % 2 == 1:
@@ -419,7 +444,7 @@ class _HeteroLayer(torch.autograd.Function):
         lanes = _Lanes(dev, ng)
         for gi, g in enumerate(spec.groups):   # destination types are independent chains
             w, b = wb[2 * gi], wb[2 * gi + 1]
-            with torch.cuda.stream(lanes.stream(gi)):
+            with lanes.ctx(gi):
                 if any(g.pre):
                     # pre-projected relations: P = x_src W_r^T, gathered (means summed into
                     # one [N_dst, h] input) and added in the destination update's epilogue
@@ -432,15 +457,15 @@ class _HeteroLayer(torch.autograd.Function):
                             del P
                         else:
                             aggrs.append(gather_mean(xs[src], csr))
-                    segs = aggrs + ([xs[g.dst]] if g.root else [])
-                    mk = relu_mask_for(xs[g.dst].shape[0], int(w.shape[0]), g.relu, dev)
+                    segs = aggrs + ([_root(g, xs)] if g.root else [])
+                    mk = relu_mask_for(_root(g, xs).shape[0], int(w.shape[0]), g.relu, dev)
                     y = linear_fwd(segs, _main_weight(g, w, cols),
                                    None if b is None else b.contiguous(), g.relu, add=add,
                                    mask_out=mk)
                     del add
                 else:
                     aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
-                    segs = aggrs + ([xs[g.dst]] if g.root else [])
+                    segs = aggrs + ([_root(g, xs)] if g.root else [])
                     mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev)
                     y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
                                    g.relu, mask_out=mk)
@@ -503,16 +528,12 @@ class _HeteroLayer(torch.autograd.Function):
                     dxs.append(None)
             segs = list(aggrs)
             if g.root:
-                segs.append(xs[g.dst])
-                if need_x[g.dst]:
-                    gx[g.dst] = torch.empty_like(xs[g.dst])
-                    dxs.append(gx[g.dst])
-                else:
-                    dxs.append(None)
+                segs.append(_root(g, xs))
+                dxs.append(_root_grad_buffer(g, xs, gx) if need_x[g.dst] else None)
             jobs.append((gi, g, segs, w, dout.contiguous(), dxs, need_w, need_b))
         lanes = _Lanes(saved[0].device, len(jobs))
         for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
-            with torch.cuda.stream(lanes.stream(li)):
+            with lanes.ctx(li):
                 dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w,
                                     need_b, mask=ctx.masks[gi])
             lanes.escape(li, dw, db)
@@ -530,7 +551,7 @@ class _HeteroLayer(torch.autograd.Function):
                 gx[t] = torch.zeros_like(xs[t])
         lanes = _Lanes(saved[0].device, len(pending))
         for li, (t, items) in enumerate(pending.items()):
-            with torch.cuda.stream(lanes.stream(li)):
+            with lanes.ctx(li):
                 for dA, csr in items:
                     scatter_mean_bwd(dA, csr, out=gx[t])
         lanes.join()
@@ -595,11 +616,11 @@ def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need
         else:
             dxs.append(None)
     if g.root:
-        segs.append(xs[g.dst])
+        segs.append(_root(g, xs))
         o = cols[-1][0] + cols[-1][1] if cols else 0
         seg_cols.append((o, int(w.shape[1]) - o))
         if need_x[g.dst]:
-            d_root = torch.empty_like(xs[g.dst])
+            d_root = torch.empty_like(segs[-1])
             dxs.append(d_root)
         else:
             d_root = None
@@ -613,7 +634,12 @@ def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need
             dw[:, co:co + k].copy_(dw_main[:, o:o + k])
             o += k
     if g.root and d_root is not None:
-        gx[g.dst] = d_root if gx[g.dst] is None else gx[g.dst].add_(d_root)
+        if g.n_root is not None:
+            if gx[g.dst] is None:
+                gx[g.dst] = torch.zeros_like(xs[g.dst])
+            gx[g.dst][:g.n_root].add_(d_root)
+        else:
+            gx[g.dst] = d_root if gx[g.dst] is None else gx[g.dst].add_(d_root)
     # pre-projected relations: dP = K2(dz) over the CSC, then P = x_src W_r^T's backward
     for (src, csr), pre, (o, k) in zip(g.rels, g.pre, cols):
         if not pre:
@@ -721,7 +747,7 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     # then the two dP gathers, each edge's weight recomputed from <U[u], P[post]>
     # (hgnn_score_gather); pass A (loss + dU) needs none of it.
     lanes = _Lanes(dev, 2)
-    with torch.cuda.stream(lanes.stream(1)):
+    with lanes.ctx(1):
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
         if draw is not None:
             # draws computed in the sort's first pass; `neg` (position order) for the scoring pass
@@ -752,7 +778,7 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
         ready()
         if lanes.side is not None:
             lanes.side.wait_stream(lanes.main)
-    with torch.cuda.stream(lanes.stream(1)):
+    with lanes.ctx(1):
         from .graph import NO_SPLIT, GroupedEdges, Plan
         negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(NO_SPLIT, 0, 0, None, None), np_)
         if _SCORE2:

@@ -77,21 +77,21 @@ class NeighborSampler:
                                           N.stream_ptr(dev)), "hgnn_sample_neighbors")
         return rowptr, ws
 
-    def _fill(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int, rowptr, ws,
+    def _fill(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int, rowptr,
               total: int):
-        """Phase 2: the sampled source ids (global) into a ``total``-long column array."""
+        """Phase 2 (one launch, on phase 1's rowptr): the sampled source ids (global) into a
+        ``total``-long column array."""
         g = self.csr[et].fwd
         lib, dev = N.lib(), self.device
         col = torch.empty(total, dtype=torch.int32, device=dev)
-        N.check(lib.hgnn_sample_neighbors(N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst),
-                                          int(dst.numel()), fanout, seed, N.ptr(rowptr),
-                                          N.ptr(col), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                "hgnn_sample_neighbors")
+        N.check(lib.hgnn_sample_fill(N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(dst),
+                                     int(dst.numel()), fanout, seed, N.ptr(rowptr), N.ptr(col),
+                                     N.stream_ptr(dev)), "hgnn_sample_fill")
         return col
 
     def _sample(self, et: EdgeType, dst: torch.Tensor, fanout: int, seed: int):
-        rowptr, ws = self._count(et, dst, fanout)
-        return rowptr, self._fill(et, dst, fanout, seed, rowptr, ws, int(rowptr[-1]))
+        rowptr, _ = self._count(et, dst, fanout)
+        return rowptr, self._fill(et, dst, fanout, seed, rowptr, int(rowptr[-1]))
 
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
         lib, dev = N.lib(), self.device
@@ -110,26 +110,32 @@ class NeighborSampler:
         checks = []
         for t, s in seeds.items():
             s = _i32(s.to(self.device))
-            if s.numel():    # [min, max, any duplicate]: read back for all types in one sync
+            if s.numel():    # [min, max, any duplicate], read back with the first hop's totals
                 ss = torch.sort(s).values
                 dup = (ss[1:] == ss[:-1]).any().to(s.dtype)
                 checks.append((t, torch.stack([ss[0], ss[-1], dup])))
             cur[t] = s
-        if checks:
-            vals = torch.stack([c for _, c in checks]).tolist()
-            for (t, _), (lo, hi, dup) in zip(checks, vals):
-                if lo < 0 or hi >= self.num_nodes[t]:
-                    raise ValueError(f"seed ids of type {t!r} out of range")
-                if dup:
-                    raise ValueError(f"seed ids of type {t!r} must be distinct")
         nodes, blocks = [cur], []
         for hop, fanout in enumerate(self.fanouts):
             hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
             ets = [et for et in self.relations if et[2] in cur]
+            # phase 1 counts ids outside the table as degree 0 (never dereferenced), so the seed
+            # check rides on this hop's one read-back and raises before anything uses the counts
             counted = {et: self._count(et, cur[et[2]], fanout) for et in ets}
-            totals = (torch.stack([counted[et][0][-1] for et in ets]).tolist() if ets else [])
+            back = [counted[et][0][-1:] for et in ets]
+            if hop == 0:
+                back += [c for _, c in checks]
+            vals = torch.cat(back).tolist() if back else []
+            totals = vals[:len(ets)]
+            if hop == 0:
+                for i, (t, _) in enumerate(checks):
+                    lo, hi, dup = vals[len(ets) + 3 * i:len(ets) + 3 * i + 3]
+                    if lo < 0 or hi >= self.num_nodes[t]:
+                        raise ValueError(f"seed ids of type {t!r} out of range")
+                    if dup:
+                        raise ValueError(f"seed ids of type {t!r} must be distinct")
             sampled = {et: (counted[et][0], self._fill(et, cur[et[2]], fanout, hop_seed,
-                                                       counted[et][0], counted[et][1], tot))
+                                                       counted[et][0], tot))
                        for et, tot in zip(ets, totals)}          # one sync for every relation
             types = sorted(set(cur) | {et[0] for et in sampled})
             relabeled = {}
@@ -168,16 +174,20 @@ def forward_blocks(model: HeteroSAGE, batch: MiniBatch,
         raise ValueError(f"{len(batch.blocks)} blocks for a {len(model.layers)}-layer model")
     h = {t: x_dict[t].index_select(0, ids.long()) for t, ids in batch.nodes[0].items()}
     for convs, blk in zip(model.layers, batch.blocks):
-        out = {}
+        # one fused hetero layer per block (ops.hetero_layer: per destination type the K1 means of
+        # its relations and one K3 over [aggr..., root prefix], one autograd node for the layer)
+        out, groups, weights = {}, [], []
         for dst, n_dst in blk.n_dst.items():
             msgs = [("__".join(et), et, w) for et, w in model.relations
                     if et[2] == dst and et in blk.csr]
-            root = h[dst][:n_dst]
             if not msgs:                      # no relation into this type: kept as is
-                out[dst] = root
+                out[dst] = h[dst][:n_dst]
                 continue
-            W, b = _fused_weights(convs, msgs, h)
-            aggrs = [ops.mean_gather(h[et[0]], blk.csr[et]) for _, et, _ in msgs]
-            out[dst] = ops.fused_linear(aggrs + [root.contiguous()], W, b, True)
+            rels = tuple((et[0], blk.csr[et]) for _, et, _ in msgs)
+            groups.append(ops.DstGroup(dst, rels, True, True, (), n_root=n_dst))
+            weights.append(_fused_weights(convs, msgs, h))
+        if groups:
+            out.update(ops.hetero_layer(ops.LayerSpec(tuple(sorted(h)), tuple(groups)), h,
+                                        weights))
         h = out
     return h
