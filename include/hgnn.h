@@ -295,6 +295,22 @@ int hgnn_sample_neighbors(const int32_t* rowptr, const int32_t* col, int64_t n_r
 int hgnn_sample_fill(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                      const int32_t* dst_ids, int64_t n_dst, int32_t fanout, uint64_t seed,
                      const int32_t* out_rowptr, int32_t* out_col, hgnn_stream_t stream);
+/* One hop of the sampler over every relation into the frontier (at most 8), one launch per phase
+ * (hgnn_sample_neighbors / hgnn_sample_fill per relation, batched; the samples are identical).
+ * Count: out_rowptrs[r][n_dst[r]+1] zero-based per relation, d_totals[r] (device int32) = its
+ * size; ws: hgnn_sample_hop_ws_bytes(sum of n_dst).  Fill: relation r's sample into out_cols[r]
+ * (d_totals[r] entries).  Host arrays of n_rel entries; one fanout and seed for the hop. */
+size_t hgnn_sample_hop_ws_bytes(int64_t n_total_dst);
+int hgnn_sample_hop_count(int32_t n_rel, const int32_t* const* rowptrs, const int64_t* n_rows,
+                          const int32_t* const* dst_ids, const int64_t* n_dst, int32_t fanout,
+                          int32_t* const* out_rowptrs, int32_t* d_totals, void* ws,
+                          size_t ws_bytes, hgnn_stream_t stream);
+int hgnn_sample_hop_fill(int32_t n_rel, const int32_t* const* rowptrs, const int32_t* const* cols,
+                         const int64_t* n_rows, const int32_t* const* dst_ids,
+                         const int64_t* n_dst, int32_t fanout, uint64_t seed,
+                         const int32_t* const* out_rowptrs, int32_t* const* out_cols,
+                         hgnn_stream_t stream);
+
 /* Next layer's node set of one type: nodes_out = [prefix (order kept), then every item id not in
  * prefix, once, in order of first appearance in items]; local_out[k] = position of items[k] in
  * nodes_out; *d_count = total.  Prefix ids distinct; ids are non-negative int32.  nodes_out holds

@@ -254,3 +254,33 @@ def test_csr_transpose_equals_coo_grouping(n_src, n_dst, E):
     assert torch.equal(got.col, want.col)
     assert torch.equal(got.perm, want.perm)
     assert torch.equal(blk.bwd_weights, full.inv_deg[got.col.long()])
+
+
+@pytest.mark.parametrize("fanout", [3, 10, -1])
+def test_hop_batch_equals_per_relation_sampling(fanout):
+    """hgnn_sample_hop_count/_fill (every relation of a hop in one launch per phase) give, per
+    relation, exactly the rowptr and sample of hgnn_sample_neighbors on its own — including a
+    relation with no destinations and ids outside the table (counted as degree 0)."""
+    from truth_recommendation_gnn_amd import sampler
+    rng = np.random.default_rng(7)
+    ei = {("a", "r1", "b"): _rand_csr_graph(rng, 400, 300, 9000),
+          ("b", "r2", "b"): _rand_csr_graph(rng, 300, 300, 4000),
+          ("a", "r3", "a"): _rand_csr_graph(rng, 400, 400, 100),
+          ("b", "r4", "a"): _rand_csr_graph(rng, 300, 400, 7000)}
+    ets = list(ei)
+    s = sampler.NeighborSampler({"a": 400, "b": 300}, {k: v.to(DEV) for k, v in ei.items()},
+                                ets, [fanout])
+    cur = {"b": torch.from_numpy(rng.permutation(300)[:120].astype(np.int32)).to(DEV),
+           "a": torch.empty(0, dtype=torch.int32, device=DEV)}
+    rowptr, cols, totals = s._hop(ets, cur, fanout, 99, [], 1)
+    o = 0
+    for et in ets:
+        rp, col = s._sample(et, cur[et[2]], fanout, 99)
+        assert torch.equal(rowptr[et], rp), et
+        assert totals[et] == int(rp[-1])
+        assert torch.equal(cols[o:o + totals[et]], col), et
+        o += totals[et]
+    bad = {"b": torch.tensor([5, 300, -2, 7], dtype=torch.int32, device=DEV)}
+    rowptr, cols, totals = s._hop([("a", "r1", "b")], bad, fanout, 1, [], 1)
+    deg = rowptr[("a", "r1", "b")].diff().tolist()
+    assert deg[1] == 0 and deg[2] == 0

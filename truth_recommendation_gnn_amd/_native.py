@@ -66,6 +66,10 @@ _SIGS = {
     "hgnn_score_gather2": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _c_i64, _p,
                                     ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_sample_hop_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_sample_hop_count": (_c_i32, [_c_i32, _p, _p, _p, _p, _c_i32, _p, _p, _p, _c_sz, _p]),
+    "hgnn_sample_hop_fill": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _c_i32, ctypes.c_uint64, _p,
+                                      _p, _p]),
     "hgnn_sample_fill": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p, _p,
                                   _p]),
     "hgnn_csr_transpose": (_c_i32, [_p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz,
@@ -177,21 +181,28 @@ def workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 
 def ptr_array(ts: Sequence[Optional[torch.Tensor]]):
-    arr = (_p * MAX_SEG)()
+    arr = (_p * max(MAX_SEG, len(ts)))()
     for i, t in enumerate(ts):
         arr[i] = None if t is None else t.data_ptr()
     return arr
 
 
 def int_array(vals: Sequence[int]):
-    arr = (_c_i32 * MAX_SEG)()
+    arr = (_c_i32 * max(MAX_SEG, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr
+
+
+def i64_array(vals: Sequence[int]):
+    arr = (_c_i64 * max(MAX_SEG, len(vals)))()
     for i, v in enumerate(vals):
         arr[i] = int(v)
     return arr
 
 
 def float_array(vals: Sequence[float]):
-    arr = (ctypes.c_float * MAX_SEG)()
+    arr = (ctypes.c_float * max(MAX_SEG, len(vals)))()
     for i, v in enumerate(vals):
         arr[i] = float(v)
     return arr

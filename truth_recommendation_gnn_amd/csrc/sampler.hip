@@ -22,6 +22,8 @@
 
 namespace hgnn {
 
+constexpr int kHopMax = 8;   // relations per hop (hgnn_sample_hop_*)
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -38,31 +40,27 @@ __device__ __forceinline__ uint32_t draw(uint64_t seed, int32_t node, int r, uin
 
 // A destination id outside [0, n_rows) has no neighbours (count 0): the caller validates the ids
 // it was given with the first read-back it makes anyway, and nothing is read out of bounds.
+__device__ __forceinline__ int32_t sample_count(const int32_t* rowptr, int64_t n_rows, int32_t d,
+                                                int32_t fanout) {
+  if (d < 0 || d >= n_rows) return 0;
+  const int32_t deg = rowptr[d + 1] - rowptr[d];
+  return (fanout < 0 || deg <= fanout) ? deg : fanout;
+}
+
 __global__ void k_sample_count(const int32_t* rowptr, int64_t n_rows, const int32_t* dst_ids,
                                int64_t n, int32_t fanout, int32_t* counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const int32_t d = dst_ids[i];
-  if (d < 0 || d >= n_rows) {
-    counts[i] = 0;
-    return;
-  }
-  const int32_t deg = rowptr[d + 1] - rowptr[d];
-  counts[i] = (fanout < 0 || deg <= fanout) ? deg : fanout;
+  counts[i] = sample_count(rowptr, n_rows, dst_ids[i], fanout);
 }
 
-__global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, const int32_t* col,
-                                                     int64_t n_rows, const int32_t* dst_ids,
-                                                     int64_t n, int32_t fanout, uint64_t seed,
-                                                     const int32_t* out_rowptr,
-                                                     int32_t* out_col) {
+// One wave: the sample of destination d into out[0 .. count).
+__device__ __forceinline__ void sample_fill(const int32_t* rowptr, const int32_t* col,
+                                            int64_t n_rows, int32_t d, int32_t fanout,
+                                            uint64_t seed, int32_t* out) {
   const int lane = threadIdx.x & 63;
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (w >= n) return;
-  const int32_t d = dst_ids[w];
-  if (d < 0 || d >= n_rows) return;   // counted 0 by k_sample_count
+  if (d < 0 || d >= n_rows) return;   // counted 0
   const int32_t beg = rowptr[d], deg = rowptr[d + 1] - beg;
-  int32_t* out = out_col + out_rowptr[w];
   if (fanout < 0 || deg <= fanout) {   // keep every neighbour, in CSR order
     for (int32_t j = lane; j < deg; j += 64) out[j] = col[beg + j];
     return;
@@ -76,6 +74,66 @@ __global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, cons
     if (lane == r) chosen = taken ? jj : t;
   }
   if (lane < fanout) out[lane] = col[beg + chosen];
+}
+
+__global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, const int32_t* col,
+                                                     int64_t n_rows, const int32_t* dst_ids,
+                                                     int64_t n, int32_t fanout, uint64_t seed,
+                                                     const int32_t* out_rowptr,
+                                                     int32_t* out_col) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= n) return;
+  sample_fill(rowptr, col, n_rows, dst_ids[w], fanout, seed, out_col + out_rowptr[w]);
+}
+
+// ---- one hop over every relation into the frontier: one launch per phase ------------------------
+// Destinations of all relations concatenated (relation r owns [off[r], off[r+1])); the counts are
+// scanned once over the concatenation and split back into zero-based per-relation rowptrs.
+struct HopTab {
+  const int32_t* rowptr[kHopMax];
+  const int32_t* col[kHopMax];
+  const int32_t* dst[kHopMax];
+  int32_t* out_rowptr[kHopMax];
+  int32_t* out_col[kHopMax];
+  int64_t n_rows[kHopMax];
+  int64_t off[kHopMax + 1];
+  int32_t n_rel;
+  int32_t fanout;
+  uint64_t seed;
+};
+
+__device__ __forceinline__ int hop_rel(const HopTab& t, int64_t i) {
+  int r = 0;
+  while (r + 1 < t.n_rel && i >= t.off[r + 1]) ++r;
+  return r;
+}
+
+__global__ void k_hop_count(const HopTab t, int32_t* counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.off[t.n_rel]) return;
+  const int r = hop_rel(t, i);
+  counts[i] = sample_count(t.rowptr[r], t.n_rows[r], t.dst[r][i - t.off[r]], t.fanout);
+}
+
+// entry j <= n_r of relation r sits at g = off[r] + r + j
+__global__ void k_hop_rowptr(const HopTab t, const int32_t* pre, int32_t* totals) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= t.off[t.n_rel] + t.n_rel) return;
+  int r = 0;
+  while (r + 1 < t.n_rel && g >= t.off[r + 1] + r + 1) ++r;
+  const int64_t j = g - t.off[r] - r;
+  const int32_t v = pre[t.off[r] + j] - pre[t.off[r]];
+  t.out_rowptr[r][j] = v;
+  if (j == t.off[r + 1] - t.off[r]) totals[r] = v;
+}
+
+__global__ void __launch_bounds__(256) k_hop_fill(const HopTab t) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= t.off[t.n_rel]) return;
+  const int r = hop_rel(t, w);
+  const int64_t j = w - t.off[r];
+  sample_fill(t.rowptr[r], t.col[r], t.n_rows[r], t.dst[r][j], t.fanout, t.seed,
+              t.out_col[r] + t.out_rowptr[r][j]);
 }
 
 // ---- relabel: a hash set over the ids this call sees, O(n_prefix + n_items) work --------------
@@ -213,6 +271,94 @@ int hgnn_sample_fill(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                      as_stream(stream), rowptr, col, n_rows, dst_ids, n_dst, fanout, seed,
                      out_rowptr, out_col);
   return check_launch("k_sample_fill");
+}
+
+static int hop_table(HopTab& t, int32_t n_rel, const int32_t* const* rowptrs,
+                     const int32_t* const* cols, const int64_t* n_rows,
+                     const int32_t* const* dst_ids, const int64_t* n_dst, int32_t fanout,
+                     const char* what) {
+  if (n_rel < 1 || n_rel > kHopMax || fanout == 0 || fanout > 64 || !rowptrs || !n_rows ||
+      !dst_ids || !n_dst)
+    return fail(HGNN_E_ARG, "%s: n_rel=%d (1..%d) fanout=%d (1..64 or <0)", what, n_rel, kHopMax,
+                fanout);
+  t.n_rel = n_rel;
+  t.fanout = fanout;
+  t.off[0] = 0;
+  for (int r = 0; r < n_rel; ++r) {
+    if (n_rows[r] < 0 || n_dst[r] < 0 || (n_dst[r] > 0 && (!rowptrs[r] || !dst_ids[r])))
+      return fail(HGNN_E_ARG, "%s: relation %d", what, r);
+    t.rowptr[r] = rowptrs[r];
+    t.col[r] = cols ? cols[r] : nullptr;
+    t.dst[r] = dst_ids[r];
+    t.n_rows[r] = n_rows[r];
+    t.off[r + 1] = t.off[r] + n_dst[r];
+  }
+  if (t.off[n_rel] >= (int64_t)INT32_MAX) return fail(HGNN_E_ARG, "%s: too many destinations", what);
+  return HGNN_OK;
+}
+
+size_t hgnn_sample_hop_ws_bytes(int64_t n_total_dst) {
+  const int64_t n = n_total_dst < 1 ? 1 : n_total_dst;
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n, nullptr, &scan_b, 0);
+  return 2 * align_up((size_t)(n + 1) * 4, 256) + scan_b + 256;
+}
+
+int hgnn_sample_hop_count(int32_t n_rel, const int32_t* const* rowptrs, const int64_t* n_rows,
+                          const int32_t* const* dst_ids, const int64_t* n_dst, int32_t fanout,
+                          int32_t* const* out_rowptrs, int32_t* d_totals, void* ws,
+                          size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  HopTab t{};
+  if (int rc = hop_table(t, n_rel, rowptrs, nullptr, n_rows, dst_ids, n_dst, fanout,
+                         "sample_hop_count"))
+    return rc;
+  if (!out_rowptrs || !d_totals) return fail(HGNN_E_ARG, "sample_hop_count: null output");
+  for (int r = 0; r < n_rel; ++r) {
+    if (!out_rowptrs[r]) return fail(HGNN_E_ARG, "sample_hop_count: out_rowptrs[%d] is null", r);
+    t.out_rowptr[r] = out_rowptrs[r];
+  }
+  const int64_t n = t.off[n_rel];
+  if (ws_bytes < hgnn_sample_hop_ws_bytes(n))
+    return fail(HGNN_E_WS, "sample_hop_count: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* counts = w.take<int32_t>(n + 1);
+  int32_t* pre = w.take<int32_t>(n + 1);
+  size_t scan_b = 0;
+  exclusive_scan_i32(nullptr, nullptr, n < 1 ? 1 : n, nullptr, &scan_b, stream);
+  void* scan_ws = w.take<char>(scan_b);
+  if (n > 0) {
+    hipLaunchKernelGGL(k_hop_count, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, stream, t,
+                       counts);
+    if (int rc = check_launch("k_hop_count")) return rc;
+  }
+  if (int rc = exclusive_scan_i32(counts, pre, n, scan_ws, &scan_b, stream)) return rc;
+  hipLaunchKernelGGL(k_hop_rowptr, dim3((unsigned)cdiv(n + n_rel, 256)), dim3(256), 0, stream, t,
+                     pre, d_totals);
+  return check_launch("k_hop_rowptr");
+}
+
+int hgnn_sample_hop_fill(int32_t n_rel, const int32_t* const* rowptrs, const int32_t* const* cols,
+                         const int64_t* n_rows, const int32_t* const* dst_ids,
+                         const int64_t* n_dst, int32_t fanout, uint64_t seed,
+                         const int32_t* const* out_rowptrs, int32_t* const* out_cols,
+                         hgnn_stream_t stream_) {
+  HopTab t{};
+  if (int rc = hop_table(t, n_rel, rowptrs, cols, n_rows, dst_ids, n_dst, fanout,
+                         "sample_hop_fill"))
+    return rc;
+  if (!out_rowptrs || !out_cols || !cols) return fail(HGNN_E_ARG, "sample_hop_fill: null array");
+  for (int r = 0; r < n_rel; ++r) {
+    if (n_dst[r] > 0 && (!cols[r] || !out_rowptrs[r] || !out_cols[r]))
+      return fail(HGNN_E_ARG, "sample_hop_fill: relation %d: null pointer", r);
+    t.out_rowptr[r] = const_cast<int32_t*>(out_rowptrs[r]);
+    t.out_col[r] = out_cols[r];
+  }
+  t.seed = seed;
+  const int64_t n = t.off[n_rel];
+  if (n == 0) return HGNN_OK;
+  hipLaunchKernelGGL(k_hop_fill, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, as_stream(stream_), t);
+  return check_launch("k_hop_fill");
 }
 
 size_t hgnn_sample_ws_bytes(int64_t n_dst) {

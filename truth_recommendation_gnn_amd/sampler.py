@@ -93,6 +93,57 @@ class NeighborSampler:
         rowptr, _ = self._count(et, dst, fanout)
         return rowptr, self._fill(et, dst, fanout, seed, rowptr, int(rowptr[-1]))
 
+    def _hop(self, ets, cur, fanout: int, seed: int, checks, hop: int):
+        """Count + fill of every relation into the frontier in one launch per phase
+        (``hgnn_sample_hop_count`` / ``_fill``) and the hop's one read-back of the sizes (with the
+        seed check on the first hop: the kernels count ids outside the table as degree 0, so the
+        check raises before any sample is used).  Returns per relation its zero-based rowptr,
+        the hop's column buffer (relations in ``ets`` order, adjacent) and the sizes."""
+        lib, dev = N.lib(), self.device
+        if not ets:
+            vals = torch.cat([c for _, c in checks]).tolist() if (hop == 0 and checks) else []
+            self._raise_bad_seeds(checks, vals)
+            return {}, torch.empty(0, dtype=torch.int32, device=dev), {}
+        g = [self.csr[et].fwd for et in ets]
+        dsts = [cur[et[2]] for et in ets]
+        n_dst = [int(d.numel()) for d in dsts]
+        n_tot = sum(n_dst)
+        rp_all = torch.empty(n_tot + len(ets) + len(ets), dtype=torch.int32, device=dev)
+        rps, o = [], 0
+        for n in n_dst:
+            rps.append(rp_all[o:o + n + 1])
+            o += n + 1
+        d_tot = rp_all[o:]
+        ws = N.workspace(lib.hgnn_sample_hop_ws_bytes(n_tot), dev)
+        R = len(ets)
+        a_rp, a_dst = N.ptr_array([x.rowptr for x in g]), N.ptr_array(dsts)
+        a_nr, a_nd = N.i64_array([x.n_rows for x in g]), N.i64_array(n_dst)
+        a_out = N.ptr_array(rps)
+        s = N.stream_ptr(dev)
+        N.check(lib.hgnn_sample_hop_count(R, a_rp, a_nr, a_dst, a_nd, fanout, a_out, N.ptr(d_tot),
+                                          N.ptr(ws), ws.numel(), s), "hgnn_sample_hop_count")
+        back = [d_tot] + ([c for _, c in checks] if hop == 0 else [])
+        vals = torch.cat(back).tolist()                    # the hop's one sync
+        self._raise_bad_seeds(checks if hop == 0 else [], vals[R:])
+        totals = vals[:R]
+        cols = torch.empty(sum(totals), dtype=torch.int32, device=dev)
+        views, o = [], 0
+        for t in totals:
+            views.append(cols[o:o + t])
+            o += t
+        N.check(lib.hgnn_sample_hop_fill(R, a_rp, N.ptr_array([x.col for x in g]), a_nr, a_dst,
+                                         a_nd, fanout, seed, a_out, N.ptr_array(views), s),
+                "hgnn_sample_hop_fill")
+        return dict(zip(ets, rps)), cols, dict(zip(ets, totals))
+
+    def _raise_bad_seeds(self, checks, vals):
+        for i, (t, _) in enumerate(checks):
+            lo, hi, dup = vals[3 * i:3 * i + 3]
+            if lo < 0 or hi >= self.num_nodes[t]:
+                raise ValueError(f"seed ids of type {t!r} out of range")
+            if dup:
+                raise ValueError(f"seed ids of type {t!r} must be distinct")
+
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
         lib, dev = N.lib(), self.device
         n_p, n_i = int(prefix.numel()), int(items.numel())
@@ -118,33 +169,21 @@ class NeighborSampler:
         nodes, blocks = [cur], []
         for hop, fanout in enumerate(self.fanouts):
             hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
-            ets = [et for et in self.relations if et[2] in cur]
-            # phase 1 counts ids outside the table as degree 0 (never dereferenced), so the seed
-            # check rides on this hop's one read-back and raises before anything uses the counts
-            counted = {et: self._count(et, cur[et[2]], fanout) for et in ets}
-            back = [counted[et][0][-1:] for et in ets]
-            if hop == 0:
-                back += [c for _, c in checks]
-            vals = torch.cat(back).tolist() if back else []
-            totals = vals[:len(ets)]
-            if hop == 0:
-                for i, (t, _) in enumerate(checks):
-                    lo, hi, dup = vals[len(ets) + 3 * i:len(ets) + 3 * i + 3]
-                    if lo < 0 or hi >= self.num_nodes[t]:
-                        raise ValueError(f"seed ids of type {t!r} out of range")
-                    if dup:
-                        raise ValueError(f"seed ids of type {t!r} must be distinct")
-            sampled = {et: (counted[et][0], self._fill(et, cur[et[2]], fanout, hop_seed,
-                                                       counted[et][0], tot))
-                       for et, tot in zip(ets, totals)}          # one sync for every relation
-            types = sorted(set(cur) | {et[0] for et in sampled})
+            # relations into the frontier, grouped by source type: each type's sampled items are
+            # then one contiguous run of the hop's column buffer (no concatenation for relabel)
+            types = sorted(set(cur) | {et[0] for et in self.relations if et[2] in cur})
+            ets = sorted((et for et in self.relations if et[2] in cur),
+                         key=lambda et: types.index(et[0]))
+            rowptr, cols, totals = self._hop(ets, cur, fanout, hop_seed, checks, hop)
             relabeled = {}
+            o = 0
             for t in types:
-                src_ets = [et for et in sampled if et[0] == t]
-                items = (torch.cat([sampled[et][1] for et in src_ets]) if src_ets else
-                         torch.empty(0, dtype=torch.int32, device=self.device))
+                src_ets = [et for et in ets if et[0] == t]
+                n_t = sum(totals[et] for et in src_ets)
+                items = cols[o:o + n_t]
+                o += n_t
                 prefix = cur.get(t, torch.empty(0, dtype=torch.int32, device=self.device))
-                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items.contiguous())
+                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items)
             sizes = torch.cat([relabeled[t][3] for t in types]).tolist()   # one sync per hop
             nxt: Dict[str, torch.Tensor] = {}
             local: Dict[EdgeType, torch.Tensor] = {}
@@ -153,13 +192,12 @@ class NeighborSampler:
                 nxt[t] = nodes_buf[:size]
                 o = 0
                 for et in src_ets:
-                    n = int(sampled[et][1].numel())
-                    local[et] = loc[o:o + n]
-                    o += n
-            csrs = {et: RelationCSR.from_csr(rowptr, local[et], int(nxt[et[0]].numel()),
+                    local[et] = loc[o:o + totals[et]]
+                    o += totals[et]
+            csrs = {et: RelationCSR.from_csr(rowptr[et], local[et], int(nxt[et[0]].numel()),
                                              int(cur[et[2]].numel()),
                                              may_have_heavy_rows=fanout < 0)
-                    for et, (rowptr, _) in sampled.items()}
+                    for et in ets}
             blocks.append(Block(csrs, {t: int(v.numel()) for t, v in cur.items()},
                                 {t: int(v.numel()) for t, v in nxt.items()}))
             nodes.append(nxt)
