@@ -114,6 +114,17 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
 
 /* K1 forward: aggr = mean_{(j->i)} x_src[j]  — PyG propagate(aggr='mean') inside SAGEConv:
  * x_src.index_select(0, src) + scatter(..., dst, reduce='mean'), train_gnn.py:177-198. */
+/* hgnn_gather_reduce with a per-row output scale: out[i,:] (+)= row_w[i] * sum_p w_p x[col[p],:]
+ * (row_w replaces HGNN_MEAN's 1/segment length; not both).  With row_w = 1/deg of the whole
+ * relation this is one pass of a mean split over source blocks: the passes over the blocks' CSRs
+ * (HGNN_ACCUMULATE from the second on) sum to the relation's mean, each pass reading only its
+ * block of the source table. */
+int hgnn_gather_reduce_scaled(const float* x, int64_t n_x, int32_t d, const int32_t* rowptr,
+                              const int32_t* col, int64_t n_rows, const float* edge_w,
+                              const float* col_w, const float* row_w, int32_t flags,
+                              const int32_t* heavy_rows, const int32_t* heavy_first,
+                              int64_t n_heavy, int64_t n_chunks, int32_t chunk, float* slab,
+                              float* out, hgnn_stream_t stream);
 int hgnn_gather_mean_fwd(const float* x_src, int64_t n_src, int32_t d, const int32_t* rowptr,
                          const int32_t* col, int64_t n_dst, const int32_t* heavy_rows,
                          const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,

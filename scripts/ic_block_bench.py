@@ -1,7 +1,8 @@
 """Experiment: K1 over the cfg4 post <- user relation (200M edges, 9M x 128 fp32 source table =
-4.6 GB) as one pass vs B passes, pass b summing only the sources of user block b (a 4.6/B GB
-slice: at B >= 24 it fits the 256 MB Infinity Cache), accumulating into the output.  Prints
-ms per full gather for each B.  usage: python scripts/ic_block_bench.py [B ...]"""
+4.6 GB) as one pass vs B x D passes: pass (d, b) sums, for the destination rows of group d (D
+contiguous ranges of posts), only the sources in user block b (a 4.6/B GB slice), accumulating
+into the output.  D > 1 keeps each group's accumulator (512/D MB) cache-resident across its B
+passes.  Prints ms per full gather.  usage: python scripts/ic_block_bench.py [B:D ...]"""
 import sys
 import time
 
@@ -11,16 +12,19 @@ sys.path.insert(0, ".")
 from truth_recommendation_gnn_amd import graph, ops, synth  # noqa: E402
 
 
-def timed(fn, reps=5):
+def timed(fn, reps=7):
     fn()
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record()
+    ts = []
     for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
         fn()
-    ev[1].record()
-    torch.cuda.synchronize()
-    return ev[0].elapsed_time(ev[1]) / reps
+        ev[1].record()
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]))
+    ts.sort()
+    return ts[len(ts) // 2]
 
 
 def main():
@@ -36,27 +40,30 @@ def main():
     csr = graph.relation_csr(ei, n_u, n_p)
     ref = torch.empty(n_p, x.shape[1], device=dev)
     t_one = timed(lambda: ops._gather(x, csr.fwd, None, False, ref, False))
-    print(f"B=1 {t_one:.3f} ms  heavy={csr.fwd.plan.n_heavy}", flush=True)
-    Bs = [int(b) for b in sys.argv[1:]] or [8, 16, 24, 32, 48]
-    for B in Bs:
+    print(f"B=1 D=1 {t_one:.3f} ms", flush=True)
+    specs = sys.argv[1:] or ["8:1", "16:1", "8:2", "8:4", "16:4", "16:8", "24:8", "32:8"]
+    for spec in specs:
+        B, D = (int(v) for v in spec.split(":"))
         bs = -(-n_u // B)
         key = (ei[0] // bs) * n_p + ei[1]
         ge = graph.group_edges(key, ei[0], B * n_p, n_u)
         del key
+        ds = -(-n_p // D)
         parts = []
-        for b in range(B):
-            rp = ge.rowptr[b * n_p:(b + 1) * n_p + 1]
-            parts.append(graph.GroupedEdges(rp, ge.col, ge.perm,
-                                            graph._plan(rp, n_p, ge.plan.chunk), n_p))
+        for d in range(D):
+            lo, hi = d * ds, min((d + 1) * ds, n_p)
+            for b in range(B):
+                rp = ge.rowptr[b * n_p + lo:b * n_p + hi + 1]
+                parts.append((lo, hi, b, graph.GroupedEdges(
+                    rp, ge.col, ge.perm, graph._plan(rp, hi - lo, ge.plan.chunk), hi - lo)))
         out = torch.empty_like(ref)
 
         def run():
-            for b, gb in enumerate(parts):
-                ops._gather(x, gb, None, False, out, b > 0)
+            for lo, hi, b, gb in parts:
+                ops._gather(x, gb, None, False, out[lo:hi], b > 0)
         t = timed(run)
         err = float((out - ref).abs().max() / ref.abs().max())
-        print(f"B={B} {t:.3f} ms ({t_one / t:.2f}x)  rel_err={err:.2e}  "
-              f"heavy={sum(p.plan.n_heavy for p in parts)}", flush=True)
+        print(f"B={B} D={D} {t:.3f} ms ({t_one / t:.3f}x)  rel_err={err:.2e}", flush=True)
         del ge, parts, out
         torch.cuda.empty_cache()
 

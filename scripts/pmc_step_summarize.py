@@ -53,10 +53,11 @@ def main():
            "correction": "hbm bytes = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024 (gfx950 wide-read tally)",
            "config": cfg, "steps_profiled": steps, "launches": {}, "kernels": {}}
     for role, meta in info["roles"].items():
+        grids = meta["grid"] if isinstance(meta["grid"], list) else [meta["grid"]]
         fk = [(k, v) for k, v in fetch.items() if match(k[0], meta["kernel"])
-              and (meta["grid"] is None or k[1] == meta["grid"])]
+              and (meta["grid"] is None or k[1] in grids)]
         wk = [(k, v) for k, v in write.items() if match(k[0], meta["kernel"])
-              and (meta["grid"] is None or k[1] == meta["grid"])]
+              and (meta["grid"] is None or k[1] in grids)]
         if not fk or not wk:
             continue
         f_tot = sum(sum(v) for _, v in fk)

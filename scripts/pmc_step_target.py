@@ -62,14 +62,25 @@ def grid(grouped):
     return -(-(grouped.n_rows + grouped.plan.n_chunks) // 4) * 256
 
 
+# gathers over the 9M-row user-side tables run as source-block passes (ops.gather_blocks): one
+# dispatch (grid) per block, every pass of a gather attributed to it
+B = ops.gather_blocks(torch.empty(U, d, device="meta"))
+
+
+def grids(csr, side):
+    if B == 1:
+        return grid(csr.fwd if side == "fwd" else csr.bwd)
+    return [grid(p) for p in csr.blocks(side, B)[0]]
+
+
 gb = ops.gather_bytes
 roles = {
     # (kernel-name fragment, grid threads) -> role, algorithmic bytes per launch
-    "gather_fwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, false, false>", "grid": grid(eng.fwd),
+    "gather_fwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, false, false>", "grid": grids(eng, "fwd"),
                                "alg_bytes": gb(E, P, d, False), "per_step": 2},
     "gather_fwd[user<-post]": {"kernel": "k_gather<32, 1, 4, 4, false, false>", "grid": grid(rev.fwd),
                                "alg_bytes": gb(E, U, d, False), "per_step": 2},
-    "gather_bwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, true, false>", "grid": grid(rev.bwd),
+    "gather_bwd[post<-user]": {"kernel": "k_gather<32, 1, 4, 4, true, false>", "grid": grids(rev, "bwd"),
                                "alg_bytes": gb(E, P, d, True), "per_step": 1},
     "gather_bwd[user<-post]": {"kernel": "k_gather<32, 1, 4, 4, true, false>", "grid": grid(eng.bwd),
                                "alg_bytes": gb(E, U, d, True), "per_step": 1},
@@ -84,5 +95,5 @@ roles = {
                        "note": "all kernels of the per-step sort summed (launches per step)"},
     "fixup": {"kernel": "k_fixup", "grid": None, "alg_bytes": None, "per_step": None},
 }
-print("PMC_TARGET " + json.dumps({"config": cfg.name, "steps": STEPS, "marker": "k_uniform_i32", "E": E, "U": U, "P": P,
+print("PMC_TARGET " + json.dumps({"config": cfg.name, "steps": STEPS, "marker": "k_uniform_i32", "blocks": B, "E": E, "U": U, "P": P,
                                   "d": d, "roles": roles}), flush=True)

@@ -144,6 +144,38 @@ def test_score_gather2_matches_float64(d):
     close(out, ref)
 
 
+@pytest.mark.parametrize("d,slice_rows", [(64, 700), (128, 333), (4, 1200)])
+def test_source_blocked_gathers_match_oracle(monkeypatch, d, slice_rows):
+    """K1 mean and K2 as passes over source blocks (what gathers over multi-GB tables run, e.g.
+    cfg4's 4.6 GB user table in 8 passes), forced here on small tables: each pass sums its block
+    scaled by 1/deg of the whole relation into the output (skewed graph, heavy rows split per
+    block, empty rows, accumulate mode) — against the oracle / autograd as the one-pass path."""
+    monkeypatch.setattr(ops, "GATHER_BLOCK_BYTES", 1)
+    monkeypatch.setattr(ops, "GATHER_BLOCK_SLICE", slice_rows * d * 4)
+    rng = np.random.default_rng(77 + d)
+    n_src, n_dst, E = 5000, 300, 60000
+    ei = rand_coo(rng, n_src, n_dst, E, skew=True)
+    ei = ei[:, ei[1] != 7]                                   # an empty destination row
+    x = torch.from_numpy(rng.standard_normal((n_src, d)).astype(np.float32)).requires_grad_()
+    csr = graph.RelationCSR(ei.to(DEV), n_src, n_dst, chunk=64)
+    assert ops.gather_blocks(x) > 3
+    ref = sage_ref.mean_aggregate(x, ei, n_dst)
+    got = ops.gather_mean(x.detach().to(DEV), csr)
+    close(got, ref)
+    assert float(got[7].abs().max()) == 0.0
+    passes, _ = csr.blocks("fwd", ops.gather_blocks(x))
+    assert sum(p.plan.n_heavy for p in passes) > 0
+    acc = torch.ones(n_dst, d, device=DEV)
+    ops.gather_mean(x.detach().to(DEV), csr, out=acc)
+    close(acc, ref + 1.0)
+    # K2: blocks over the destinations' gradient rows (the table K2 reads)
+    g = torch.from_numpy(rng.standard_normal((n_dst, d)).astype(np.float32))
+    ref.backward(g)
+    monkeypatch.setattr(ops, "GATHER_BLOCK_SLICE", 40 * d * 4)
+    assert ops.gather_blocks(g) > 3
+    close(ops.scatter_mean_bwd(g.to(DEV), csr), x.grad)
+
+
 def test_gather_is_deterministic_bitwise():
     rng = np.random.default_rng(5)
     ei = rand_coo(rng, 5000, 200, 100000, skew=True).to(DEV)

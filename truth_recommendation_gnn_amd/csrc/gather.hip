@@ -24,6 +24,7 @@ struct GatherArgs {
   const int32_t* col;
   const float* edge_w;
   const float* col_w;
+  const float* row_w;          // per-row output scale (replaces the mean's 1/segment length)
   const int32_t* heavy_rows;
   const int32_t* heavy_first;
   float* slab;
@@ -170,7 +171,10 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
   slot_combine<LPR, VPL, W>(acc);
   if (!writer) return;
   float s = 1.f;
-  if (!partial && a.mean) s = end > beg ? 1.f / (float)(end - beg) : 0.f;
+  if (!partial) {
+    if (a.row_w) s = a.row_w[row];
+    else if (a.mean) s = end > beg ? 1.f / (float)(end - beg) : 0.f;
+  }
 #pragma unroll
   for (int q = 0; q < VPL; ++q) {
     const int c = (q * LPR + sl) * W;
@@ -195,7 +199,7 @@ __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
   const int64_t row = a.heavy_rows[h];
   const int64_t f0 = a.heavy_first[h], f1 = a.heavy_first[h + 1];
   const int64_t deg = a.rowptr[row + 1] - a.rowptr[row];
-  const float s = a.mean ? (deg > 0 ? 1.f / (float)deg : 0.f) : 1.f;
+  const float s = a.row_w ? a.row_w[row] : (a.mean ? (deg > 0 ? 1.f / (float)deg : 0.f) : 1.f);
   const int nvec = (a.d + W - 1) / W;
   int cpb = 1;
   while (cpb < nvec && cpb < 256) cpb <<= 1;
@@ -328,6 +332,24 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
   a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
   a.d = d; a.chunk = chunk; a.mean = (flags & HGNN_MEAN) ? 1 : 0;
+  a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+  return run_gather(a, as_stream(stream));
+}
+
+int hgnn_gather_reduce_scaled(const float* x, int64_t n_x, int32_t d, const int32_t* rowptr,
+                              const int32_t* col, int64_t n_rows, const float* edge_w,
+                              const float* col_w, const float* row_w, int32_t flags,
+                              const int32_t* heavy_rows, const int32_t* heavy_first,
+                              int64_t n_heavy, int64_t n_chunks, int32_t chunk, float* slab,
+                              float* out, hgnn_stream_t stream) {
+  (void)n_x;
+  if (row_w && (flags & HGNN_MEAN))
+    return fail(HGNN_E_ARG, "gather_reduce_scaled: row_w replaces HGNN_MEAN, not both");
+  GatherArgs a{};
+  a.x = x; a.rowptr = rowptr; a.col = col; a.edge_w = edge_w; a.col_w = col_w; a.row_w = row_w;
+  a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
+  a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
+  a.d = d; a.chunk = chunk; a.mean = 0;
   a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
   return run_gather(a, as_stream(stream));
 }

@@ -287,6 +287,35 @@ class RelationCSR:
             self._bwd_w = w
         return w
 
+    def blocks(self, side: str, n_blocks: int):
+        """The relation split into ``n_blocks`` passes over contiguous blocks of the table a
+        gather reads: ``side="fwd"`` (K1, reads the sources; rows = destinations) blocks by
+        source id, ``side="bwd"`` (K2, reads the destinations' gradients; rows = sources) by
+        destination id.  Returns (passes, weights): one GroupedEdges per block (its rowptr a slice
+        of one CSR keyed by (block, row) — absolute offsets into a shared col — with its own skew
+        plan), and for "bwd" the 1/deg(destination) per position in that order.  Built once (one
+        K5 sort) and cached; see ops.GATHER_BLOCK_BYTES for why."""
+        key = (side, int(n_blocks))
+        cache = self.__dict__.setdefault("_blocks", {})
+        if key in cache:
+            return cache[key]
+        B = int(n_blocks)
+        ei = self.edge_index
+        if side == "fwd":
+            n_rows, n_read, rows, reads = self.n_dst, self.n_src, ei[1], ei[0]
+        else:
+            n_rows, n_read, rows, reads = self.n_src, self.n_dst, ei[0], ei[1]
+        bs = -(-n_read // B)
+        ge = group_edges((reads // bs) * n_rows + rows, reads, B * n_rows, n_read, chunk=NO_SPLIT)
+        chunk = default_chunk(max(self.num_edges // B, 1))
+        passes = []
+        for b in range(B):
+            rp = ge.rowptr[b * n_rows:(b + 1) * n_rows + 1]
+            passes.append(GroupedEdges(rp, ge.col, None, _plan(rp, n_rows, chunk), n_rows))
+        w = self.inv_deg[ge.col.long()].contiguous() if side == "bwd" else None
+        cache[key] = (passes, w)
+        return cache[key]
+
     def release_coo(self):
         """Drop the COO reference once the CSC exists (saves 16 B/edge of HBM)."""
         if self._bwd is not None:

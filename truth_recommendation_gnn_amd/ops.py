@@ -100,6 +100,43 @@ def gather_compulsory_bytes(n_edges: int, n_rows: int, n_src: int, d: int, weigh
 
 
 # ----------------------------------------------------------------------------- raw kernel calls
+# Source-blocked gathers.  Random rows from a table of several GB come back at ~6.3 TB/s; the
+# same rows from a ~600 MB slice of it at ~7.2 TB/s (cfg4 K1 post<-user, scripts/ic_block_bench.py:
+# 16.96 ms in one pass, 15.36 ms in 8 passes over 575-MB user blocks, each pass adding its block's
+# sum into the output).  The passes re-read and re-write the output (B-1 extra round trips of
+# N_dst x 4d bytes), which the gain pays for only while the blocks stay large: 8 passes is the
+# best measured split of a 4.6 GB table, 16 is already even.  So a gather whose source table is
+# at least GATHER_BLOCK_BYTES is split into ceil(table / GATHER_BLOCK_SLICE) passes.
+GATHER_BLOCK_BYTES = int(float(os.environ.get("HGNN_GATHER_BLOCK_GB", "2")) * 2**30)
+GATHER_BLOCK_SLICE = int(float(os.environ.get("HGNN_GATHER_BLOCK_MB", "600")) * 2**20)
+
+
+def gather_blocks(x: torch.Tensor) -> int:
+    """Number of source-block passes for a gather reading table ``x`` (1: one plain pass)."""
+    nbytes = x.numel() * x.element_size()
+    if GATHER_BLOCK_BYTES <= 0 or nbytes < GATHER_BLOCK_BYTES:
+        return 1
+    return int(-(-nbytes // GATHER_BLOCK_SLICE))
+
+
+def _gather_blocked(x, passes, row_w, edge_w, out, accumulate, name, nbytes, cbytes):
+    """All passes of a source-blocked gather, timed as one gather (its algorithmic bytes are the
+    unblocked gather's)."""
+    dev = out.device
+    d = int(out.shape[1])
+    lib, s = N.lib(), N.stream_ptr(dev)
+    with _timed(name, nbytes, cbytes):
+        for b, g in enumerate(passes):
+            p = g.plan
+            slab = (torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
+                    if p.n_heavy else None)
+            flags = N.HGNN_ACCUMULATE if (accumulate or b > 0) else 0
+            N.check(lib.hgnn_gather_reduce_scaled(
+                N.ptr(x), x.shape[0], d, N.ptr(g.rowptr), N.ptr(g.col), g.n_rows, N.ptr(edge_w),
+                None, N.ptr(row_w), flags, N.ptr(p.heavy_rows), N.ptr(p.heavy_first), p.n_heavy,
+                p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out), s), "hgnn_gather_reduce_scaled")
+
+
 def gather_mean(x_src: torch.Tensor, csr: RelationCSR,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K1: ``aggr[i] = mean_{(j->i)} x_src[j]`` (0 for an empty row); added into ``out`` when
@@ -112,6 +149,15 @@ def gather_mean(x_src: torch.Tensor, csr: RelationCSR,
     acc = out is not None
     if out is None:
         out = torch.empty(csr.n_dst, d, dtype=torch.float32, device=dev)
+    B = gather_blocks(x_src) if csr.num_edges else 1
+    if B > 1:
+        passes, _ = csr.blocks("fwd", B)
+        E = csr.num_edges
+        _gather_blocked(x_src, passes, csr.inv_deg, None, out, acc,
+                        f"gather_fwd[{csr.n_dst}<-{csr.n_src}]x{d}",
+                        gather_bytes(E, csr.n_dst, d, False),
+                        gather_compulsory_bytes(E, csr.n_dst, csr.n_src, d, False))
+        return out
     _gather(x_src, csr.fwd, None, csr_mean=True, out=out, accumulate=acc)
     return out
 
@@ -190,6 +236,15 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
     acc = out is not None
     if out is None:
         out = torch.empty(csr.n_src, d, dtype=torch.float32, device=dev)
+    B = gather_blocks(grad_aggr) if csr.num_edges else 1
+    if B > 1:
+        passes, w = csr.blocks("bwd", B)
+        E = csr.num_edges
+        _gather_blocked(grad_aggr, passes, None, w, out, acc,
+                        f"gather_bwd[{csr.n_src}<-{csr.n_dst}]x{d}",
+                        gather_bytes(E, csr.n_src, d, True),
+                        gather_compulsory_bytes(E, csr.n_src, csr.n_dst, d, True))
+        return out
     _gather(grad_aggr, csr.bwd, None, csr_mean=False, out=out, accumulate=acc,
             edge_w=csr.bwd_weights)
     return out
