@@ -315,15 +315,49 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
 def split_weight_grads(dW: torch.Tensor, db: Optional[torch.Tensor], ks: Sequence[int],
                        k_root: int, scales: Sequence[float],
                        dwl: Sequence[Optional[torch.Tensor]], dwr: Sequence[Optional[torch.Tensor]],
-                       dbl: Sequence[Optional[torch.Tensor]]) -> None:
+                       dbl: Sequence[Optional[torch.Tensor]], plan=None) -> None:
     """Adjoint of :func:`fuse_weights` into the given gradient buffers (entries may be None):
     dwl[r] = s_r dW[:, block r], dwr[r] = s_r dW[:, root], dbl[r] = s_r db (one launch)."""
     dev = dW.device
+    a_ks = plan.a_ks if plan is not None else N.int_array(ks)
+    a_sc = plan.a_sc if plan is not None else N.float_array(scales)
     N.check(N.lib().hgnn_split_weight_grads(
         len(ks), N.ptr(dW.contiguous()), N.ptr(None if db is None else db.contiguous()),
-        N.int_array(ks), int(k_root), N.float_array(scales), int(dW.shape[0]),
+        a_ks, int(k_root), a_sc, int(dW.shape[0]),
         N.ptr_array(dwl), N.ptr_array(dwr), N.ptr_array(dbl), N.stream_ptr(dev)),
         "hgnn_split_weight_grads")
+
+
+class _FusePlan:
+    """The host side of one fused-weight launch, built once per set of parameter buffers: the
+    layout (meta) and the ctypes argument arrays.  Parameters keep their storage across
+    optimizer steps, so a sampled mini-batch step (four of these per step at cfg5, where the
+    host issue time is the step time) reuses them instead of rebuilding them per call."""
+    __slots__ = ("meta", "a_wl", "a_wr", "a_bl", "a_ks", "a_sc")
+
+    def __init__(self, meta, wl, wr, bl):
+        ks, k_root, scales, _, _ = meta
+        self.meta = meta
+        self.a_wl, self.a_wr, self.a_bl = N.ptr_array(wl), N.ptr_array(wr), N.ptr_array(bl)
+        self.a_ks, self.a_sc = N.int_array(ks), N.float_array(scales)
+
+
+_FUSE_PLANS: "Dict[tuple, _FusePlan]" = {}
+
+
+def _fuse_plan(meta, wl, wr, bl) -> _FusePlan:
+    ts = [t for t in (*wl, *wr, *bl) if t is not None]
+    if not all(t.is_contiguous() for t in ts):
+        return _FusePlan(meta, [t.contiguous() for t in wl],
+                         [None if t is None else t.contiguous() for t in wr],
+                         [None if t is None else t.contiguous() for t in bl])
+    key = (meta, tuple(0 if t is None else t.data_ptr() for t in (*wl, *wr, *bl)))
+    plan = _FUSE_PLANS.get(key)
+    if plan is None:
+        if len(_FUSE_PLANS) >= 1024:
+            _FUSE_PLANS.clear()
+        plan = _FUSE_PLANS[key] = _FusePlan(meta, wl, wr, bl)
+    return plan
 
 
 class _FuseWeights(torch.autograd.Function):
@@ -340,13 +374,11 @@ class _FuseWeights(torch.autograd.Function):
         h, dev = int(wl[0].shape[0]), wl[0].device
         W = torch.empty(h, sum(ks) + k_root, dtype=torch.float32, device=dev)
         b = torch.empty(h, dtype=torch.float32, device=dev) if any(has_b) else None
-        N.check(N.lib().hgnn_fuse_weights(
-            R, N.ptr_array([t.contiguous() for t in wl]), N.int_array(ks),
-            N.ptr_array([None if t is None else t.contiguous() for t in wr]), int(k_root),
-            N.ptr_array([None if t is None else t.contiguous() for t in bl]),
-            N.float_array(scales), h, N.ptr(W), N.ptr(b), N.stream_ptr(dev)),
-            "hgnn_fuse_weights")
-        ctx.meta, ctx.h, ctx.dev = meta, h, dev
+        plan = _fuse_plan(meta, wl, wr, bl)
+        N.check(N.lib().hgnn_fuse_weights(R, plan.a_wl, plan.a_ks, plan.a_wr, int(k_root),
+                                          plan.a_bl, plan.a_sc, h, N.ptr(W), N.ptr(b),
+                                          N.stream_ptr(dev)), "hgnn_fuse_weights")
+        ctx.meta, ctx.h, ctx.dev, ctx.plan = meta, h, dev, plan
         return (W, b) if b is not None else W
 
     @staticmethod
@@ -367,7 +399,8 @@ class _FuseWeights(torch.autograd.Function):
             i += hb
         if dW is None:
             dW = torch.zeros(ctx.h, sum(ks) + k_root, dtype=torch.float32, device=ctx.dev)
-        split_weight_grads(dW, db if any(has_b) else None, ks, k_root, scales, dwl, dwr, dbl)
+        split_weight_grads(dW, db if any(has_b) else None, ks, k_root, scales, dwl, dwr, dbl,
+                           plan=ctx.plan)
         return (None, *dwl, *[t for t, hr in zip(dwr, has_r) if hr],
                 *[t for t, hb in zip(dbl, has_b) if hb])
 
