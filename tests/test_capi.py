@@ -76,3 +76,16 @@ def test_heterodata_lite():
     assert set(g.edge_index_dict) == {("user", "engages", "post"), ("post", "rev_engages", "user")}
     assert g.metadata()[0] == ["user", "post"]
     assert g.to("cpu") is g
+
+
+def test_source_block_count_follows_the_table_size(monkeypatch):
+    """Host rule of the source-blocked gathers (ops.gather_blocks): a table of >= 2 GB is split
+    into ~600 MB source blocks (cfg4's 9M x 128 fp32 user table: 8 passes), smaller tables run
+    in one pass; the threshold 0 turns the blocking off."""
+    from truth_recommendation_gnn_amd import ops
+    big = torch.empty(9_000_000, 128, device="meta")
+    assert ops.gather_blocks(big) == 8
+    assert ops.gather_blocks(torch.empty(1_000_000, 128, device="meta")) == 1   # 512 MB
+    assert ops.gather_blocks(torch.empty(4_500_000, 128, device="meta")) == 4   # 2.3 GB
+    monkeypatch.setattr(ops, "GATHER_BLOCK_BYTES", 0)
+    assert ops.gather_blocks(big) == 1
