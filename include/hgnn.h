@@ -331,6 +331,13 @@ size_t hgnn_relabel_ws_bytes(int64_t n_prefix, int64_t n_items);
 int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
                  int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
                  size_t ws_bytes, hgnn_stream_t stream);
+/* hgnn_relabel that also checks the prefix (a mini-batch's seeds): d_count2[0] = the count,
+ * d_count2[1] = flags, bit 0 a repeated prefix id, bit 1 a prefix id outside [0, id_limit).
+ * The outputs are unspecified when a flag is set; nothing is read out of bounds. */
+int hgnn_relabel_checked(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
+                         const int32_t* items, int64_t n_items, int32_t* local_out,
+                         int32_t* nodes_out, int32_t* d_count2, void* ws, size_t ws_bytes,
+                         hgnn_stream_t stream);
 
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of

@@ -76,7 +76,7 @@ def test_relabel_prefix_then_new_ids_in_first_appearance_order():
     s = sampler.NeighborSampler({"a": n}, {("a", "r", "a"): ei}, [("a", "r", "a")], [3])
     nodes, local, count = s._relabel("a", torch.from_numpy(prefix).to(DEV),
                                      torch.from_numpy(items).to(DEV))
-    nodes, local = nodes[:int(count)].cpu().numpy(), local.cpu().numpy()
+    nodes, local = nodes[:int(count[0])].cpu().numpy(), local.cpu().numpy()
     assert np.array_equal(nodes[:50], prefix)
     pre = set(prefix.tolist())
     new = list(dict.fromkeys(i for i in items.tolist() if i not in pre))
@@ -219,20 +219,25 @@ def test_relabel_edge_cases_and_seed_checks():
     pre = torch.tensor([2, 0], dtype=torch.int32, device=DEV)
     none = torch.empty(0, dtype=torch.int32, device=DEV)
     nodes, local, count = s._relabel("a", pre, none)                  # no items
-    assert int(count) == 2 and nodes[:2].tolist() == [2, 0] and local.numel() == 0
+    assert int(count[0]) == 2 and nodes[:2].tolist() == [2, 0] and local.numel() == 0
     nodes, local, count = s._relabel("a", none, torch.tensor([5, 5, 3, 9, 3], dtype=torch.int32,
                                                                device=DEV))   # no prefix
-    assert int(count) == 3 and nodes[:3].tolist() == [5, 3, 9] and local.tolist() == [0, 0, 1, 2, 1]
-    with pytest.raises(ValueError):
+    assert int(count[0]) == 3 and nodes[:3].tolist() == [5, 3, 9] and local.tolist() == [0, 0, 1, 2, 1]
+    with pytest.raises(ValueError, match="distinct"):
         s.sample({"a": torch.tensor([0, 0])})
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="out of range"):
         s.sample({"a": torch.tensor([3])})
     mb = s.sample({"a": torch.tensor([1])}, seed=1)
     assert mb.nodes[-1]["a"].tolist() == [1]
-    with pytest.raises(ValueError):      # far outside the table: counted as degree 0, no read
+    with pytest.raises(ValueError, match="out of range"):   # far outside: degree 0, no read
         s.sample({"a": torch.tensor([1, 10**6])})
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="out of range"):
         s.sample({"a": torch.tensor([-1])})
+    with pytest.raises(ValueError, match="distinct"):      # a repeat among many seeds
+        s.sample({"a": torch.tensor([2, 0, 1, 0])})
+    # the flags are per call: a clean batch after a bad one samples normally
+    mb = s.sample({"a": torch.tensor([2, 0])}, seed=3)
+    assert mb.nodes[-1]["a"].tolist() == [2, 0]
 
 
 @pytest.mark.parametrize("n_src,n_dst,E", [(1, 1, 1), (37, 11, 500), (5000, 300, 60000),
@@ -272,7 +277,7 @@ def test_hop_batch_equals_per_relation_sampling(fanout):
                                 ets, [fanout])
     cur = {"b": torch.from_numpy(rng.permutation(300)[:120].astype(np.int32)).to(DEV),
            "a": torch.empty(0, dtype=torch.int32, device=DEV)}
-    rowptr, cols, totals = s._hop(ets, cur, fanout, 99, [], 1)
+    rowptr, cols, totals = s._hop(ets, cur, fanout, 99)
     o = 0
     for et in ets:
         rp, col = s._sample(et, cur[et[2]], fanout, 99)
@@ -281,6 +286,6 @@ def test_hop_batch_equals_per_relation_sampling(fanout):
         assert torch.equal(cols[o:o + totals[et]], col), et
         o += totals[et]
     bad = {"b": torch.tensor([5, 300, -2, 7], dtype=torch.int32, device=DEV)}
-    rowptr, cols, totals = s._hop([("a", "r1", "b")], bad, fanout, 1, [], 1)
+    rowptr, cols, totals = s._hop([("a", "r1", "b")], bad, fanout, 1)
     deg = rowptr[("a", "r1", "b")].diff().tolist()
     assert deg[1] == 0 and deg[2] == 0

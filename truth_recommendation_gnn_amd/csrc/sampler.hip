@@ -143,31 +143,52 @@ struct RelabelTab {
   int32_t* key;
   int32_t* ppos;
   int32_t* first;
+  int32_t* nflags;   // ~flags of the prefix check (starts all ones with the key memset)
   uint32_t mask;
   int shift;   // 64 - log2(capacity)
+  int64_t id_limit;  // prefix ids must lie in [0, id_limit) (checked only if > 0)
 };
 
-__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t id) {
+// slot of `id`; *found = the id was already in the table (inserted by another thread)
+__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t id,
+                                                      bool* found = nullptr) {
   uint32_t s = (uint32_t)(((uint64_t)(uint32_t)id * 0x9E3779B97F4A7C15ull) >> t.shift);
   for (uint32_t probe = 0; probe <= t.mask; ++probe) {   // ends: load factor <= 1/2
     const int32_t k = __atomic_load_n(&t.key[s], __ATOMIC_RELAXED);
-    if (k == id) return s;
+    if (k == id) {
+      if (found) *found = true;
+      return s;
+    }
     if (k == -1) {
       const int32_t old = atomicCAS(&t.key[s], -1, id);
-      if (old == -1 || old == id) return s;
+      if (old == -1) return s;
+      if (old == id) {
+        if (found) *found = true;
+        return s;
+      }
     }
     s = (s + 1) & t.mask;
   }
   return 0;   // unreachable with the capacity the host sizes
 }
 
+// Prefix ids (the previous frontier, or the seeds) are expected distinct and in range: a
+// repeated id (found already inserted) clears bit 0 of nflags, an id outside [0, id_limit)
+// bit 1 — the caller reads the flags with the node count it reads anyway (no extra sync).
 __global__ void k_relabel_prefix(RelabelTab t, const int32_t* prefix, int64_t n_prefix,
                                  int32_t* nodes) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_prefix) return;
-  const uint32_t s = rl_find_or_insert(t, prefix[i]);
-  t.ppos[s] = (int32_t)i;   // prefix ids are distinct: one writer per slot
-  nodes[i] = prefix[i];
+  const int32_t id = prefix[i];
+  nodes[i] = id;
+  if (t.id_limit > 0 && (id < 0 || id >= t.id_limit)) {   // flagged, never inserted
+    if (t.nflags) atomicAnd(t.nflags, ~2);
+    return;
+  }
+  bool found = false;
+  const uint32_t s = rl_find_or_insert(t, id, &found);
+  if (found && t.nflags) atomicAnd(t.nflags, ~1);
+  t.ppos[s] = (int32_t)i;   // one writer per slot when the prefix ids are distinct
 }
 
 __global__ void k_relabel_insert(RelabelTab t, const int32_t* items, int64_t n_items,
@@ -205,8 +226,9 @@ __global__ void k_relabel_assign(RelabelTab t, const int32_t* items, const int32
 }
 
 __global__ void k_relabel_count(const int32_t* rank, int64_t n_items, int64_t n_prefix,
-                                int32_t* d_count) {
-  *d_count = (int32_t)(n_prefix + (n_items > 0 ? rank[n_items] : 0));
+                                const int32_t* nflags, int32_t* d_count) {
+  d_count[0] = (int32_t)(n_prefix + (n_items > 0 ? rank[n_items] : 0));
+  if (nflags) d_count[1] = ~*nflags;
 }
 
 static int64_t relabel_cap(int64_t n) {
@@ -218,13 +240,18 @@ static int64_t relabel_cap(int64_t n) {
 static size_t relabel_ws(int64_t n_prefix, int64_t n_items, size_t* scan_b) {
   const int64_t cap = relabel_cap(n_prefix + n_items);
   exclusive_scan_i32(nullptr, nullptr, n_items < 1 ? 1 : n_items, nullptr, scan_b, 0);
-  return 3 * align_up((size_t)cap * 4, 256) + 3 * align_up((size_t)(n_items + 1) * 4, 256) +
+  return 3 * align_up((size_t)cap * 4, 256) + 256 + 3 * align_up((size_t)(n_items + 1) * 4, 256) +
          *scan_b + 256;
 }
 
 }  // namespace hgnn
 
 using namespace hgnn;
+
+static int relabel(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
+                   const int32_t* items, int64_t n_items, int32_t* local_out, int32_t* nodes_out,
+                   int32_t* d_count, bool check, void* ws, size_t ws_bytes,
+                   hipStream_t stream);
 
 extern "C" {
 
@@ -375,7 +402,24 @@ size_t hgnn_relabel_ws_bytes(int64_t n_prefix, int64_t n_items) {
 int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
                  int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
                  size_t ws_bytes, hgnn_stream_t stream_) {
-  hipStream_t stream = as_stream(stream_);
+  return relabel(prefix, n_prefix, 0, items, n_items, local_out, nodes_out, d_count, false, ws,
+                 ws_bytes, as_stream(stream_));
+}
+
+int hgnn_relabel_checked(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
+                         const int32_t* items, int64_t n_items, int32_t* local_out,
+                         int32_t* nodes_out, int32_t* d_count2, void* ws, size_t ws_bytes,
+                         hgnn_stream_t stream_) {
+  return relabel(prefix, n_prefix, id_limit, items, n_items, local_out, nodes_out, d_count2, true,
+                 ws, ws_bytes, as_stream(stream_));
+}
+
+}  // extern "C"
+
+static int relabel(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
+                   const int32_t* items, int64_t n_items, int32_t* local_out, int32_t* nodes_out,
+                   int32_t* d_count, bool check, void* ws, size_t ws_bytes,
+                   hipStream_t stream) {
   if (n_prefix < 0 || n_items < 0 || n_prefix + n_items >= (int64_t)INT32_MAX / 2)
     return fail(HGNN_E_ARG, "relabel: bad sizes");
   if (!d_count || (n_prefix > 0 && (!prefix || !nodes_out)) ||
@@ -389,8 +433,10 @@ int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, 
   while ((int64_t(1) << log2cap) < cap) ++log2cap;
   Workspace w(ws, ws_bytes);
   RelabelTab t;
-  t.key = w.take<int32_t>(2 * cap);     // key and ppos adjacent: one 0xFF memset
+  t.key = w.take<int32_t>(2 * cap + 64);   // key, ppos and the flags word: one 0xFF memset
   t.ppos = t.key + cap;
+  t.nflags = check ? t.key + 2 * cap : nullptr;
+  t.id_limit = id_limit;
   t.first = w.take<int32_t>(cap);
   t.mask = (uint32_t)(cap - 1);
   t.shift = 64 - log2cap;
@@ -398,7 +444,7 @@ int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, 
   int32_t* flags = w.take<int32_t>(n_items + 1);
   int32_t* rank = w.take<int32_t>(n_items + 1);
   void* scan_ws = w.take<char>(scan_b);
-  (void)hipMemsetAsync(t.key, 0xFF, (size_t)cap * 8, stream);       // key = ppos = -1
+  (void)hipMemsetAsync(t.key, 0xFF, (size_t)cap * 8 + 4, stream);   // key = ppos = -1, flags
   (void)hipMemsetAsync(t.first, 0x7F, (size_t)cap * 4, stream);     // "infinity"
   if (n_prefix > 0)
     hipLaunchKernelGGL(k_relabel_prefix, dim3((unsigned)cdiv(n_prefix, 256)), dim3(256), 0,
@@ -415,8 +461,6 @@ int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, 
                        n_items, n_prefix, local_out, nodes_out);
   }
   hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(1), 0, stream, rank, n_items, n_prefix,
-                     d_count);
+                     t.nflags, d_count);
   return check_launch("relabel");
 }
-
-}  // extern "C"

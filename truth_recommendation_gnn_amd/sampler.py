@@ -93,16 +93,15 @@ class NeighborSampler:
         rowptr, _ = self._count(et, dst, fanout)
         return rowptr, self._fill(et, dst, fanout, seed, rowptr, int(rowptr[-1]))
 
-    def _hop(self, ets, cur, fanout: int, seed: int, checks, hop: int):
+    def _hop(self, ets, cur, fanout: int, seed: int):
         """Count + fill of every relation into the frontier in one launch per phase
-        (``hgnn_sample_hop_count`` / ``_fill``) and the hop's one read-back of the sizes (with the
-        seed check on the first hop: the kernels count ids outside the table as degree 0, so the
-        check raises before any sample is used).  Returns per relation its zero-based rowptr,
-        the hop's column buffer (relations in ``ets`` order, adjacent) and the sizes."""
+        (``hgnn_sample_hop_count`` / ``_fill``) and the hop's one read-back of the sizes.  The
+        kernels count ids outside the table as degree 0, so unchecked seeds are never
+        dereferenced (they are checked by the first relabel).  Returns per relation its
+        zero-based rowptr, the hop's column buffer (relations in ``ets`` order, adjacent) and
+        the sizes."""
         lib, dev = N.lib(), self.device
         if not ets:
-            vals = torch.cat([c for _, c in checks]).tolist() if (hop == 0 and checks) else []
-            self._raise_bad_seeds(checks, vals)
             return {}, torch.empty(0, dtype=torch.int32, device=dev), {}
         g = [self.csr[et].fwd for et in ets]
         dsts = [cur[et[2]] for et in ets]
@@ -122,50 +121,50 @@ class NeighborSampler:
         s = N.stream_ptr(dev)
         N.check(lib.hgnn_sample_hop_count(R, a_rp, a_nr, a_dst, a_nd, fanout, a_out, N.ptr(d_tot),
                                           N.ptr(ws), ws.numel(), s), "hgnn_sample_hop_count")
-        back = [d_tot] + ([c for _, c in checks] if hop == 0 else [])
-        vals = torch.cat(back).tolist()                    # the hop's one sync
-        self._raise_bad_seeds(checks if hop == 0 else [], vals[R:])
-        totals = vals[:R]
-        cols = torch.empty(sum(totals), dtype=torch.int32, device=dev)
-        views, o = [], 0
-        for t in totals:
-            views.append(cols[o:o + t])
+        totals = d_tot.tolist()                            # the hop's first sync
+        # one buffer, at least one element: every relation's output address is non-null, an
+        # empty relation's included (an empty tensor view reports a null data_ptr)
+        buf = torch.empty(max(sum(totals), 1), dtype=torch.int32, device=dev)
+        cols = buf[:sum(totals)]
+        outs, o = (N._p * max(R, 1))(), 0
+        for r, t in enumerate(totals):
+            outs[r] = buf.data_ptr() + 4 * o
             o += t
         N.check(lib.hgnn_sample_hop_fill(R, a_rp, N.ptr_array([x.col for x in g]), a_nr, a_dst,
-                                         a_nd, fanout, seed, a_out, N.ptr_array(views), s),
+                                         a_nd, fanout, seed, a_out, outs, s),
                 "hgnn_sample_hop_fill")
         return dict(zip(ets, rps)), cols, dict(zip(ets, totals))
 
-    def _raise_bad_seeds(self, checks, vals):
-        for i, (t, _) in enumerate(checks):
-            lo, hi, dup = vals[3 * i:3 * i + 3]
-            if lo < 0 or hi >= self.num_nodes[t]:
-                raise ValueError(f"seed ids of type {t!r} out of range")
-            if dup:
-                raise ValueError(f"seed ids of type {t!r} must be distinct")
-
-    def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor):
+    def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor, check: bool = False):
+        """Next node set of type ``t``; returns (nodes, local, count2): ``count2[0]`` = the
+        node count, ``count2[1]`` the prefix check's flags when ``check`` (bit 0 a repeated
+        prefix id, bit 1 one outside the type's id range), read back by the caller."""
         lib, dev = N.lib(), self.device
         n_p, n_i = int(prefix.numel()), int(items.numel())
         nodes = torch.empty(n_p + n_i, dtype=torch.int32, device=dev)
         local = torch.empty(n_i, dtype=torch.int32, device=dev)
-        count = torch.empty(1, dtype=torch.int32, device=dev)
+        count = torch.zeros(2, dtype=torch.int32, device=dev) if check else \
+            torch.empty(2, dtype=torch.int32, device=dev)
         ws = N.workspace(lib.hgnn_relabel_ws_bytes(n_p, n_i), dev)
-        N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, N.ptr(local),
-                                 N.ptr(nodes), N.ptr(count), N.ptr(ws), ws.numel(),
-                                 N.stream_ptr(dev)), "hgnn_relabel")
-        return nodes, local, count      # nodes[:count] is the node set (count read by the caller)
+        if check:
+            N.check(lib.hgnn_relabel_checked(N.ptr(prefix), n_p, self.num_nodes[t], N.ptr(items),
+                                             n_i, N.ptr(local), N.ptr(nodes), N.ptr(count),
+                                             N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                    "hgnn_relabel_checked")
+        else:
+            N.check(lib.hgnn_relabel(N.ptr(prefix), n_p, N.ptr(items), n_i, N.ptr(local),
+                                     N.ptr(nodes), N.ptr(count), N.ptr(ws), ws.numel(),
+                                     N.stream_ptr(dev)), "hgnn_relabel")
+        return nodes, local, count
 
     def sample(self, seeds: Mapping[str, torch.Tensor], seed: int = 0) -> MiniBatch:
         cur: Dict[str, torch.Tensor] = {}
-        checks = []
         for t, s in seeds.items():
-            s = _i32(s.to(self.device))
-            if s.numel():    # [min, max, any duplicate], read back with the first hop's totals
-                ss = torch.sort(s).values
-                dup = (ss[1:] == ss[:-1]).any().to(s.dtype)
-                checks.append((t, torch.stack([ss[0], ss[-1], dup])))
-            cur[t] = s
+            if t not in self.num_nodes:
+                raise ValueError(f"unknown node type {t!r}")
+            cur[t] = _i32(s.to(self.device))
+        # the seeds are checked (distinct, in range) by the first hop's relabel, whose prefix
+        # they are; its flags come back with the node counts (no sync of its own)
         nodes, blocks = [cur], []
         for hop, fanout in enumerate(self.fanouts):
             hop_seed = (int(seed) * 1_000_003 + hop) & 0xFFFFFFFFFFFFFFFF
@@ -174,7 +173,7 @@ class NeighborSampler:
             types = sorted(set(cur) | {et[0] for et in self.relations if et[2] in cur})
             ets = sorted((et for et in self.relations if et[2] in cur),
                          key=lambda et: types.index(et[0]))
-            rowptr, cols, totals = self._hop(ets, cur, fanout, hop_seed, checks, hop)
+            rowptr, cols, totals = self._hop(ets, cur, fanout, hop_seed)
             relabeled = {}
             o = 0
             for t in types:
@@ -183,8 +182,15 @@ class NeighborSampler:
                 items = cols[o:o + n_t]
                 o += n_t
                 prefix = cur.get(t, torch.empty(0, dtype=torch.int32, device=self.device))
-                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items)
-            sizes = torch.cat([relabeled[t][3] for t in types]).tolist()   # one sync per hop
+                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items, check=hop == 0)
+            vals = torch.cat([relabeled[t][3] for t in types]).tolist()    # one sync per hop
+            sizes = vals[0::2]
+            if hop == 0:
+                for t, flags in zip(types, vals[1::2]):
+                    if flags & 2:
+                        raise ValueError(f"seed ids of type {t!r} out of range")
+                    if flags & 1:
+                        raise ValueError(f"seed ids of type {t!r} must be distinct")
             nxt: Dict[str, torch.Tensor] = {}
             local: Dict[EdgeType, torch.Tensor] = {}
             for t, size in zip(types, sizes):
