@@ -338,6 +338,18 @@ int hgnn_relabel_checked(const int32_t* prefix, int64_t n_prefix, int64_t id_lim
                          const int32_t* items, int64_t n_items, int32_t* local_out,
                          int32_t* nodes_out, int32_t* d_count2, void* ws, size_t ws_bytes,
                          hgnn_stream_t stream);
+/* Every node type of a hop in one call (n_types <= 8): type t's prefix prefix[t][n_prefix[t]],
+ * its items the consecutive range n_items[t] of `items` (types in order), its node set into
+ * nodes_out[t] (n_prefix[t] + n_items[t] entries), the local ids of all items into local_out
+ * (per type, as hgnn_relabel); ids < id_limit[t] (required when n_types > 1: the table is keyed
+ * by id * n_types + t, so id_limit * n_types < 2^31).  d_count2: with check, (count, flags) per
+ * type as hgnn_relabel_checked; without, the counts only.  The same nodes and local ids as one
+ * hgnn_relabel per type.  ws: hgnn_relabel_multi_ws_bytes(sum of n_prefix, sum of n_items). */
+size_t hgnn_relabel_multi_ws_bytes(int64_t n_prefix_total, int64_t n_items_total);
+int hgnn_relabel_multi(int32_t n_types, const int32_t* const* prefix, const int64_t* n_prefix,
+                       const int64_t* id_limit, const int32_t* items, const int64_t* n_items,
+                       int32_t* local_out, int32_t* const* nodes_out, int32_t* d_count2,
+                       int32_t check, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of

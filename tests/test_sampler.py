@@ -289,3 +289,33 @@ def test_hop_batch_equals_per_relation_sampling(fanout):
     rowptr, cols, totals = s._hop([("a", "r1", "b")], bad, fanout, 1)
     deg = rowptr[("a", "r1", "b")].diff().tolist()
     assert deg[1] == 0 and deg[2] == 0
+
+
+def test_relabel_multi_equals_per_type_relabel():
+    """hgnn_relabel_multi (every type of a hop in one call, table keyed by id x types + type)
+    gives each type the node set and local ids of its own hgnn_relabel call — the same id in two
+    types stays two nodes."""
+    from truth_recommendation_gnn_amd import sampler
+    rng = np.random.default_rng(9)
+    num = {"a": 700, "b": 300, "c": 50}
+    ei = torch.zeros(2, 1, dtype=torch.int64, device=DEV)
+    s = sampler.NeighborSampler(num, {("a", "r", "a"): ei}, [("a", "r", "a")], [3])
+    types = ["a", "b", "c"]
+    cur = {"a": torch.from_numpy(rng.permutation(700)[:40].astype(np.int32)).to(DEV),
+           "b": torch.from_numpy(rng.permutation(300)[:25].astype(np.int32)).to(DEV)}
+    items = {"a": rng.integers(0, 300, 2000), "b": rng.integers(0, 300, 900),
+             "c": rng.integers(0, 50, 70)}                  # "a" ids overlap "b" ids
+    items["a"][:30] = cur["a"][:30].cpu().numpy()
+    allit = torch.from_numpy(np.concatenate([items[t] for t in types]).astype(np.int32)).to(DEV)
+    n_items = [len(items[t]) for t in types]
+    nodes, local, counts = s._relabel_hop(types, cur, allit, n_items)
+    counts = counts.tolist()
+    o = 0
+    for i, t in enumerate(types):
+        pre = cur.get(t, torch.empty(0, dtype=torch.int32, device=DEV))
+        it = allit[o:o + n_items[i]]
+        n1, l1, c1 = s._relabel(t, pre, it)
+        assert counts[2 * i] == int(c1[0]) and counts[2 * i + 1] == 0
+        assert torch.equal(nodes[t][:counts[2 * i]], n1[:int(c1[0])]), t
+        assert torch.equal(local[o:o + n_items[i]], l1), t
+        o += n_items[i]

@@ -82,6 +82,9 @@ _SIGS = {
     "hgnn_relabel": (_c_i32, [_p, _c_i64, _p, _c_i64, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_relabel_checked": (_c_i32, [_p, _c_i64, _c_i64, _p, _c_i64, _p, _p, _p, _p, _c_sz,
                                       _p]),
+    "hgnn_relabel_multi_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_relabel_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _c_i32, _p, _c_sz,
+                                    _p]),
     "hgnn_topk_metrics": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _c_i32, _p, _p, _p,
                                    _p]),
     "hgnn_topk_metrics_rows": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _c_i32, _p,

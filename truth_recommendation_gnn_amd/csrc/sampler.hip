@@ -137,32 +137,47 @@ __global__ void __launch_bounds__(256) k_hop_fill(const HopTab t) {
 }
 
 // ---- relabel: a hash set over the ids this call sees, O(n_prefix + n_items) work --------------
+// One call relabels every node type of a hop: the table is keyed by id * T + type, the items of
+// the types lie in consecutive ranges of one buffer, and the new ids of a type are ranked by one
+// exclusive scan over all items (a type's ranks start at the scan's value at its first item).
 // slot arrays (capacity a power of two >= 2·(n_prefix + n_items)): key (-1 empty), ppos (prefix
 // position or -1), first (smallest item position of a non-prefix id; atomicMin, so deterministic)
+constexpr int kRelabelMaxTypes = 8;
 struct RelabelTab {
   int32_t* key;
   int32_t* ppos;
   int32_t* first;
-  int32_t* nflags;   // ~flags of the prefix check (starts all ones with the key memset)
+  int32_t* nflags;   // per type: ~flags of the prefix check (all ones from the key memset)
   uint32_t mask;
   int shift;   // 64 - log2(capacity)
-  int64_t id_limit;  // prefix ids must lie in [0, id_limit) (checked only if > 0)
+  int32_t T;   // node types
+  const int32_t* prefix[kRelabelMaxTypes];
+  int32_t* nodes[kRelabelMaxTypes];
+  int64_t id_limit[kRelabelMaxTypes];   // checked prefix ids must lie in [0, id_limit)
+  int64_t p_off[kRelabelMaxTypes + 1];  // concatenated prefix positions per type
+  int64_t i_off[kRelabelMaxTypes + 1];  // item ranges per type
 };
 
-// slot of `id`; *found = the id was already in the table (inserted by another thread)
-__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t id,
+__device__ __forceinline__ int rl_type(const int64_t* off, int T, int64_t i) {
+  int t = 0;
+  while (t + 1 < T && i >= off[t + 1]) ++t;
+  return t;
+}
+
+// slot of `key`; *found = the key was already in the table (inserted by another thread)
+__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t key,
                                                       bool* found = nullptr) {
-  uint32_t s = (uint32_t)(((uint64_t)(uint32_t)id * 0x9E3779B97F4A7C15ull) >> t.shift);
+  uint32_t s = (uint32_t)(((uint64_t)(uint32_t)key * 0x9E3779B97F4A7C15ull) >> t.shift);
   for (uint32_t probe = 0; probe <= t.mask; ++probe) {   // ends: load factor <= 1/2
     const int32_t k = __atomic_load_n(&t.key[s], __ATOMIC_RELAXED);
-    if (k == id) {
+    if (k == key) {
       if (found) *found = true;
       return s;
     }
     if (k == -1) {
-      const int32_t old = atomicCAS(&t.key[s], -1, id);
+      const int32_t old = atomicCAS(&t.key[s], -1, key);
       if (old == -1) return s;
-      if (old == id) {
+      if (old == key) {
         if (found) *found = true;
         return s;
       }
@@ -172,47 +187,47 @@ __device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32
   return 0;   // unreachable with the capacity the host sizes
 }
 
-// Prefix ids (the previous frontier, or the seeds) are expected distinct and in range: a
-// repeated id (found already inserted) clears bit 0 of nflags, an id outside [0, id_limit)
-// bit 1 — the caller reads the flags with the node count it reads anyway (no extra sync).
-__global__ void k_relabel_prefix(RelabelTab t, const int32_t* prefix, int64_t n_prefix,
-                                 int32_t* nodes) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_prefix) return;
-  const int32_t id = prefix[i];
-  nodes[i] = id;
-  if (t.id_limit > 0 && (id < 0 || id >= t.id_limit)) {   // flagged, never inserted
-    if (t.nflags) atomicAnd(t.nflags, ~2);
+// Prefix ids (the previous frontier, or the seeds) are expected distinct and in range: with the
+// check on, a repeated id (found already inserted) clears bit 0 of its type's nflags word, an id
+// outside [0, id_limit) bit 1 (that id is not inserted) — read back with the node counts.
+__global__ void k_relabel_prefix(RelabelTab t) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= t.p_off[t.T]) return;
+  const int ty = rl_type(t.p_off, t.T, g);
+  const int64_t i = g - t.p_off[ty];
+  const int32_t id = t.prefix[ty][i];
+  t.nodes[ty][i] = id;
+  if (id < 0 || (t.id_limit[ty] > 0 && id >= t.id_limit[ty])) {   // flagged, never inserted
+    if (t.nflags) atomicAnd(&t.nflags[ty], ~2);
     return;
   }
   bool found = false;
-  const uint32_t s = rl_find_or_insert(t, id, &found);
-  if (found && t.nflags) atomicAnd(t.nflags, ~1);
+  const uint32_t s = rl_find_or_insert(t, id * t.T + ty, &found);
+  if (found && t.nflags) atomicAnd(&t.nflags[ty], ~1);
   t.ppos[s] = (int32_t)i;   // one writer per slot when the prefix ids are distinct
 }
 
-__global__ void k_relabel_insert(RelabelTab t, const int32_t* items, int64_t n_items,
-                                 int32_t* slot_of) {
+__global__ void k_relabel_insert(RelabelTab t, const int32_t* items, int32_t* slot_of) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_items) return;
-  const uint32_t s = rl_find_or_insert(t, items[k]);
+  if (k >= t.i_off[t.T]) return;
+  const int ty = rl_type(t.i_off, t.T, k);
+  const uint32_t s = rl_find_or_insert(t, items[k] * t.T + ty);
   slot_of[k] = (int32_t)s;
   if (t.ppos[s] < 0) atomicMin(&t.first[s], (int32_t)k);
 }
 
-__global__ void k_relabel_flags(RelabelTab t, const int32_t* slot_of, int64_t n_items,
-                                int32_t* flags) {
+__global__ void k_relabel_flags(RelabelTab t, const int32_t* slot_of, int32_t* flags) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_items) return;
+  if (k >= t.i_off[t.T]) return;
   const int32_t s = slot_of[k];
   flags[k] = t.ppos[s] < 0 && t.first[s] == (int32_t)k;
 }
 
 __global__ void k_relabel_assign(RelabelTab t, const int32_t* items, const int32_t* slot_of,
-                                 const int32_t* rank, int64_t n_items, int64_t n_prefix,
-                                 int32_t* local, int32_t* nodes) {
+                                 const int32_t* rank, int32_t* local) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n_items) return;
+  if (k >= t.i_off[t.T]) return;
+  const int ty = rl_type(t.i_off, t.T, k);
   const int32_t s = slot_of[k];
   const int32_t pp = t.ppos[s];
   if (pp >= 0) {
@@ -220,15 +235,20 @@ __global__ void k_relabel_assign(RelabelTab t, const int32_t* items, const int32
     return;
   }
   const int32_t f = t.first[s];
-  const int32_t l = (int32_t)(n_prefix + rank[f]);
+  const int64_t n_prefix = t.p_off[ty + 1] - t.p_off[ty];
+  const int32_t l = (int32_t)(n_prefix + rank[f] - rank[t.i_off[ty]]);
   local[k] = l;
-  if (f == (int32_t)k) nodes[l] = items[k];
+  if (f == (int32_t)k) t.nodes[ty][l] = items[k];
 }
 
-__global__ void k_relabel_count(const int32_t* rank, int64_t n_items, int64_t n_prefix,
-                                const int32_t* nflags, int32_t* d_count) {
-  d_count[0] = (int32_t)(n_prefix + (n_items > 0 ? rank[n_items] : 0));
-  if (nflags) d_count[1] = ~*nflags;
+__global__ void k_relabel_count(RelabelTab t, const int32_t* rank, int32_t* d_count2) {
+  const int ty = threadIdx.x;
+  if (ty >= t.T) return;
+  const int64_t n_new = t.i_off[t.T] > 0 ? rank[t.i_off[ty + 1]] - rank[t.i_off[ty]] : 0;
+  // checked calls return (count, flags) per type; the plain single-type call only the count
+  const int stride = t.nflags ? 2 : 1;
+  d_count2[stride * ty] = (int32_t)(t.p_off[ty + 1] - t.p_off[ty] + n_new);
+  if (t.nflags) d_count2[2 * ty + 1] = ~t.nflags[ty];
 }
 
 static int64_t relabel_cap(int64_t n) {
@@ -248,10 +268,10 @@ static size_t relabel_ws(int64_t n_prefix, int64_t n_items, size_t* scan_b) {
 
 using namespace hgnn;
 
-static int relabel(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
-                   const int32_t* items, int64_t n_items, int32_t* local_out, int32_t* nodes_out,
-                   int32_t* d_count, bool check, void* ws, size_t ws_bytes,
-                   hipStream_t stream);
+static int relabel(int32_t T, const int32_t* const* prefix, const int64_t* n_prefix,
+                   const int64_t* id_limit, const int32_t* items, const int64_t* n_items,
+                   int32_t* local_out, int32_t* const* nodes_out, int32_t* d_count, bool check,
+                   void* ws, size_t ws_bytes, hipStream_t stream);
 
 extern "C" {
 
@@ -402,65 +422,94 @@ size_t hgnn_relabel_ws_bytes(int64_t n_prefix, int64_t n_items) {
 int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, int64_t n_items,
                  int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
                  size_t ws_bytes, hgnn_stream_t stream_) {
-  return relabel(prefix, n_prefix, 0, items, n_items, local_out, nodes_out, d_count, false, ws,
-                 ws_bytes, as_stream(stream_));
+  int32_t* nodes[1] = {nodes_out};
+  const int64_t zero = 0;
+  return relabel(1, &prefix, &n_prefix, &zero, items, &n_items, local_out, nodes, d_count, false,
+                 ws, ws_bytes, as_stream(stream_));
 }
 
 int hgnn_relabel_checked(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
                          const int32_t* items, int64_t n_items, int32_t* local_out,
                          int32_t* nodes_out, int32_t* d_count2, void* ws, size_t ws_bytes,
                          hgnn_stream_t stream_) {
-  return relabel(prefix, n_prefix, id_limit, items, n_items, local_out, nodes_out, d_count2, true,
-                 ws, ws_bytes, as_stream(stream_));
+  int32_t* nodes[1] = {nodes_out};
+  return relabel(1, &prefix, &n_prefix, &id_limit, items, &n_items, local_out, nodes, d_count2,
+                 true, ws, ws_bytes, as_stream(stream_));
+}
+
+size_t hgnn_relabel_multi_ws_bytes(int64_t n_prefix_total, int64_t n_items_total) {
+  size_t scan_b = 0;
+  return relabel_ws(n_prefix_total < 0 ? 0 : n_prefix_total,
+                    n_items_total < 0 ? 0 : n_items_total, &scan_b);
+}
+
+int hgnn_relabel_multi(int32_t n_types, const int32_t* const* prefix, const int64_t* n_prefix,
+                       const int64_t* id_limit, const int32_t* items, const int64_t* n_items,
+                       int32_t* local_out, int32_t* const* nodes_out, int32_t* d_count2,
+                       int32_t check, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  return relabel(n_types, prefix, n_prefix, id_limit, items, n_items, local_out, nodes_out,
+                 d_count2, check != 0, ws, ws_bytes, as_stream(stream_));
 }
 
 }  // extern "C"
 
-static int relabel(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
-                   const int32_t* items, int64_t n_items, int32_t* local_out, int32_t* nodes_out,
-                   int32_t* d_count, bool check, void* ws, size_t ws_bytes,
-                   hipStream_t stream) {
-  if (n_prefix < 0 || n_items < 0 || n_prefix + n_items >= (int64_t)INT32_MAX / 2)
-    return fail(HGNN_E_ARG, "relabel: bad sizes");
-  if (!d_count || (n_prefix > 0 && (!prefix || !nodes_out)) ||
-      (n_items > 0 && (!items || !local_out || !nodes_out)))
-    return fail(HGNN_E_ARG, "relabel: null pointer");
+static int relabel(int32_t T, const int32_t* const* prefix, const int64_t* n_prefix,
+                   const int64_t* id_limit, const int32_t* items, const int64_t* n_items,
+                   int32_t* local_out, int32_t* const* nodes_out, int32_t* d_count, bool check,
+                   void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (T < 1 || T > kRelabelMaxTypes || !prefix || !n_prefix || !id_limit || !n_items ||
+      !nodes_out || !d_count)
+    return fail(HGNN_E_ARG, "relabel: n_types=%d (1..%d) or null array", T, kRelabelMaxTypes);
+  RelabelTab t{};
+  t.T = T;
+  t.p_off[0] = t.i_off[0] = 0;
+  int64_t max_limit = 0;
+  for (int ty = 0; ty < T; ++ty) {
+    if (n_prefix[ty] < 0 || n_items[ty] < 0) return fail(HGNN_E_ARG, "relabel: bad sizes");
+    if ((n_prefix[ty] > 0 && !prefix[ty]) || (n_prefix[ty] + n_items[ty] > 0 && !nodes_out[ty]))
+      return fail(HGNN_E_ARG, "relabel: type %d: null pointer", ty);
+    t.prefix[ty] = prefix[ty];
+    t.nodes[ty] = nodes_out[ty];
+    t.id_limit[ty] = id_limit[ty];
+    max_limit = std::max<int64_t>(max_limit, id_limit[ty]);
+    t.p_off[ty + 1] = t.p_off[ty] + n_prefix[ty];
+    t.i_off[ty + 1] = t.i_off[ty] + n_items[ty];
+  }
+  const int64_t np = t.p_off[T], ni = t.i_off[T];
+  if (np + ni >= (int64_t)INT32_MAX / 2) return fail(HGNN_E_ARG, "relabel: bad sizes");
+  if (T > 1 && (max_limit <= 0 || max_limit * T >= (int64_t)INT32_MAX))
+    return fail(HGNN_E_ARG, "relabel: %d types need id limits with limit x types < 2^31", T);
+  if (ni > 0 && (!items || !local_out)) return fail(HGNN_E_ARG, "relabel: null items/local");
   size_t scan_b = 0;
-  if (ws_bytes < relabel_ws(n_prefix, n_items, &scan_b))
+  if (ws_bytes < relabel_ws(np, ni, &scan_b))
     return fail(HGNN_E_WS, "relabel: workspace too small");
-  const int64_t cap = relabel_cap(n_prefix + n_items);
+  const int64_t cap = relabel_cap(np + ni);
   int log2cap = 0;
   while ((int64_t(1) << log2cap) < cap) ++log2cap;
   Workspace w(ws, ws_bytes);
-  RelabelTab t;
-  t.key = w.take<int32_t>(2 * cap + 64);   // key, ppos and the flags word: one 0xFF memset
+  t.key = w.take<int32_t>(2 * cap + 64);   // key, ppos and the flag words: one 0xFF memset
   t.ppos = t.key + cap;
   t.nflags = check ? t.key + 2 * cap : nullptr;
-  t.id_limit = id_limit;
   t.first = w.take<int32_t>(cap);
   t.mask = (uint32_t)(cap - 1);
   t.shift = 64 - log2cap;
-  int32_t* slot_of = w.take<int32_t>(n_items + 1);
-  int32_t* flags = w.take<int32_t>(n_items + 1);
-  int32_t* rank = w.take<int32_t>(n_items + 1);
+  int32_t* slot_of = w.take<int32_t>(ni + 1);
+  int32_t* flags = w.take<int32_t>(ni + 1);
+  int32_t* rank = w.take<int32_t>(ni + 1);
   void* scan_ws = w.take<char>(scan_b);
-  (void)hipMemsetAsync(t.key, 0xFF, (size_t)cap * 8 + 4, stream);   // key = ppos = -1, flags
+  (void)hipMemsetAsync(t.key, 0xFF, (size_t)cap * 8 + 4 * kRelabelMaxTypes, stream);
   (void)hipMemsetAsync(t.first, 0x7F, (size_t)cap * 4, stream);     // "infinity"
-  if (n_prefix > 0)
-    hipLaunchKernelGGL(k_relabel_prefix, dim3((unsigned)cdiv(n_prefix, 256)), dim3(256), 0,
-                       stream, t, prefix, n_prefix, nodes_out);
-  if (n_items > 0) {
-    const unsigned g = (unsigned)cdiv(n_items, 256);
-    hipLaunchKernelGGL(k_relabel_insert, dim3(g), dim3(256), 0, stream, t, items, n_items,
-                       slot_of);
-    hipLaunchKernelGGL(k_relabel_flags, dim3(g), dim3(256), 0, stream, t, slot_of, n_items,
-                       flags);
+  if (np > 0)
+    hipLaunchKernelGGL(k_relabel_prefix, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, stream, t);
+  if (ni > 0) {
+    const unsigned g = (unsigned)cdiv(ni, 256);
+    hipLaunchKernelGGL(k_relabel_insert, dim3(g), dim3(256), 0, stream, t, items, slot_of);
+    hipLaunchKernelGGL(k_relabel_flags, dim3(g), dim3(256), 0, stream, t, slot_of, flags);
     if (int rc = check_launch("k_relabel_flags")) return rc;
-    if (int rc = exclusive_scan_i32(flags, rank, n_items, scan_ws, &scan_b, stream)) return rc;
+    if (int rc = exclusive_scan_i32(flags, rank, ni, scan_ws, &scan_b, stream)) return rc;
     hipLaunchKernelGGL(k_relabel_assign, dim3(g), dim3(256), 0, stream, t, items, slot_of, rank,
-                       n_items, n_prefix, local_out, nodes_out);
+                       local_out);
   }
-  hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(1), 0, stream, rank, n_items, n_prefix,
-                     t.nflags, d_count);
+  hipLaunchKernelGGL(k_relabel_count, dim3(1), dim3(64), 0, stream, t, rank, d_count);
   return check_launch("relabel");
 }

@@ -135,6 +135,29 @@ class NeighborSampler:
                 "hgnn_sample_hop_fill")
         return dict(zip(ets, rps)), cols, dict(zip(ets, totals))
 
+    def _relabel_hop(self, types, cur, items: torch.Tensor, n_items):
+        """Next node sets of every type of the hop in one call (``hgnn_relabel_multi``): type
+        t's prefix is ``cur[t]`` (the previous frontier, or the seeds), its items the t-th
+        consecutive range of ``items``.  Returns (nodes per type, local ids of all items,
+        counts) with counts[2t] = t's node count and counts[2t+1] its prefix-check flags (read
+        on the first hop, whose prefix is the seeds; later frontiers are distinct by
+        construction)."""
+        lib, dev = N.lib(), self.device
+        empty = torch.empty(0, dtype=torch.int32, device=dev)
+        prefixes = [cur.get(t, empty) for t in types]
+        n_pre = [int(p.numel()) for p in prefixes]
+        nodes = {t: torch.empty(max(n_pre[i] + n_items[i], 1), dtype=torch.int32, device=dev)
+                 for i, t in enumerate(types)}
+        local = torch.empty(max(int(items.numel()), 1), dtype=torch.int32, device=dev)
+        counts = torch.zeros(2 * len(types), dtype=torch.int32, device=dev)
+        ws = N.workspace(lib.hgnn_relabel_multi_ws_bytes(sum(n_pre), int(items.numel())), dev)
+        N.check(lib.hgnn_relabel_multi(
+            len(types), N.ptr_array(prefixes), N.i64_array(n_pre),
+            N.i64_array([self.num_nodes[t] for t in types]), N.ptr(items) if items.numel() else
+            N.ptr(local), N.i64_array(n_items), N.ptr(local), N.ptr_array([nodes[t] for t in types]),
+            N.ptr(counts), 1, N.ptr(ws), ws.numel(), N.stream_ptr(dev)), "hgnn_relabel_multi")
+        return nodes, local[:int(items.numel())], counts
+
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor, check: bool = False):
         """Next node set of type ``t``; returns (nodes, local, count2): ``count2[0]`` = the
         node count, ``count2[1]`` the prefix check's flags when ``check`` (bit 0 a repeated
@@ -174,16 +197,9 @@ class NeighborSampler:
             ets = sorted((et for et in self.relations if et[2] in cur),
                          key=lambda et: types.index(et[0]))
             rowptr, cols, totals = self._hop(ets, cur, fanout, hop_seed)
-            relabeled = {}
-            o = 0
-            for t in types:
-                src_ets = [et for et in ets if et[0] == t]
-                n_t = sum(totals[et] for et in src_ets)
-                items = cols[o:o + n_t]
-                o += n_t
-                prefix = cur.get(t, torch.empty(0, dtype=torch.int32, device=self.device))
-                relabeled[t] = (src_ets,) + self._relabel(t, prefix, items, check=hop == 0)
-            vals = torch.cat([relabeled[t][3] for t in types]).tolist()    # one sync per hop
+            n_items = [sum(totals[et] for et in ets if et[0] == t) for t in types]
+            nodes_t, local_all, counts = self._relabel_hop(types, cur, cols, n_items)
+            vals = counts.tolist()                                         # one sync per hop
             sizes = vals[0::2]
             if hop == 0:
                 for t, flags in zip(types, vals[1::2]):
@@ -191,15 +207,12 @@ class NeighborSampler:
                         raise ValueError(f"seed ids of type {t!r} out of range")
                     if flags & 1:
                         raise ValueError(f"seed ids of type {t!r} must be distinct")
-            nxt: Dict[str, torch.Tensor] = {}
+            nxt: Dict[str, torch.Tensor] = {t: nodes_t[t][:n] for t, n in zip(types, sizes)}
             local: Dict[EdgeType, torch.Tensor] = {}
-            for t, size in zip(types, sizes):
-                src_ets, nodes_buf, loc, _ = relabeled[t]
-                nxt[t] = nodes_buf[:size]
-                o = 0
-                for et in src_ets:
-                    local[et] = loc[o:o + totals[et]]
-                    o += totals[et]
+            o = 0
+            for et in ets:                       # ets are grouped by source type in `types` order
+                local[et] = local_all[o:o + totals[et]]
+                o += totals[et]
             csrs = {et: RelationCSR.from_csr(rowptr[et], local[et], int(nxt[et[0]].numel()),
                                              int(cur[et[2]].numel()),
                                              may_have_heavy_rows=fanout < 0)
@@ -216,7 +229,7 @@ def forward_blocks(model: HeteroSAGE, batch: MiniBatch,
     """``model`` on the sampled blocks; returns the seeds' embeddings per type (seed order)."""
     if len(batch.blocks) != len(model.layers):
         raise ValueError(f"{len(batch.blocks)} blocks for a {len(model.layers)}-layer model")
-    h = {t: x_dict[t].index_select(0, ids.long()) for t, ids in batch.nodes[0].items()}
+    h = {t: x_dict[t].index_select(0, ids) for t, ids in batch.nodes[0].items()}   # int32 ids
     for convs, blk in zip(model.layers, batch.blocks):
         # one fused hetero layer per block (ops.hetero_layer: per destination type the K1 means of
         # its relations and one K3 over [aggr..., root prefix], one autograd node for the layer)
