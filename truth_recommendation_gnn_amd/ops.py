@@ -194,7 +194,8 @@ def _score_gather(U, P, grouped, mode, cscale, inv_e, out, accumulate, tag):
         slab = torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
     E = int(grouped.col.numel())
     nb = gather_bytes(E, grouped.n_rows, d, False) + 4 * grouped.n_rows * d
-    cb = gather_compulsory_bytes(E, grouped.n_rows, int(U.shape[0]), d, False) + 4 * grouped.n_rows * d
+    cb = (gather_compulsory_bytes(E, grouped.n_rows, int(U.shape[0]), d, False)
+          + 4 * grouped.n_rows * d)
     with _timed(f"score_gather_{tag}[{grouped.n_rows}<-{U.shape[0]}]x{d}", nb, cb):
         N.check(N.lib().hgnn_score_gather(
             N.ptr(U), U.shape[0], N.ptr(P), d, N.ptr(grouped.rowptr), N.ptr(grouped.col),

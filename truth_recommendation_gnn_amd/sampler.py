@@ -20,7 +20,7 @@ With fanouts at least the maximum degree, the seeds' embeddings equal the full-g
 from __future__ import annotations
 
 import dataclasses
-from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+from typing import Dict, List, Mapping, Sequence, Tuple
 
 import torch
 
@@ -151,11 +151,12 @@ class NeighborSampler:
         local = torch.empty(max(int(items.numel()), 1), dtype=torch.int32, device=dev)
         counts = torch.zeros(2 * len(types), dtype=torch.int32, device=dev)
         ws = N.workspace(lib.hgnn_relabel_multi_ws_bytes(sum(n_pre), int(items.numel())), dev)
+        items_p = N.ptr(items) if items.numel() else N.ptr(local)   # a non-null address
         N.check(lib.hgnn_relabel_multi(
             len(types), N.ptr_array(prefixes), N.i64_array(n_pre),
-            N.i64_array([self.num_nodes[t] for t in types]), N.ptr(items) if items.numel() else
-            N.ptr(local), N.i64_array(n_items), N.ptr(local), N.ptr_array([nodes[t] for t in types]),
-            N.ptr(counts), 1, N.ptr(ws), ws.numel(), N.stream_ptr(dev)), "hgnn_relabel_multi")
+            N.i64_array([self.num_nodes[t] for t in types]), items_p, N.i64_array(n_items),
+            N.ptr(local), N.ptr_array([nodes[t] for t in types]), N.ptr(counts), 1, N.ptr(ws),
+            ws.numel(), N.stream_ptr(dev)), "hgnn_relabel_multi")
         return nodes, local[:int(items.numel())], counts
 
     def _relabel(self, t: str, prefix: torch.Tensor, items: torch.Tensor, check: bool = False):
