@@ -174,6 +174,9 @@ def test_source_blocked_gathers_match_oracle(monkeypatch, d, slice_rows):
     monkeypatch.setattr(ops, "GATHER_BLOCK_SLICE", 40 * d * 4)
     assert ops.gather_blocks(g) > 3
     close(ops.scatter_mean_bwd(g.to(DEV), csr), x.grad)
+    acc = torch.full((n_src, d), 2.0, device=DEV)          # K2 accumulating into a buffer
+    ops.scatter_mean_bwd(g.to(DEV), csr, out=acc)
+    close(acc, x.grad + 2.0)
 
 
 def test_gather_is_deterministic_bitwise():
