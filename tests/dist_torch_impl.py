@@ -98,7 +98,7 @@ class TorchImpl:
     gather_mean_raw = mean_gather
 
     @staticmethod
-    def weighted_gather_raw(x, rel, w_fwd):
+    def weighted_gather_raw(x, rel, w_fwd, row_w=None):
         ei, _, n_dst = rel
         return torch.zeros(n_dst, x.shape[1], dtype=x.dtype).index_add(0, ei[1],
                                                                         x[ei[0]] * w_fwd[:, None])

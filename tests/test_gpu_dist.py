@@ -176,3 +176,32 @@ def test_sharded_halo_relations_on_hip_kernels_match_oracle(world, kind, slice_i
         assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
         assert r["grad_err"] < 1e-4, r
         assert r["step_loss_err"] < 1e-4 and r["step_grad_err"] < 1e-4, r
+
+
+@pytest.mark.parametrize("world,kind,slice_inputs", [(3, "rel4", True), (2, "engage2", True),
+                                                     (3, "rgcn", False)])
+def test_sharded_step_with_source_blocked_gathers_matches_oracle(monkeypatch, world, kind,
+                                                                 slice_inputs):
+    """The sharded step with every gather forced into source-block passes (what tables of
+    >= 2 GB get: the layer-1 slice mean over the whole input user table, the row-scaled
+    post partial sums, the K2s), via the switches the worker processes read at import: the
+    same oracle bar as the one-pass runs above."""
+    monkeypatch.setenv("HGNN_GATHER_BLOCK_GB", "1e-9")
+    monkeypatch.setenv("HGNN_GATHER_BLOCK_MB", "0.002")        # 2 KB of rows per block
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_case_worker, args=(r, world, port, q, kind, slice_inputs))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+    errs = [r["error"] for r in res if "error" in r]
+    assert not errs, errs
+    for r in res:
+        assert r["loss_err"] < 1e-4, r
+        assert r["user_err"] < 1e-4 and r["post_err"] < 1e-4, r
+        assert r["grad_err"] < 1e-4, r
+        assert r["step_loss_err"] < 1e-4 and r["step_grad_err"] < 1e-4, r

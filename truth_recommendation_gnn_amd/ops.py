@@ -1069,10 +1069,23 @@ def await_pending(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def weighted_gather_raw(x_src: torch.Tensor, csr: RelationCSR, w_fwd: torch.Tensor) -> torch.Tensor:
-    """``out[i] = sum_{p in row i} w_fwd[p] x_src[col[p]]`` (K1 with per-edge weights)."""
+def weighted_gather_raw(x_src: torch.Tensor, csr: RelationCSR, w_fwd: torch.Tensor,
+                        row_w: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``out[i] = sum_{p in row i} w_fwd[p] x_src[col[p]]`` (K1 with per-edge weights).
+    ``row_w``: the same weights when they are constant per row (w_fwd[p] = row_w[i], the
+    sharded step's 1/deg_global): a source table of several GB is then gathered in
+    source-block passes scaled per row (see :func:`gather_blocks`)."""
     x_src = _check_f32(x_src, "weighted_gather")
     out = torch.empty(csr.n_dst, x_src.shape[1], dtype=torch.float32, device=x_src.device)
+    B = gather_blocks(x_src) if (row_w is not None and csr.num_edges) else 1
+    if B > 1:
+        passes, _ = csr.blocks("fwd", B)
+        d, E = int(x_src.shape[1]), csr.num_edges
+        _gather_blocked(x_src, passes, row_w, None, out, False,
+                        f"gather_wfwd[{csr.n_dst}<-{csr.n_src}]x{d}",
+                        gather_bytes(E, csr.n_dst, d, False),
+                        gather_compulsory_bytes(E, csr.n_dst, csr.n_src, d, False))
+        return out
     _gather(x_src, csr.fwd, None, csr_mean=False, out=out, accumulate=False, edge_w=w_fwd,
             kind="wfwd")
     return out

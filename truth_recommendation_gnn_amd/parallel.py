@@ -406,6 +406,9 @@ class _Rel:
     csr: object
     w_fwd: Optional[torch.Tensor] = None
     w_bwd: Optional[torch.Tensor] = None
+    # user->post: the same 1/deg_global per destination row (w_fwd is it per position), for the
+    # source-blocked form of the partial-sum gather over a multi-GB user table
+    row_w: Optional[torch.Tensor] = None
     # user->post only, with ``UserShard(slice_inputs=True)``: every edge INTO the owned post slice
     # (global user ids).  Layer 1 reads the static input user table, which each rank can hold
     # whole: the slice's mean is then computed locally, with no partial sums to reduce-scatter.
@@ -525,7 +528,7 @@ class UserShard:
                 sl = torch.stack([src[ms], dst[ms] - self.p_lo]).contiguous()
                 slice_rel = impl.relation(sl, self.n_users, self.post_rows)
             return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv),
-                        slice_rel)
+                        inv, slice_rel)
         # post -> post: edges into the owned slice of the post table
         m = (dst >= self.p_lo) & (dst < self.p_hi)
         local = torch.stack([src[m], dst[m] - self.p_lo]).contiguous()
@@ -803,7 +806,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     # static inputs held whole: the owned slice's mean, no partial sums to reduce
                     rs[et] = (impl.gather_mean_raw(x_user_full, r.slice_csr), _Done())
                     continue
-                part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd)
+                part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd, r.row_w)
                 rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
                 rs_issued = True
         if ag is not None:                      # F3 the previous layer's post table
