@@ -79,6 +79,17 @@ int hgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, int64_t n_rows
                        int64_t n_cols, int32_t* t_rowptr, int32_t* t_col, int32_t* t_perm,
                        float* t_w, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* hgnn_csr_transpose for n_rel (<= 8) CSRs in one sort (the relations of one sampled block):
+ * relation r's CSR rowptr[r][n_rows[r]+1] / col[r][E[r]] with columns in [0, n_cols[r]); outputs
+ * per relation exactly as hgnn_csr_transpose's.  ws: hgnn_csr_transpose_multi_ws_bytes(sum of E,
+ * sum of n_cols). */
+size_t hgnn_csr_transpose_multi_ws_bytes(int64_t E_total, int64_t n_cols_total);
+int hgnn_csr_transpose_multi(int32_t n_rel, const int32_t* const* rowptr,
+                             const int32_t* const* col, const int64_t* n_rows, const int64_t* E,
+                             const int64_t* n_cols, int32_t* const* t_rowptr,
+                             int32_t* const* t_col, int32_t* const* t_perm, float* const* t_w,
+                             void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* The loss's negatives drawn and grouped in one call: exactly hgnn_uniform_i32(d_seed, E, n_keys,
  * neg_out) followed by hgnn_sort_pairs_i32(neg_out, a, NULL, E, n_keys, rowptr, a_sorted, NULL,
  * NULL, ...), with the draws computed inside the sort's first pass instead of being written and

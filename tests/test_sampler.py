@@ -319,3 +319,26 @@ def test_relabel_multi_equals_per_type_relabel():
         assert torch.equal(nodes[t][:counts[2 * i]], n1[:int(c1[0])]), t
         assert torch.equal(local[o:o + n_items[i]], l1), t
         o += n_items[i]
+
+
+def test_block_csc_group_equals_per_relation_transpose():
+    """The CSCs of a sampled block's relations built together (hgnn_csr_transpose_multi, one
+    sort) equal the per-relation hgnn_csr_transpose: rowptr, rows, positions and K2 weights —
+    including a relation with no edges."""
+    from truth_recommendation_gnn_amd import graph
+    rng = np.random.default_rng(11)
+    specs = [(300, 120, 4000), (50, 120, 0), (700, 80, 9000), (120, 300, 2500)]
+    rels_a, rels_b = [], []
+    for n_src, n_dst, E in specs:
+        ei = _rand_csr_graph(rng, n_src, n_dst, E).to(DEV) if E else \
+            torch.zeros(2, 0, dtype=torch.int64, device=DEV)
+        full = graph.RelationCSR(ei, n_src, n_dst)
+        for out in (rels_a, rels_b):
+            out.append(graph.RelationCSR.from_csr(full.fwd.rowptr, full.fwd.col, n_src, n_dst,
+                                                  may_have_heavy_rows=False))
+    graph.build_csc_group(rels_a)
+    for a, b in zip(rels_a, rels_b):
+        ga, gb = a.bwd, b.bwd                     # b: the one-relation transpose
+        assert torch.equal(ga.rowptr, gb.rowptr)
+        assert torch.equal(ga.col, gb.col) and torch.equal(ga.perm, gb.perm)
+        assert torch.equal(a.bwd_weights, b.bwd_weights)

@@ -76,6 +76,9 @@ _SIGS = {
                                   _p]),
     "hgnn_csr_transpose": (_c_i32, [_p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _c_sz,
                                     _p]),
+    "hgnn_csr_transpose_multi_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_csr_transpose_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _c_sz,
+                                          _p]),
     "hgnn_sample_neighbors": (_c_i32, [_p, _p, _c_i64, _p, _c_i64, _c_i32, ctypes.c_uint64, _p,
                                        _p, _p, _c_sz, _p]),
     "hgnn_relabel_ws_bytes": (_c_sz, [_c_i64, _c_i64]),

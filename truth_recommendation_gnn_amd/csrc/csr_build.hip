@@ -645,6 +645,134 @@ int hgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, int64_t n_rows
   return check_launch("k_transpose_finish");
 }
 
+}  // extern "C"
+
+namespace hgnn {
+// The CSCs of several destination-grouped CSRs in one sort: relation r's columns are keyed
+// col + cbase[r] and its positions numbered from ebase[r], so one stable sort over the combined
+// key range groups every relation's entries by (relation, column); each output then takes its
+// slice, zero-based.
+constexpr int kTransposeMax = 8;
+struct TransposeTab {
+  const int32_t* rowptr[kTransposeMax];
+  const int32_t* col[kTransposeMax];
+  int32_t* t_rowptr[kTransposeMax];
+  int32_t* t_col[kTransposeMax];
+  int32_t* t_perm[kTransposeMax];
+  float* t_w[kTransposeMax];
+  int64_t n_rows[kTransposeMax];
+  int64_t ebase[kTransposeMax + 1];   // position offsets
+  int64_t cbase[kTransposeMax + 1];   // key (column) offsets
+  int32_t n;
+};
+
+__device__ __forceinline__ int tt_find(const int64_t* off, int n, int64_t i) {
+  int r = 0;
+  while (r + 1 < n && i >= off[r + 1]) ++r;
+  return r;
+}
+
+__global__ void k_transpose_keys(const TransposeTab t, int32_t* keys) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.ebase[t.n]) return;
+  const int r = tt_find(t.ebase, t.n, i);
+  keys[i] = t.col[r][i - t.ebase[r]] + (int32_t)t.cbase[r];
+}
+
+// sorted entry i (global position p = perm_all[i]): relation r, its row (binary search in r's
+// rowptr), 1/deg of the row; written at i - (first sorted index of r)
+__global__ void k_transpose_finish_multi(const TransposeTab t, const int32_t* perm_all,
+                                         const int32_t* rowptr_all) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.ebase[t.n]) return;
+  const int64_t p = perm_all[i];
+  const int r = tt_find(t.ebase, t.n, p);
+  const int64_t pos = p - t.ebase[r];
+  const int32_t* rp = t.rowptr[r];
+  int64_t lo = 0, hi = t.n_rows[r];
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rp[mid] <= pos) lo = mid; else hi = mid;
+  }
+  const int64_t j = i - rowptr_all[t.cbase[r]];
+  t.t_col[r][j] = (int32_t)lo;
+  t.t_perm[r][j] = (int32_t)pos;
+  if (t.t_w[r]) t.t_w[r][j] = 1.f / (float)(rp[lo + 1] - rp[lo]);
+}
+
+__global__ void k_transpose_rowptr_split(const TransposeTab t, const int32_t* rowptr_all) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;   // entry j of relation r
+  if (g >= t.cbase[t.n] + t.n) return;                                // sits at cbase[r] + r + j
+  int r = 0;
+  while (r + 1 < t.n && g >= t.cbase[r + 1] + r + 1) ++r;
+  const int64_t j = g - t.cbase[r] - r;
+  t.t_rowptr[r][j] = rowptr_all[t.cbase[r] + j] - rowptr_all[t.cbase[r]];
+}
+}  // namespace hgnn
+
+extern "C" {
+
+size_t hgnn_csr_transpose_multi_ws_bytes(int64_t E_total, int64_t n_cols_total) {
+  const int64_t E = E_total < 1 ? 1 : E_total;
+  return sort_ws_bytes(E) + 2 * align_up((size_t)E * 4, 256) +
+         align_up((size_t)(n_cols_total + 1) * 4, 256) + 512;
+}
+
+int hgnn_csr_transpose_multi(int32_t n_rel, const int32_t* const* rowptr,
+                             const int32_t* const* col, const int64_t* n_rows, const int64_t* E,
+                             const int64_t* n_cols, int32_t* const* t_rowptr,
+                             int32_t* const* t_col, int32_t* const* t_perm, float* const* t_w,
+                             void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  hipStream_t stream = as_stream(stream_);
+  if (n_rel < 1 || n_rel > kTransposeMax || !rowptr || !col || !n_rows || !E || !n_cols ||
+      !t_rowptr || !t_col || !t_perm)
+    return fail(HGNN_E_ARG, "csr_transpose_multi: n_rel=%d (1..%d) or null array", n_rel,
+                kTransposeMax);
+  TransposeTab t{};
+  t.n = n_rel;
+  for (int r = 0; r < n_rel; ++r) {
+    if (E[r] < 0 || n_rows[r] < 0 || n_cols[r] < 0 || !t_rowptr[r] ||
+        (E[r] > 0 && (!rowptr[r] || !col[r] || !t_col[r] || !t_perm[r])))
+      return fail(HGNN_E_ARG, "csr_transpose_multi: relation %d", r);
+    t.rowptr[r] = rowptr[r]; t.col[r] = col[r]; t.n_rows[r] = n_rows[r];
+    t.t_rowptr[r] = t_rowptr[r]; t.t_col[r] = t_col[r]; t.t_perm[r] = t_perm[r];
+    t.t_w[r] = t_w ? t_w[r] : nullptr;
+    t.ebase[r + 1] = t.ebase[r] + E[r];
+    t.cbase[r + 1] = t.cbase[r] + n_cols[r];
+  }
+  const int64_t Et = t.ebase[n_rel], K = t.cbase[n_rel];
+  if (Et >= (int64_t(1) << 31) - 1 || K >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "csr_transpose_multi: E=%lld keys=%lld out of range",
+                (long long)Et, (long long)K);
+  if (ws_bytes < hgnn_csr_transpose_multi_ws_bytes(Et, K))
+    return fail(HGNN_E_WS, "csr_transpose_multi: workspace too small");
+  Workspace w(ws, ws_bytes);
+  int32_t* keys = w.take<int32_t>(Et < 1 ? 1 : Et);
+  int32_t* perm = w.take<int32_t>(Et < 1 ? 1 : Et);
+  int32_t* rp_all = w.take<int32_t>(K + 1);
+  if (Et > 0 && K > 0) {
+    hipLaunchKernelGGL(k_transpose_keys, dim3(cdiv(Et, 256)), dim3(256), 0, stream, t, keys);
+    if (int rc = check_launch("k_transpose_keys")) return rc;
+    int32_t* ka = w.take<int32_t>(Et);
+    const int32_t* sk = nullptr;
+    if (int rc = radix_sort_pairs(keys, ka, Et, K, nullptr, nullptr, perm, nullptr, w, stream,
+                                  &sk))
+      return rc;
+    hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(K + 1, 256)), dim3(256), 0, stream, sk,
+                       Et, K, rp_all);
+    if (int rc = check_launch("k_rowptr_from_sorted")) return rc;
+    hipLaunchKernelGGL(k_transpose_finish_multi, dim3(cdiv(Et, 256)), dim3(256), 0, stream, t,
+                       perm, rp_all);
+    if (int rc = check_launch("k_transpose_finish_multi")) return rc;
+  } else {
+    hipLaunchKernelGGL(k_fill_i32, dim3(cdiv(K + 1, 256)), dim3(256), 0, stream, rp_all, K + 1,
+                       0);
+  }
+  hipLaunchKernelGGL(k_transpose_rowptr_split, dim3(cdiv(K + n_rel, 256)), dim3(256), 0, stream,
+                     t, rp_all);
+  return check_launch("k_transpose_rowptr_split");
+}
+
 int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E, int64_t n_keys,
                              int32_t* neg_out, int32_t* rowptr, int32_t* a_sorted, void* ws,
                              size_t ws_bytes, hgnn_stream_t stream_) {

@@ -258,6 +258,12 @@ class RelationCSR:
         the per-position 1/deg that K2 streams (``bwd_weights``).  No skew plan (it needs a host
         sync to size): a source row is summed by one wave however long it is — a hot post drawn
         by many sampled edges included (at cfg5, 700+ of one block's 15k rev_engages edges)."""
+        group = getattr(self, "_csc_group", None)     # weak references to the block's relations
+        if group is not None:
+            members = [m for m in (ref() for ref in group) if m is not None]
+            if any(m is self for m in members):
+                build_csc_group(members)     # every relation of the block in one sort
+                return self._bwd
         g, E = self.fwd, self.num_edges
         dev = g.col.device
         rowptr = torch.empty(self.n_src + 1, dtype=torch.int32, device=dev)
@@ -320,6 +326,39 @@ class RelationCSR:
         """Drop the COO reference once the CSC exists (saves 16 B/edge of HBM)."""
         if self._bwd is not None:
             self._ei = None
+
+
+def build_csc_group(rels) -> None:
+    """The CSCs (and K2 weights) of several ``RelationCSR.from_csr`` relations — one sampled
+    block's — in one sort (``hgnn_csr_transpose_multi``), cached on each relation.  A block's
+    backward needs all of them, so the first relation asked builds the group."""
+    rels = [r for r in rels if r._bwd is None]
+    if not rels:
+        return
+    dev = rels[0].fwd.col.device
+    outs = []
+    for r in rels:
+        E = r.num_edges
+        outs.append((torch.empty(r.n_src + 1, dtype=torch.int32, device=dev),
+                     torch.empty(max(E, 1), dtype=torch.int32, device=dev),
+                     torch.empty(max(E, 1), dtype=torch.int32, device=dev),
+                     torch.empty(max(E, 1), dtype=torch.float32, device=dev)))
+    lib = N.lib()
+    Es = [r.num_edges for r in rels]
+    ws = N.workspace(lib.hgnn_csr_transpose_multi_ws_bytes(sum(Es), sum(r.n_src for r in rels)),
+                     dev)
+    N.check(lib.hgnn_csr_transpose_multi(
+        len(rels), N.ptr_array([r.fwd.rowptr for r in rels]),
+        N.ptr_array([r.fwd.col if r.num_edges else o[1] for r, o in zip(rels, outs)]),
+        N.i64_array([r.n_dst for r in rels]), N.i64_array(Es),
+        N.i64_array([r.n_src for r in rels]), N.ptr_array([o[0] for o in outs]),
+        N.ptr_array([o[1] for o in outs]), N.ptr_array([o[2] for o in outs]),
+        N.ptr_array([o[3] for o in outs]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+        "hgnn_csr_transpose_multi")
+    for r, (rp, col, perm, w) in zip(rels, outs):
+        E = r.num_edges
+        r._bwd = GroupedEdges(rp, col[:E], perm[:E], Plan(NO_SPLIT, 0, 0, None, None), r.n_src)
+        r._bwd_w = w[:E]
 
 
 class _CsrCache:

@@ -20,6 +20,7 @@ With fanouts at least the maximum degree, the seeds' embeddings equal the full-g
 from __future__ import annotations
 
 import dataclasses
+import weakref
 from typing import Dict, List, Mapping, Sequence, Tuple
 
 import torch
@@ -218,6 +219,9 @@ class NeighborSampler:
                                              int(cur[et[2]].numel()),
                                              may_have_heavy_rows=fanout < 0)
                     for et in ets}
+            group = [weakref.ref(c) for c in csrs.values()]   # the block's backward CSCs:
+            for c in csrs.values():                           # one sort for all of them
+                c._csc_group = group
             blocks.append(Block(csrs, {t: int(v.numel()) for t, v in cur.items()},
                                 {t: int(v.numel()) for t, v in nxt.items()}))
             nodes.append(nxt)
