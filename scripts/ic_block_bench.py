@@ -2,7 +2,9 @@
 4.6 GB) as one pass vs B x D passes: pass (d, b) sums, for the destination rows of group d (D
 contiguous ranges of posts), only the sources in user block b (a 4.6/B GB slice), accumulating
 into the output.  D > 1 keeps each group's accumulator (512/D MB) cache-resident across its B
-passes.  Prints ms per full gather.  usage: python scripts/ic_block_bench.py [B:D ...]"""
+passes.  IC_REV=1: the user <- post relation (the 512 MB post table) instead.  Prints ms per
+full gather.  usage: [IC_REV=1] python scripts/ic_block_bench.py [B:D ...]"""
+import os
 import sys
 import time
 
@@ -32,9 +34,12 @@ def main():
     cfg = synth.CONFIGS["cfg4"]
     t0 = time.time()
     g = synth.make_graph(cfg, device=dev, device_gen=True)
-    ei = g.edge_index_dict[synth.ENGAGES]            # user -> post
+    rev = os.environ.get("IC_REV", "0") == "1"       # the user <- post relation instead
+    ei = g.edge_index_dict[synth.REV_ENGAGES if rev else synth.ENGAGES]
     n_u, n_p = cfg.num_users, cfg.num_posts
-    x = g.x_dict["user"]
+    x = g.x_dict["post" if rev else "user"]
+    if rev:                                           # sources: posts, destinations: users
+        n_u, n_p = n_p, n_u
     del g
     print(f"graph {time.time() - t0:.1f}s E={ei.shape[1]}", flush=True)
     csr = graph.relation_csr(ei, n_u, n_p)
