@@ -5,7 +5,9 @@ tensors; RCCL needs one GPU per rank).  Reference: the single-process path on th
 parameters and negatives (``HeteroSAGE`` + ``ops.edge_bce_loss`` + ``backward()``), itself checked
 against float64 at this size by ``tests/test_full_size.py``.  The loss must agree to 1e-5 and
 every parameter gradient to rtol 1e-4 (atol 1e-5 x its max).  World 3 pads the post table (100k
-rows over 3 slices) and puts the slice pre-projection on uneven slices."""
+rows over 3 slices) and puts the slice pre-projection on uneven slices.  The cfg4 case runs the
+north-star graph (9M users, 1M posts, 200M engages + reverse) at world 2, where the per-rank gathers
+over tables above 2 GB take the source-blocked path (``ops.gather_blocks``)."""
 import os
 import socket
 
@@ -23,10 +25,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _setup():
+def _setup(name="cfg2"):
     from truth_recommendation_gnn_amd import HeteroSAGE, synth
     dev = torch.device("cuda:0")
-    cfg = synth.CONFIGS["cfg2"]
+    cfg = synth.CONFIGS[name]
     g = synth.make_graph(cfg, device=dev)
     rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
     torch.manual_seed(synth.WEIGHT_SEED)
@@ -37,12 +39,12 @@ def _setup():
     return cfg, g, model, pos, neg, pw
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, name="cfg2"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from truth_recommendation_gnn_amd import ops, parallel, synth
-        cfg, g, model, pos, neg, pw = _setup()
+        cfg, g, model, pos, neg, pw = _setup(name)
         if rank == 0:        # the single-process reference step on the same inputs
             out = model(g.x_dict, g.edge_index_dict)
             loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw)
@@ -76,12 +78,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_step_at_cfg2_size_matches_single_process(world):
+@pytest.mark.parametrize("world,name", [(2, "cfg2"), (3, "cfg2"), (2, "cfg4")])
+def test_sharded_step_at_full_size_matches_single_process(world, name):
+    """(the cfg4 case: the north-star graph on 2 ranks — each rank's own-user table is 2.3 GB,
+    so its post partial sums and the layer-1 slice mean over the whole 4.6 GB input table run
+    as source-block passes)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, name)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=600) for _ in procs]
