@@ -580,7 +580,8 @@ def test_sample_negatives_uniform_and_seeded():
 
 @pytest.mark.parametrize("E,n_keys", [(0, 7), (1, 1), (1000, 1), (5000, 37),
                                       (300_000, 100_000), (2_000_000, 1_000_000),
-                                      (1_000_003, 2**21 + 5)])
+                                      (1_000_003, 2**21 + 5),
+                                      (70_000_001, 1_000_000)])   # > 2^26 draws, ragged last tile
 def test_draw_sort_negatives_is_draw_then_sort(E, n_keys):
     """hgnn_draw_sort_negatives (draws computed inside the sort's first pass) is bit for bit
     hgnn_uniform_i32 followed by hgnn_sort_pairs_i32, and a stable sort (numpy) of the draws."""
@@ -668,6 +669,7 @@ def test_weighted_rgcn_fused_loss_step_matches_golden():
                                   (8192, 1000),          # exactly one onesweep tile
                                   (8193, 100),           # one item in a second tile
                                   (2_500_001, 100_000),  # 306 tiles of look-back, ragged tail
+                                  (2**26 + 3, 1_000_000),  # > 2^26 keys, two payloads
                                   (40000, -1)])          # every key equal: one digit holds all
 def test_sort_pairs_matches_numpy(E, nk):
     rng = np.random.default_rng(9 + abs(nk))
