@@ -14,6 +14,10 @@
 // partial sums go to a slab, then k_fixup adds them in chunk order.
 #include "hgnn_common.h"
 
+#ifndef HGNN_NT_GATHER
+#define HGNN_NT_GATHER 0   // 1: nt loads in every gather (measurement builds only)
+#endif
+
 #include <stdlib.h>
 
 namespace hgnn {
@@ -84,7 +88,13 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, const int32_t* 
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
           const int c = (q * LPR + sl) * W;
-          v[u][q] = (e < n && c < d) ? V::load(xr + c) : V::zero();
+          // the dP score gather streams its rows with nt loads (cfg4: 33.1 -> 32.1 ms); the mean
+          // gathers keep the default policy (nt costs them 25-45 %: the source-block passes and
+          // the Zipf-hot post rows live on cache reuse)
+          if constexpr (SC || HGNN_NT_GATHER)
+            v[u][q] = (e < n && c < d) ? V::load_nt(xr + c) : V::zero();
+          else
+            v[u][q] = (e < n && c < d) ? V::load(xr + c) : V::zero();
         }
       }
       if constexpr (SC) {

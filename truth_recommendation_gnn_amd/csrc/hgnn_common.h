@@ -61,6 +61,12 @@ struct Vec<4> {
   static __device__ __forceinline__ T load(const float* p) {
     return *reinterpret_cast<const float4*>(p);
   }
+  // streaming (nt) load: for rows gathered once per edge
+  static __device__ __forceinline__ T load_nt(const float* p) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
   static __device__ __forceinline__ void store(float* p, T v) {
     *reinterpret_cast<float4*>(p) = v;
   }
@@ -87,6 +93,7 @@ struct Vec<1> {
   using T = float;
   static __device__ __forceinline__ T zero() { return 0.f; }
   static __device__ __forceinline__ T load(const float* p) { return *p; }
+  static __device__ __forceinline__ T load_nt(const float* p) { return __builtin_nontemporal_load(p); }
   static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
   static __device__ __forceinline__ void fma(T& a, float w, T v) { a = fmaf(w, v, a); }
   static __device__ __forceinline__ void add(T& a, T v) { a += v; }
