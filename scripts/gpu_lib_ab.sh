@@ -15,7 +15,7 @@ import json, sys
 d = json.load(open(sys.argv[1]))
 k = d["kernels"]
 print(sys.argv[2], d["ms_per_step"], {n: v["ms_per_step"] for n, v in k.items()
-                                      if n.startswith(("gather", "score"))})
+                                      if n.startswith(("gather", "score", "edge"))})
 PY
   done
 done
