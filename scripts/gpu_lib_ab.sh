@@ -11,11 +11,11 @@ for rep in 1 2; do
     HGNN_LIB=$lib timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
       --json-out gpurun_out/ab_${i}_${lib%.so}.json > gpurun_out/ab_${i}.log 2>&1 || exit $?
     python - gpurun_out/ab_${i}_${lib%.so}.json "$lib" <<'PY'
-import json, sys
+import json, os, sys
 d = json.load(open(sys.argv[1]))
 k = d["kernels"]
 print(sys.argv[2], d["ms_per_step"], {n: v["ms_per_step"] for n, v in k.items()
-                                      if n.startswith(("gather", "score", "edge"))})
+                                      if n.startswith(tuple(os.environ.get("AB_KERNELS", "gather,score,edge").split(",")))})
 PY
   done
 done

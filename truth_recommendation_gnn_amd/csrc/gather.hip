@@ -14,6 +14,11 @@
 // partial sums go to a slab, then k_fixup adds them in chunk order.
 #include "hgnn_common.h"
 
+#ifndef HGNN_NT_STORE
+// output rows are stored with the nt policy: the next reader is another kernel, long after the
+// row has left L2 (cfg4 step 168.1 -> 167.5 ms with the dU stores below, mostly the dP gather)
+#define HGNN_NT_STORE 1
+#endif
 #ifndef HGNN_NT_GATHER
 #define HGNN_NT_GATHER 0   // 1: nt loads in every gather (measurement builds only)
 #endif
@@ -194,7 +199,11 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
         V::scale(r, s);
         if (a.accumulate) V::add(r, V::load(dst + c));
       }
+#if HGNN_NT_STORE
+      V::store_nt(dst + c, r);
+#else
       V::store(dst + c, r);
+#endif
     }
   }
 }

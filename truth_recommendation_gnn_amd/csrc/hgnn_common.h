@@ -70,6 +70,10 @@ struct Vec<4> {
   static __device__ __forceinline__ void store(float* p, T v) {
     *reinterpret_cast<float4*>(p) = v;
   }
+  static __device__ __forceinline__ void store_nt(float* p, T v) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w}, reinterpret_cast<f4*>(p));
+  }
   static __device__ __forceinline__ void fma(T& a, float w, T v) {
     a.x = fmaf(w, v.x, a.x); a.y = fmaf(w, v.y, a.y);
     a.z = fmaf(w, v.z, a.z); a.w = fmaf(w, v.w, a.w);
@@ -95,6 +99,7 @@ struct Vec<1> {
   static __device__ __forceinline__ T load(const float* p) { return *p; }
   static __device__ __forceinline__ T load_nt(const float* p) { return __builtin_nontemporal_load(p); }
   static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
+  static __device__ __forceinline__ void store_nt(float* p, T v) { __builtin_nontemporal_store(v, p); }
   static __device__ __forceinline__ void fma(T& a, float w, T v) { a = fmaf(w, v, a); }
   static __device__ __forceinline__ void add(T& a, T v) { a += v; }
   static __device__ __forceinline__ float dot(T a, T b) { return a * b; }

@@ -19,6 +19,9 @@
 // Post rows of the negatives (uniform draws, little reuse) are read with nt loads: cfg4 scoring
 // pass 26.4 -> 25.8 ms.  The positives' rows keep the default policy: their Zipf-hot posts live on
 // cache reuse (nt on both: 33.1 ms).  Measurement builds: 0 = none, 2 = both.
+#ifndef HGNN_NT_STORE
+#define HGNN_NT_STORE 1   // dU rows stored with the nt policy (see gather.hip)
+#endif
 #ifndef HGNN_NT_SCORE
 #define HGNN_NT_SCORE 1
 #endif
@@ -178,7 +181,11 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
 #pragma unroll
       for (int q = 0; q < VPL; ++q) {
         const int cc = (q * LPR + sl) * W;
+#if HGNN_NT_STORE
+        if (cc < d) V::store_nt(a.dU + u * d + cc, acc[q]);
+#else
         if (cc < d) V::store(a.dU + u * d + cc, acc[q]);
+#endif
       }
     }
   }
