@@ -14,15 +14,8 @@
 // partial sums go to a slab, then k_fixup adds them in chunk order.
 #include "hgnn_common.h"
 
-#ifndef HGNN_NT_STORE
-// output rows are stored with the nt policy: the next reader is another kernel, long after the
-// row has left L2 (cfg4 step 168.1 -> 167.5 ms with the dU stores below, mostly the dP gather)
-#define HGNN_NT_STORE 1
-#endif
-#ifndef HGNN_NT_GATHER
-#define HGNN_NT_GATHER 0   // 1: nt loads in every gather (measurement builds only)
-#endif
-
+// Cache policy of the gathered rows and the output rows (set per launch from the table sizes,
+// `nt_policy` below): nt loads / stores when the table is far larger than the caches.
 #include <stdlib.h>
 
 namespace hgnn {
@@ -53,6 +46,8 @@ struct GatherArgs {
   // hgnn_score_gather2: a second grouped list (the negatives, mode 2, no heavy-row plan) summed
   // into the same rows in the same pass; null otherwise
   const int32_t* rowptr2;
+  int32_t nt_load;             // rows gathered with nt loads (score gathers over multi-GB tables)
+  int32_t nt_store;            // output rows stored with nt stores
   const int32_t* col2;
 };
 
@@ -93,10 +88,11 @@ __device__ __forceinline__ void segment_sum(const GatherArgs& a, const int32_t* 
 #pragma unroll
         for (int q = 0; q < VPL; ++q) {
           const int c = (q * LPR + sl) * W;
-          // the dP score gather streams its rows with nt loads (cfg4: 33.1 -> 32.1 ms); the mean
-          // gathers keep the default policy (nt costs them 25-45 %: the source-block passes and
-          // the Zipf-hot post rows live on cache reuse)
-          if constexpr (SC || HGNN_NT_GATHER)
+          // the dP score gather over a multi-GB user table streams its rows with nt loads (cfg4:
+          // 32.4 -> 31.0 ms; on a table the Infinity Cache half holds, cfg3, 2.80 -> 3.42 ms, so
+          // only above 1 GiB); the mean gathers keep the default policy (nt costs them 25-45 %:
+          // the source-block passes and the Zipf-hot post rows live on cache reuse)
+          if (SC && a.nt_load)
             v[u][q] = (e < n && c < d) ? V::load_nt(xr + c) : V::zero();
           else
             v[u][q] = (e < n && c < d) ? V::load(xr + c) : V::zero();
@@ -199,11 +195,8 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
         V::scale(r, s);
         if (a.accumulate) V::add(r, V::load(dst + c));
       }
-#if HGNN_NT_STORE
-      V::store_nt(dst + c, r);
-#else
-      V::store(dst + c, r);
-#endif
+      if (a.nt_store) V::store_nt(dst + c, r);
+      else V::store(dst + c, r);
     }
   }
 }
@@ -310,6 +303,15 @@ static int dispatch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) 
   return fail(HGNN_E_UNSUPPORTED, "gather: d=%d > 1024", d);
 }
 
+// nt above 1 GiB: cfg4's 4.6 GB user table and its 4.6 GB user-side outputs.  Output rows of
+// the dP gather / K2s / means are read by another kernel long after they left L2 (cfg4 step
+// 168.1 -> 167.5 ms with nt stores, mostly the dP gather); cfg2/cfg3 tables stay cache-resident.
+constexpr int64_t kNtBytes = int64_t(1) << 30;
+static void nt_policy(GatherArgs& a, int64_t n_x) {
+  a.nt_load = a.score && n_x * a.d * 4 >= kNtBytes ? 1 : 0;
+  a.nt_store = (a.score ? a.nt_load : a.n_rows * a.d * 4 >= kNtBytes) ? 1 : 0;
+}
+
 static int run_gather(GatherArgs a, hipStream_t stream) {
   if (a.d <= 0 || a.n_rows < 0 || a.n_heavy < 0 || a.chunk <= 0)
     return fail(HGNN_E_ARG, "gather: bad sizes d=%d n_rows=%lld chunk=%d", a.d,
@@ -345,13 +347,13 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
                        const float* col_w, int32_t flags, const int32_t* heavy_rows,
                        const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
                        int32_t chunk, float* slab, float* out, hgnn_stream_t stream) {
-  (void)n_x;
   GatherArgs a{};
   a.x = x; a.rowptr = rowptr; a.col = col; a.edge_w = edge_w; a.col_w = col_w;
   a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
   a.d = d; a.chunk = chunk; a.mean = (flags & HGNN_MEAN) ? 1 : 0;
   a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+  nt_policy(a, n_x);
   return run_gather(a, as_stream(stream));
 }
 
@@ -361,7 +363,6 @@ int hgnn_gather_reduce_scaled(const float* x, int64_t n_x, int32_t d, const int3
                               const int32_t* heavy_rows, const int32_t* heavy_first,
                               int64_t n_heavy, int64_t n_chunks, int32_t chunk, float* slab,
                               float* out, hgnn_stream_t stream) {
-  (void)n_x;
   if (row_w && (flags & HGNN_MEAN))
     return fail(HGNN_E_ARG, "gather_reduce_scaled: row_w replaces HGNN_MEAN, not both");
   GatherArgs a{};
@@ -370,6 +371,7 @@ int hgnn_gather_reduce_scaled(const float* x, int64_t n_x, int32_t d, const int3
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
   a.d = d; a.chunk = chunk; a.mean = 0;
   a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+  nt_policy(a, n_x);
   return run_gather(a, as_stream(stream));
 }
 
@@ -399,7 +401,6 @@ int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t 
                       const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
                       int32_t chunk, float* slab, float* out, int32_t accumulate,
                       hgnn_stream_t stream) {
-  (void)n_x;
   if (mode != 1 && mode != 2) return fail(HGNN_E_ARG, "score_gather: mode=%d", mode);
   GatherArgs a{};
   a.x = x; a.rowptr = rowptr; a.col = col;
@@ -407,6 +408,7 @@ int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t 
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
   a.d = d; a.chunk = chunk; a.accumulate = accumulate ? 1 : 0;
   a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = mode;
+  nt_policy(a, n_x);
   return run_gather(a, as_stream(stream));
 }
 
@@ -416,7 +418,6 @@ int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t
                        const int32_t* heavy_rows, const int32_t* heavy_first, int64_t n_heavy,
                        int64_t n_chunks, int32_t chunk, float* slab, float* out,
                        hgnn_stream_t stream) {
-  (void)n_x;
   if (!rowptr_n && n_rows > 0) return fail(HGNN_E_ARG, "score_gather2: rowptr_n is null");
   GatherArgs a{};
   a.x = x; a.rowptr = rowptr; a.col = col;
@@ -425,6 +426,7 @@ int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t
   a.d = d; a.chunk = chunk; a.accumulate = 0;
   a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = 1;
   a.rowptr2 = rowptr_n; a.col2 = col_n;
+  nt_policy(a, n_x);
   return run_gather(a, as_stream(stream));
 }
 

@@ -19,12 +19,11 @@
 // Post rows of the negatives (uniform draws, little reuse) are read with nt loads: cfg4 scoring
 // pass 26.4 -> 25.8 ms.  The positives' rows keep the default policy: their Zipf-hot posts live on
 // cache reuse (nt on both: 33.1 ms).  Measurement builds: 0 = none, 2 = both.
-#ifndef HGNN_NT_STORE
-#define HGNN_NT_STORE 1   // dU rows stored with the nt policy (see gather.hip)
-#endif
-#ifndef HGNN_NT_SCORE
-#define HGNN_NT_SCORE 1
-#endif
+// Cache policy (per launch, from the table sizes): the negatives' post rows (uniform draws,
+// little reuse) are read with nt loads when the post table outgrows the Infinity Cache (cfg4,
+// 488 MiB: 26.4 -> 25.8 ms; the positives' Zipf-hot rows keep the default policy: nt on both
+// measured 33.1 ms); the dU rows are then stored nt too.  Its own instantiation, so the
+// default-policy kernel (cfg2/cfg3) is the same code as before.
 
 
 namespace hgnn {
@@ -49,6 +48,7 @@ struct ScoreArgs {
   int64_t n_posts;
   float inv_e;
   int32_t d;
+  int32_t nt_neg;              // nt policy: negatives' post rows loaded, dU rows stored
 };
 
 template <int LPR, int VPL, int W>
@@ -67,7 +67,7 @@ __device__ __forceinline__ float slot_dot(const typename Vec<W>::T (&a)[VPL],
   return slot_sum<LPR>(s);
 }
 
-template <int LPR, int VPL, int W>
+template <int LPR, int VPL, int W, bool NT = false>
 __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   using V = Vec<W>;
   constexpr int NS = 64 / LPR;
@@ -116,16 +116,9 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         for (int q = 0; q < VPL; ++q) {
           const int cc = (q * LPR + sl) * W;
           const int ccl = cc < d ? cc : 0;
-#if HGNN_NT_SCORE >= 2
-          xp[q] = V::load_nt(a.P + (int64_t)pp * d + ccl);
-#else
           xp[q] = V::load(a.P + (int64_t)pp * d + ccl);
-#endif
-#if HGNN_NT_SCORE >= 1
-          xn[q] = V::load_nt(a.P + (int64_t)qq * d + ccl);
-#else
-          xn[q] = V::load(a.P + (int64_t)qq * d + ccl);
-#endif
+          if constexpr (NT) xn[q] = V::load_nt(a.P + (int64_t)qq * d + ccl);
+          else xn[q] = V::load(a.P + (int64_t)qq * d + ccl);
         }
       };
       auto score_step = [&](int j, const typename V::T (&vp)[VPL],
@@ -181,11 +174,10 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
 #pragma unroll
       for (int q = 0; q < VPL; ++q) {
         const int cc = (q * LPR + sl) * W;
-#if HGNN_NT_STORE
-        if (cc < d) V::store_nt(a.dU + u * d + cc, acc[q]);
-#else
-        if (cc < d) V::store(a.dU + u * d + cc, acc[q]);
-#endif
+        if (cc < d) {
+          if constexpr (NT) V::store_nt(a.dU + u * d + cc, acc[q]);
+          else V::store(a.dU + u * d + cc, acc[q]);
+        }
       }
     }
   }
@@ -249,7 +241,11 @@ __global__ void k_loss_final(const double* red, const float* cscale, float inv_e
 
 template <int LPR, int VPL, int W>
 static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream) {
-  hipLaunchKernelGGL((k_edge_score<LPR, VPL, W>), dim3((unsigned)nblocks), dim3(256), 0,
+  if (a.nt_neg)   // the cache policy as its own instantiation: the default one is unchanged
+    hipLaunchKernelGGL((k_edge_score<LPR, VPL, W, true>), dim3((unsigned)nblocks), dim3(256), 0,
+                       stream, a);
+  else
+    hipLaunchKernelGGL((k_edge_score<LPR, VPL, W>), dim3((unsigned)nblocks), dim3(256), 0,
                      stream, a);
   return check_launch("k_edge_score");
 }
@@ -285,6 +281,7 @@ static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_u
   a.to_post_pos = to_post_pos; a.cscale = cscale; a.dU = dU; a.hpos = hpos; a.neg_key = neg_key;
   a.neg_u = neg_user; a.neg_w = neg_w; a.part = part; a.err = err; a.n_users = n_users;
   a.n_posts = n_posts; a.inv_e = n_edges > 0 ? 1.f / (float)n_edges : 0.f; a.d = d;
+  a.nt_neg = n_posts * d * 4 >= (int64_t(256) << 20) ? 1 : 0;
   const int64_t nb = cdiv(n_users, 4);   // blocks of 4 user-waves
   int rc = HGNN_OK;
   if (nb > 0) {
