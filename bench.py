@@ -471,7 +471,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                    "edges_per_step": edges_step, "global_batch": edges_step,
                    "parallelism": (f"dst-partitioned x{world} (user shards + post-table slices: "
                                    "RCCL reduce-scatter / all-gather per layer)"
-                                   if sharded and world > 1 else "single")},
+                                   if sharded else "single")},
         "roofline": roof, "projection": proj, "cpu_baseline": cpu,
         "kernel_timer": {"steps": args.timer_steps if kern else 0,
                          "ms_per_step": round(timer_ms, 3) if timer_ms else None,
