@@ -343,7 +343,8 @@ int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, 
                  int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
                  size_t ws_bytes, hgnn_stream_t stream);
 /* hgnn_relabel that also checks the prefix (a mini-batch's seeds): d_count2[0] = the count,
- * d_count2[1] = flags, bit 0 a repeated prefix id, bit 1 a prefix id outside [0, id_limit).
+ * d_count2[1] = flags, bit 0 a repeated prefix id, bit 1 a prefix id outside [0, id_limit)
+ * (id_limit 0: a type with no nodes, every id flagged; id_limit < 0: no range check).
  * The outputs are unspecified when a flag is set; nothing is read out of bounds. */
 int hgnn_relabel_checked(const int32_t* prefix, int64_t n_prefix, int64_t id_limit,
                          const int32_t* items, int64_t n_items, int32_t* local_out,

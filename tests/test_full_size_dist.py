@@ -1,10 +1,12 @@
 """The sharded training step (``parallel.UserShard.step``, the bench's N > 1 path) at BASELINE
 cfg2 size — 1M users, 100k posts, 20M engages + reverse, Zipf post degrees up to ~440k, so every
 rank's relations carry skew plans — on the HIP kernels, world 2 and 3 on one GPU (gloo over device
-tensors; RCCL needs one GPU per rank).  Reference: the single-process path on the same graph,
-parameters and negatives (``HeteroSAGE`` + ``ops.edge_bce_loss`` + ``backward()``), itself checked
-against float64 at this size by ``tests/test_full_size.py``.  The loss must agree to 1e-5 and
-every parameter gradient to rtol 1e-4 (atol 1e-5 x its max).  World 3 pads the post table (100k
+tensors; RCCL needs one GPU per rank).  Reference: the float64 step of ``tests/f64_step.py`` (plain
+torch on the GPU, no hgnn call) on the same graph, parameters and negatives, computed by rank 0
+before the sharded step, with the ReLU masks of an fp32 forward (see tests/test_full_step_f64.py,
+which checks the single-process step against the same reference, forward outputs included).  The
+loss and every parameter gradient must agree at the north_star's rtol 1e-4 (gradients read
+against each parameter's largest entry).  World 3 pads the post table (100k
 rows over 3 slices) and puts the slice pre-projection on uneven slices.  The cfg4 case runs the
 north-star graph (9M users, 1M posts, 200M engages + reverse) at world 2, where the per-rank gathers
 over tables above 2 GB take the source-blocked path (``ops.gather_blocks``)."""
@@ -43,16 +45,29 @@ def _worker(rank, world, port, q, name="cfg2"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from truth_recommendation_gnn_amd import ops, parallel, synth
+        from truth_recommendation_gnn_amd import parallel
         cfg, g, model, pos, neg, pw = _setup(name)
-        if rank == 0:        # the single-process reference step on the same inputs
-            out = model(g.x_dict, g.edge_index_dict)
-            loss = ops.edge_bce_loss(out["user"], out["post"], pos, neg, pw)
-            loss.backward()
-            ref = (float(loss), {n: p.grad.detach().clone() for n, p in model.named_parameters()})
-            del out, loss
-            for p in model.parameters():
-                p.grad = None
+        if rank == 0:        # the float64 reference step on the same inputs (independent code)
+            from f64_step import train_step_f64
+            from truth_recommendation_gnn_amd import HeteroSAGE, graph, synth
+            rels = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
+            params = {n: p.detach().clone() for n, p in model.named_parameters()}
+            # ReLU masks from an fp32 forward (as test_full_step_f64.py; an element within fp32
+            # rounding of 0 has no defined side), the single-process forward's layer by layer
+            h, masks = dict(g.x_dict), []
+            for li, layer in enumerate(model.layers):
+                m = HeteroSAGE(cfg.hidden, rels, num_layers=1,
+                               in_channels=cfg.dim if li == 0 else cfg.hidden).to(h["user"].device)
+                m.layers[0] = layer
+                h = m(h, g.edge_index_dict)
+                masks.append({t: h[t].detach() > 0 for t in ("user", "post")})
+            del h, m
+            graph.CSR_CACHE.clear()
+            torch.cuda.empty_cache()
+            ref = train_step_f64(params, g.x_dict["user"], g.x_dict["post"], pos, neg,
+                                 pw.double().mean(), masks=masks)
+            del params, masks
+            torch.cuda.empty_cache()
         env = parallel.DistEnv.from_torch()
         shard = parallel.UserShard(pos, cfg.num_users, cfg.num_posts, env, pos_weights=pw,
                                    slice_inputs=True)
@@ -64,9 +79,8 @@ def _worker(rank, world, port, q, name="cfg2"):
         torch.cuda.synchronize()
         if rank == 0:
             r_loss, r_grads = ref
-            errs = {n: float((p.grad - r_grads[n]).abs().max())
-                    / max(float(r_grads[n].abs().max()), 1e-12)
-                    for n, p in model.named_parameters()}
+            from f64_step import max_rel_err
+            errs = {n: max_rel_err(p.grad, r_grads[n]) for n, p in model.named_parameters()}
             q.put({"loss_err": abs(total - r_loss) / abs(r_loss), "grad_err": errs,
                    "pre_layers": shard.pre_layers})
         else:
@@ -79,7 +93,7 @@ def _worker(rank, world, port, q, name="cfg2"):
 
 
 @pytest.mark.parametrize("world,name", [(2, "cfg2"), (3, "cfg2"), (2, "cfg4")])
-def test_sharded_step_at_full_size_matches_single_process(world, name):
+def test_sharded_step_at_full_size_matches_float64(world, name):
     """(the cfg4 case: the north-star graph on 2 ranks — each rank's own-user table is 2.3 GB,
     so its post partial sums and the layer-1 slice mean over the whole 4.6 GB input table run
     as source-block passes)"""
@@ -96,7 +110,6 @@ def test_sharded_step_at_full_size_matches_single_process(world, name):
     assert not errs, errs
     r0 = next(r for r in res if "loss_err" in r)
     assert r0["pre_layers"] == [1]
-    assert r0["loss_err"] < 1e-5, r0
-    # gradients are sums over 20M edges in a different order (per-rank partial sums): the bar is
-    # the north_star's rtol 1e-4 relative to each parameter's largest entry
+    assert r0["loss_err"] < 1e-4, r0
+    # the north_star's rtol 1e-4, relative to each parameter's largest entry
     assert max(r0["grad_err"].values()) < 1e-4, r0

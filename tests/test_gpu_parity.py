@@ -418,9 +418,10 @@ def test_hetero_sage_two_layer_fused_loss_matches_golden(fixture, d):
         close(p.grad, z["grad:" + name])
 
 
-def test_fused_loss_refuses_second_backward():
-    """dU/dP are scaled in place by the upstream gradient, so a retained graph must not be
-    back-propagated twice (it would scale them twice)."""
+def test_fused_loss_second_backward_through_retained_graph():
+    """A retained graph back-propagated twice gives the same gradients both times (the second
+    backward recomputes dU/dP; the first handed its buffers on, scaled in place), as the torch
+    loss does: the leaves accumulate g1 + g2."""
     z = np.load(GOLD / "cfg2_slice_hetero_sage.npz")
     ei = torch.from_numpy(z["ei_engages"]).to(DEV)
     U = torch.from_numpy(z["out_user"]).to(DEV).requires_grad_()
@@ -428,15 +429,20 @@ def test_fused_loss_refuses_second_backward():
     loss = ops.edge_bce_loss(U, P, ei, torch.from_numpy(z["neg_p"]).to(DEV),
                              torch.from_numpy(z["pos_weights"]).to(DEV))
     (2.0 * loss).backward(retain_graph=True)
-    g1 = U.grad.clone()
-    with pytest.raises(RuntimeError, match="backward ran twice"):
-        loss.backward()
+    g1u, g1p = U.grad.clone(), P.grad.clone()
+    loss.backward(retain_graph=True)
+    g2u, g2p = U.grad - g1u, P.grad - g1p
+    loss.backward()
     U2 = U.detach().clone().requires_grad_()
     P2 = P.detach().clone().requires_grad_()
     ref = ops.link_loss(U2, P2, ei, torch.from_numpy(z["neg_p"]).to(DEV),
                         torch.from_numpy(z["pos_weights"]).to(DEV))
     (2.0 * ref).backward()
-    close(g1, U2.grad)
+    close(g1u, U2.grad)
+    close(g1p, P2.grad)
+    close(g2u, 0.5 * U2.grad)
+    close(g2p, 0.5 * P2.grad)
+    close(U.grad, 2.0 * U2.grad)     # 2 + 1 + 1
 
 
 def test_sage_conv_standalone_and_homogeneous_input():
@@ -580,11 +586,14 @@ def test_sample_negatives_uniform_and_seeded():
 
 @pytest.mark.parametrize("E,n_keys", [(0, 7), (1, 1), (1000, 1), (5000, 37),
                                       (300_000, 100_000), (2_000_000, 1_000_000),
-                                      (1_000_003, 2**21 + 5),
+                                      (1_000_003, 2**21 + 5),     # > 2^20 keys: LSD sort
+                                      (3_000_000, 2**20), (3 * 16384 + 5, 2**20 + 1),
+                                      (16384 * 5, 1000), (12_345, 2**17),
                                       (70_000_001, 1_000_000)])   # > 2^26 draws, ragged last tile
 def test_draw_sort_negatives_is_draw_then_sort(E, n_keys):
-    """hgnn_draw_sort_negatives (draws computed inside the sort's first pass) is bit for bit
-    hgnn_uniform_i32 followed by hgnn_sort_pairs_i32, and a stable sort (numpy) of the draws."""
+    """hgnn_draw_sort_negatives (draws computed inside the sort's first pass; for keys up to 2^20
+    the two-level grouping of csrc/negatives.hip) is bit for bit hgnn_uniform_i32 followed by
+    hgnn_sort_pairs_i32 (the LSD radix sort), and a stable sort (numpy) of the draws."""
     from truth_recommendation_gnn_amd import _native as Nn
     lib, s = Nn.lib(), Nn.stream_ptr(torch.device(DEV))
     seed = torch.tensor([0x1234_5678_9ABC_DEF], dtype=torch.int64, device=DEV)
@@ -863,3 +872,41 @@ def test_pre_projection_used_at_layer_two_only():
     assert not ops.use_pre_projection(h_post, x_user, 16, False)       # no root segment
     with torch.no_grad():
         assert ops.use_pre_projection(x_post, x_user, 16, True)        # inference: always
+
+
+def test_csr_cache_frees_structures_of_dead_edge_tensors():
+    """100 edge tensors built and dropped (inference.py:410-419's per-user graphs, a per-step
+    flip(0)): no cache entry and no device memory outlives them; a relation whose tensor died
+    between forward and backward still back-propagates (its COO is rebuilt from the CSR, in the
+    original edge order)."""
+    import gc
+    graph.CSR_CACHE.clear()
+    gc.collect()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    rng = np.random.default_rng(3)
+    for i in range(100):
+        ei = rand_coo(rng, 300, 200, 2000 + i).to(DEV)
+        csr = graph.relation_csr(ei, 300, 200)
+        _ = csr.bwd, csr.inv_deg
+        del ei, csr, _
+    gc.collect()
+    torch.cuda.synchronize()
+    assert len(graph.CSR_CACHE) == 0
+    assert torch.cuda.memory_allocated() == base
+    # the tensor dies after the forward: the backward's CSC comes from the rebuilt COO
+    x = torch.from_numpy(rng.standard_normal((300, 16)).astype(np.float32))
+    ei_cpu = rand_coo(rng, 300, 200, 3000)
+    xg = x.to(DEV).requires_grad_()
+    ei = ei_cpu.to(DEV)
+    csr = graph.relation_csr(ei, 300, 200)
+    y = ops.mean_gather(xg, csr)
+    del ei
+    gc.collect()
+    (y * y).sum().backward()
+    xr = x.clone().requires_grad_()
+    ref = sage_ref.mean_aggregate(xr, ei_cpu, 200)
+    (ref * ref).sum().backward()
+    close(y.detach().cpu(), ref.detach())
+    close(xg.grad.cpu(), xr.grad)
+    assert torch.equal(csr.edge_index.cpu(), ei_cpu)

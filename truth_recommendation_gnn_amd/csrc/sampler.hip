@@ -153,7 +153,7 @@ struct RelabelTab {
   int32_t T;   // node types
   const int32_t* prefix[kRelabelMaxTypes];
   int32_t* nodes[kRelabelMaxTypes];
-  int64_t id_limit[kRelabelMaxTypes];   // checked prefix ids must lie in [0, id_limit)
+  int64_t id_limit[kRelabelMaxTypes];   // prefix ids must lie in [0, id_limit) (< 0: no limit)
   int64_t p_off[kRelabelMaxTypes + 1];  // concatenated prefix positions per type
   int64_t i_off[kRelabelMaxTypes + 1];  // item ranges per type
 };
@@ -197,7 +197,7 @@ __global__ void k_relabel_prefix(RelabelTab t) {
   const int64_t i = g - t.p_off[ty];
   const int32_t id = t.prefix[ty][i];
   t.nodes[ty][i] = id;
-  if (id < 0 || (t.id_limit[ty] > 0 && id >= t.id_limit[ty])) {   // flagged, never inserted
+  if (id < 0 || (t.id_limit[ty] >= 0 && id >= t.id_limit[ty])) {   // flagged, never inserted
     if (t.nflags) atomicAnd(&t.nflags[ty], ~2);
     return;
   }
@@ -423,8 +423,8 @@ int hgnn_relabel(const int32_t* prefix, int64_t n_prefix, const int32_t* items, 
                  int32_t* local_out, int32_t* nodes_out, int32_t* d_count, void* ws,
                  size_t ws_bytes, hgnn_stream_t stream_) {
   int32_t* nodes[1] = {nodes_out};
-  const int64_t zero = 0;
-  return relabel(1, &prefix, &n_prefix, &zero, items, &n_items, local_out, nodes, d_count, false,
+  const int64_t no_limit = -1;   // unchecked: a limit of 0 would flag every id (an empty type)
+  return relabel(1, &prefix, &n_prefix, &no_limit, items, &n_items, local_out, nodes, d_count, false,
                  ws, ws_bytes, as_stream(stream_));
 }
 

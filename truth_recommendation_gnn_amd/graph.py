@@ -188,7 +188,12 @@ class RelationCSR:
         self.n_src, self.n_dst = int(n_src), int(n_dst)
         self.num_edges = int(edge_index.shape[1])
         self.chunk = chunk
-        self._ei = edge_index
+        # the COO is held weakly: the CSR cache keys on the edge tensor's lifetime, and a strong
+        # reference here would keep every cached tensor (and so its entry) alive.  When the tensor
+        # is gone (or changed in place) the COO is rebuilt from the CSR (see edge_index).
+        self._ei = None
+        self._ei_ref = weakref.ref(edge_index)
+        self._ei_version = edge_index._version
         self.fwd = group_edges(edge_index[1], edge_index[0], self.n_dst, self.n_src, chunk)
         self._inv_deg: Optional[torch.Tensor] = None
         self._bwd: Optional[GroupedEdges] = None
@@ -235,10 +240,23 @@ class RelationCSR:
 
     @property
     def edge_index(self) -> torch.Tensor:
-        """[2, E] COO (source, destination) in CSR order for a relation built ``from_csr``."""
-        if self._ei is None:
-            self._ei = torch.stack([self.fwd.col.long(), self._dst_of_positions(torch.int64)])
-        return self._ei
+        """[2, E] COO (source, destination): the caller's tensor while it lives unchanged;
+        otherwise rebuilt from the CSR — in the original edge order (``fwd.perm`` holds each CSR
+        position's COO id), or in CSR order for a relation built ``from_csr``."""
+        if self._ei is not None:
+            return self._ei
+        ref = getattr(self, "_ei_ref", None)
+        t = ref() if ref is not None else None
+        if t is not None and t._version == self._ei_version:
+            return t
+        g = self.fwd
+        coo = torch.stack([g.col.long(), self._dst_of_positions(torch.int64)])
+        if g.perm is None:
+            self._ei = coo            # from_csr: CSR order is the relation's edge order
+            return coo
+        out = torch.empty_like(coo)
+        out[:, g.perm.long()] = coo
+        return out                    # not kept: needed once per structure built from it
 
     @property
     def bwd(self) -> GroupedEdges:
@@ -306,6 +324,9 @@ class RelationCSR:
         if key in cache:
             return cache[key]
         B = int(n_blocks)
+        n_rows_side = self.n_dst if side == "fwd" else self.n_src
+        if B * n_rows_side >= 2**31 - 1:
+            raise ValueError(f"blocks: {B} passes x {n_rows_side} rows exceed the int32 rowptr")
         ei = self.edge_index
         if side == "fwd":
             n_rows, n_read, rows, reads = self.n_dst, self.n_src, ei[1], ei[0]
@@ -362,9 +383,23 @@ def build_csc_group(rels) -> None:
 
 
 class _CsrCache:
+    """Edge tensor -> its RelationCSR.  An entry lives as long as its edge tensor: a
+    ``weakref.finalize`` on the tensor drops it when the tensor is freed (a caller that builds a
+    fresh edge tensor per call — ``inference.py:410-419`` builds a graph per user, a per-step
+    ``flip(0)`` — pins nothing), and an in-place change of the tensor (new version) replaces its
+    entry.  ``cap`` bounds the entries of live tensors (least recently used dropped first)."""
+
     def __init__(self, cap: int = 64):
         self.cap = cap
         self._d: "collections.OrderedDict" = collections.OrderedDict()
+
+    def __len__(self):
+        return len(self._d)
+
+    def _drop(self, key, csr_id):
+        hit = self._d.get(key)
+        if hit is not None and id(hit[1]) == csr_id:
+            del self._d[key]
 
     def get(self, edge_index: torch.Tensor, n_src: int, n_dst: int,
             chunk: Optional[int] = None) -> RelationCSR:
@@ -376,8 +411,12 @@ class _CsrCache:
             if ref() is edge_index:
                 self._d.move_to_end(key)
                 return csr
+        # entries of this same tensor at an older version (changed in place since) are stale
+        for k in [k for k, (ref, _) in self._d.items() if ref() is edge_index]:
+            del self._d[k]
         csr = RelationCSR(edge_index, n_src, n_dst, chunk)
         self._d[key] = (weakref.ref(edge_index), csr)
+        weakref.finalize(edge_index, self._drop, key, id(csr))
         while len(self._d) > self.cap:
             self._d.popitem(last=False)
         return csr

@@ -263,6 +263,13 @@ def relu_mask_for(n: int, h: int, relu: bool, dev) -> Optional[torch.Tensor]:
 RELU_BITS = os.environ.get("HGNN_RELU_BITS", "1") == "1"
 
 
+def _check_rows(segs, n, what):
+    """Every segment of a K3 call has the same n rows (the kernels read each without bounds)."""
+    for i, s_ in enumerate(segs):
+        if s_.dim() != 2 or int(s_.shape[0]) != n:
+            raise ValueError(f"{what}: segment {i} is {tuple(s_.shape)}, expected {n} rows")
+
+
 def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.Tensor],
                relu: bool, add: Optional[torch.Tensor] = None,
                mask_out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -273,6 +280,11 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
     ks = [int(s.shape[1]) for s in segs]
     if w.shape[1] != sum(ks):
         raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(ks)}")
+    _check_rows(segs, n, "linear_fwd")
+    if add is not None and tuple(add.shape) != (n, h):
+        raise ValueError(f"linear_fwd: add is {tuple(add.shape)}, expected {(n, h)}")
+    if b is not None and b.numel() != h:
+        raise ValueError(f"linear_fwd: bias has {b.numel()} entries, expected {h}")
     dev = w.device
     out = torch.empty(n, h, dtype=torch.float32, device=dev)
     k = sum(ks)
@@ -292,6 +304,19 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
+    if w.shape[1] != sum(ks):
+        raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(ks)}")
+    _check_rows(segs, n, "linear_bwd")
+    for what, t in (("dout", dout), ("out_act", out_act), ("dz_out", dz_out)):
+        if t is not None and tuple(t.shape) != (n, h):
+            raise ValueError(f"linear_bwd: {what} is {tuple(t.shape)}, expected {(n, h)}")
+    if len(dxs) != len(segs):
+        raise ValueError(f"linear_bwd: {len(dxs)} dx buffers for {len(segs)} segments")
+    for s_, dx in zip(segs, dxs):
+        if dx is not None and tuple(dx.shape) != tuple(s_.shape):
+            raise ValueError(f"linear_bwd: dx {tuple(dx.shape)} for a {tuple(s_.shape)} segment")
+    if mask is not None and tuple(mask.shape) != (n, 4):
+        raise ValueError(f"linear_bwd: ReLU bits are {tuple(mask.shape)}, expected {(n, 4)}")
     dev = w.device
     dw = torch.empty_like(w) if need_w else None
     db = torch.empty(h, dtype=torch.float32, device=dev) if need_b else None
@@ -753,6 +778,12 @@ def hetero_layer(spec: LayerSpec, x_dict: Dict[str, torch.Tensor],
     N.require_device(*[t for t in flat if t is not None])
     for t in flat[:len(spec.types)]:
         _check_f32(t, "node features")
+    for g in spec.groups:
+        n = int(x_dict[g.dst].shape[0]) if g.n_root is None else int(g.n_root)
+        for src, csr in g.rels:
+            if csr.n_dst != n or csr.n_src != int(x_dict[src].shape[0]):
+                raise ValueError(f"hetero_layer: relation {src}->{g.dst} is {csr.n_src}->"
+                                 f"{csr.n_dst} rows, the tables give {x_dict[src].shape[0]}->{n}")
     outs = _HeteroLayer.apply(spec, *flat)
     return {g.dst: y for g, y in zip(spec.groups, outs)}
 
@@ -895,23 +926,31 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
 
 
 class _EdgeBCELoss(torch.autograd.Function):
+    """The forward computes dL/dU and dL/dP with the loss (one scoring pass, one dP gather) and
+    keeps them; the first backward scales them in place by the upstream gradient and hands them
+    on (no copy: 2 x 4.6 GB at cfg4).  A second backward through a retained graph
+    (``retain_graph=True``) recomputes them from the saved embeddings and the same negatives —
+    the kernels are deterministic, so it returns what the first did, as torch's loss would."""
+
     @staticmethod
     def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
                 ready=None):
         loss, dU, dP = _edge_bce(U, P, csr, neg_u_order, cscale, check, n_total, ready)
-        ctx.save_for_backward(dU, dP)
+        ctx.grads = (dU, dP)
+        ctx.save_for_backward(U, P)
+        ctx.args = (csr, neg_u_order, cscale, n_total)
         return loss
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, go):
-        # dU/dP are scaled in place by the upstream gradient: a second backward through the
-        # same graph (retain_graph=True) would scale them twice, so it is refused
-        if getattr(ctx, "consumed", False):
-            raise RuntimeError("edge_bce_loss: backward ran twice through the same graph; "
-                               "recompute the loss instead of retain_graph=True")
-        ctx.consumed = True
-        dU, dP = ctx.saved_tensors
+        if ctx.grads is None:        # retained graph, second backward: recompute
+            U, P = ctx.saved_tensors
+            csr, neg_u_order, cscale, n_total = ctx.args
+            _, dU, dP = _edge_bce(U, P, csr, neg_u_order, cscale, False, n_total)
+        else:
+            dU, dP = ctx.grads
+            ctx.grads = None         # handed on: autograd may accumulate into them from here
         g = go.to(torch.float32).reshape(()).contiguous()
         lib, s = N.lib(), N.stream_ptr(dU.device)
         for t in (dU, dP):   # in place; a no-op launch for loss.backward()'s gradient of 1

@@ -48,6 +48,9 @@ class MiniBatch:
     blocks: List[Block]                    # blocks[l]: nodes[l] -> nodes[l+1]
 
 
+_MAX_GROUP = 8     # relations per hop / node types per relabel / relations per CSC group
+
+
 def _i32(t: torch.Tensor) -> torch.Tensor:
     return t.to(torch.int32).contiguous()
 
@@ -56,11 +59,26 @@ class NeighborSampler:
     def __init__(self, num_nodes: Mapping[str, int],
                  edge_index_dict: Mapping[EdgeType, torch.Tensor],
                  relations: Sequence[EdgeType], fanouts: Sequence[int]):
+        if not fanouts:
+            raise ValueError("fanouts: at least one hop (one per model layer)")
         if any(f == 0 or f > 64 for f in fanouts):
             raise ValueError("fanouts must be in 1..64, or < 0 for every neighbour")
         self.num_nodes = {t: int(n) for t, n in num_nodes.items()}
         self.relations = [tuple(et) for et in relations]
         self.fanouts = list(fanouts)
+        # the one-launch hop kernels' limits (csrc/sampler.hip kHopMax / kRelabelMaxTypes, the
+        # CSC group's kTransposeMax in csr_build.hip), checked here rather than at sample time
+        types = set(self.num_nodes)
+        for et in self.relations:
+            if et[0] not in types or et[2] not in types:
+                raise ValueError(f"relation {et}: node type without a node count")
+        if len(self.relations) > _MAX_GROUP:
+            raise ValueError(f"{len(self.relations)} relations: the hop kernels take at most "
+                             f"{_MAX_GROUP} (one sampled block's CSCs are built by one sort)")
+        if len(types) > _MAX_GROUP:
+            raise ValueError(f"{len(types)} node types: the relabel takes at most {_MAX_GROUP}")
+        if len(types) > 1 and max(self.num_nodes.values()) * len(types) >= 2**31 - 1:
+            raise ValueError("node ids x types must stay below 2^31 (the relabel key)")
         # full-graph CSR per relation: rows = destinations, col = global source ids
         self.csr = {et: relation_csr(edge_index_dict[et], self.num_nodes[et[0]],
                                      self.num_nodes[et[2]]) for et in self.relations}
