@@ -211,6 +211,16 @@ int hgnn_linear_bwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
                          const float* out, const uint32_t* mask, float* const* dxs, float* dw,
                          float* db, float* dz_out, void* ws, size_t ws_bytes,
                          hgnn_stream_t stream);
+/* hgnn_linear_bwd_mask where bit s of dx_accumulate adds segment s's input gradient into what
+ * dxs[s] already holds instead of storing it: a node table whose gradient has several producers
+ * (layer 1's post output at layer 2: the post update's root term and the pre-projected
+ * relation's projection) gets the second one in the same pass, not through a separate add —
+ * autograd's gradient accumulation of train_gnn.py:283's backward. */
+int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
+                       int64_t n_rows, const float* w, int32_t h, const float* dout,
+                       const float* out, const uint32_t* mask, float* const* dxs,
+                       uint32_t dx_accumulate, float* dw, float* db, float* dz_out, void* ws,
+                       size_t ws_bytes, hgnn_stream_t stream);
 int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,

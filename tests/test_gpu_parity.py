@@ -264,6 +264,37 @@ def test_linear_bwd_variants(ks, h, mode):
         close(db, ref_db)
 
 
+@pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 128), ([128, 128], 128), ([128], 128),
+                                  ([16, 48], 128), ([3, 5], 7), ([64, 64, 128], 128)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_linear_bwd_dx_accumulate_bitwise(ks, h, masked):
+    """hgnn_linear_bwd_ex's accumulate bits (dX added into what the buffer holds, for tables with
+    two gradient producers — ops._pre_group_backward) give bitwise `held + dX` of the storing
+    backward, in every kernel family (persistent dgrad v4/v5, the fused two-role backward, the
+    general kernels), on the accumulated segments only."""
+    n = 64 * 150 + 29
+    gen = torch.Generator().manual_seed(11 * h + len(ks))
+    dsegs = [torch.randn(n, k, generator=gen).to(DEV) for k in ks]
+    w = (torch.randn(h, sum(ks), generator=gen) * 0.2).to(DEV)
+    b = torch.randn(h, generator=gen).to(DEV)
+    dout = torch.randn(n, h, generator=gen).to(DEV)
+    mk = ops.relu_mask_for(n, h, masked, torch.device(DEV))
+    out = ops.linear_fwd(dsegs, w, b, relu=masked, mask_out=mk)
+    act = out if masked else None
+    fresh = [torch.empty_like(x) for x in dsegs]
+    dw0, db0 = ops.linear_bwd(dsegs, w, dout, act, fresh, True, True, mask=mk)
+    held = [torch.randn(x.shape, generator=gen).to(DEV) for x in dsegs]
+    acc = [t.clone() for t in held]
+    add = [i % 2 == 0 for i in range(len(ks))]          # every other segment accumulates
+    for i, a in enumerate(add):
+        if not a:
+            acc[i].fill_(123.0)                          # overwritten
+    dw1, db1 = ops.linear_bwd(dsegs, w, dout, act, acc, True, True, mask=mk, dx_add=add)
+    for i, a in enumerate(add):
+        assert torch.equal(acc[i], held[i] + fresh[i] if a else fresh[i]), i
+    assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
+
+
 @pytest.mark.parametrize("case", ["rgcn", "author", "no_root", "no_bias", "single"])
 def test_fuse_weights_bitwise_equals_torch_expression(case):
     """hgnn_fuse_weights / hgnn_split_weight_grads against the torch expression they replace

@@ -50,6 +50,8 @@ _SIGS = {
                                       _p, _p]),
     "hgnn_linear_bwd_mask": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p,
                                       _p, _p, _p, _c_sz, _p]),
+    "hgnn_linear_bwd_ex": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p,
+                                    ctypes.c_uint32, _p, _p, _p, _p, _c_sz, _p]),
     "hgnn_fuse_weights": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _p, _c_i32, _p, _p, _p]),
     "hgnn_split_weight_grads": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _c_i32, _p, _p, _p,
                                          _p]),

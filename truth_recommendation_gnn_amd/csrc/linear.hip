@@ -39,6 +39,7 @@ struct LinArgs {
   uint32_t* mask_out;       // forward: write the ReLU mask as bits (nullable)
   const float* add;       // forward: [n, h] rows added before the activation (nullable)
   float* dz_out;          // backward: the masked dz written out as well (nullable; dgrad kernels)
+  uint32_t dx_acc;        // backward: bit s set = segment s's dX is added into dx, not stored
   float* out;
   float* slab;            // wgrad partials [gx][h][k_total+1]
   int64_t n;
@@ -270,12 +271,16 @@ __global__ void __launch_bounds__(256) k_linear_dgrad(const LinArgs a) {
     float* dx = a.seg[s].dx;
     if (!dx) continue;
     const int kk = col - a.seg[s].off, ks = a.seg[s].k;
+    const bool add = (a.dx_acc >> s) & 1u;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         const int64_t row = r0 + rt * 16 + 4 * g + jj;
-        if (row < a.n) dx[row * ks + kk] = acc[rt][t][jj];
+        if (row < a.n) {
+          float* p = dx + row * ks + kk;
+          *p = add ? *p + acc[rt][t][jj] : acc[rt][t][jj];
+        }
       }
   }
 }
@@ -535,10 +540,14 @@ __global__ void __launch_bounds__(256) k_linear_bwd_lds(const LinArgs a, int64_t
         float* dx = a.seg[s].dx;
         if (dx) {
           const int kk = col - a.seg[s].off, ks = a.seg[s].k;
+          const bool add = (a.dx_acc >> s) & 1u;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + rt * 16 + 4 * g + r;
-            if (row < a.n) dx[row * ks + kk] = o[r];
+            if (row < a.n) {
+              float* p = dx + row * ks + kk;
+              *p = add ? *p + o[r] : o[r];
+            }
           }
         }
       }
@@ -620,7 +629,21 @@ struct ChunkTab {
   float* dx[kMaxChunks];
   int32_t ld[kMaxChunks];
   int32_t col[kMaxChunks];   // first column of the chunk inside its segment
+  uint32_t dx_acc;           // bit c set = chunk c's dX is added into dx (LinArgs::dx_acc)
 };
+
+// dX fragment store of the persistent kernels: stored, or added into what dx holds (the
+// gradient of a node table that another update already wrote — one pass instead of a torch add)
+__device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1, float a2,
+                                          float a3) {
+  float4* q = reinterpret_cast<float4*>(p);
+  if (add) {
+    const float4 o = *q;
+    *q = make_float4(o.x + a0, o.y + a1, o.z + a2, o.w + a3);
+  } else {
+    *q = make_float4(a0, a1, a2, a3);
+  }
+}
 
 // Forward v4: persistent.  W is staged into LDS once per block; then each of the 8 waves streams
 // its own 16-row tiles (no further barriers), with the next tile's A fragments in flight during
@@ -895,8 +918,8 @@ __global__ void __launch_bounds__(512) k_linear_bwd_v4(const LinArgs a, const Ch
                 float* dx = tab.dx[ct + h2];
                 if (dx) {
                   const f32x4 o = h2 ? o1 : o0;
-                  *reinterpret_cast<float4*>(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] +
-                                             4 * g) = make_float4(o[0], o[1], o[2], o[3]);
+                  store_dx4(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] + 4 * g,
+                            (tab.dx_acc >> (ct + h2)) & 1u, o[0], o[1], o[2], o[3]);
                 }
               }
             }
@@ -1222,8 +1245,8 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
           float* dx = tab.dx[ct + h2];
           if (dx) {
             const f32x4 o = h2 ? o1 : o0;
-            *reinterpret_cast<float4*>(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] + 4 * g) =
-                make_float4(o[0], o[1], o[2], o[3]);
+            store_dx4(dx + row * tab.ld[ct + h2] + tab.col[ct + h2] + 4 * g,
+                      (tab.dx_acc >> (ct + h2)) & 1u, o[0], o[1], o[2], o[3]);
           }
         }
       }
@@ -1324,8 +1347,8 @@ __global__ void __launch_bounds__(512, 2) k_linear_dgrad_v5(const LinArgs a, con
           const int ct = gi * G + j;
           float* dx = tab.dx[ct];
           if (dx)
-            *reinterpret_cast<float4*>(dx + row * tab.ld[ct] + tab.col[ct] + 4 * g) =
-                make_float4(o[j][0], o[j][1], o[j][2], o[j][3]);
+            store_dx4(dx + row * tab.ld[ct] + tab.col[ct] + 4 * g, (tab.dx_acc >> ct) & 1u,
+                      o[j][0], o[j][1], o[j][2], o[j][3]);
         }
       }
     }
@@ -1367,6 +1390,7 @@ static ChunkTab chunk_table(const LinArgs& a) {
     while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
     t.x[c] = a.seg[s].x;
     t.dx[c] = a.seg[s].dx;
+    if ((a.dx_acc >> s) & 1u) t.dx_acc |= 1u << c;
     t.ld[c] = a.seg[s].k;
     t.col[c] = k - a.seg[s].off;
   }
@@ -1554,10 +1578,21 @@ int hgnn_linear_bwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
                          const float* w, int32_t h, const float* dout, const float* out,
                          const uint32_t* mask, float* const* dxs, float* dw, float* db,
                          float* dz_out, void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  return hgnn_linear_bwd_ex(n_seg, xs, ks, n_rows, w, h, dout, out, mask, dxs, 0u, dw, db, dz_out,
+                            ws, ws_bytes, stream_);
+}
+
+int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
+                       const float* w, int32_t h, const float* dout, const float* out,
+                       const uint32_t* mask, float* const* dxs, uint32_t dx_accumulate,
+                       float* dw, float* db, float* dz_out, void* ws, size_t ws_bytes,
+                       hgnn_stream_t stream_) {
   hipStream_t stream = as_stream(stream_);
   LinArgs a{};
   bool vec;
   if (int rc = fill_args(a, n_seg, xs, ks, dxs, n_rows, w, h, &vec)) return rc;
+  if (dx_accumulate >> n_seg) return fail(HGNN_E_ARG, "linear_bwd: accumulate bits beyond n_seg");
+  a.dx_acc = dx_accumulate;
   if (!dout && n_rows > 0) return fail(HGNN_E_ARG, "linear_bwd: dout is null");
   if (mask && (!out || h % 16 != 0 || h > 128))
     return fail(HGNN_E_ARG, "linear_bwd_mask: the bit mask needs `out` too, h %% 16 == 0, h <= 128");
@@ -1583,8 +1618,8 @@ int hgnn_linear_bwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     if (int rc = hgnn_hetero_epilogue_bwd(1, &one, n_rows * h, out ? 1 : 0, out, dout, &dz_out,
                                           stream_))
       return rc;
-    return hgnn_linear_bwd_dz(n_seg, xs, ks, n_rows, w, h, dz_out, nullptr, dxs, dw, db,
-                              nullptr, ws, ws_bytes, stream_);
+    return hgnn_linear_bwd_ex(n_seg, xs, ks, n_rows, w, h, dz_out, nullptr, nullptr, dxs,
+                              dx_accumulate, dw, db, nullptr, ws, ws_bytes, stream_);
   }
   a.dz_out = dz_out;
   if (fwd4_ok(a, vec)) {

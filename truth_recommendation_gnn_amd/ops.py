@@ -298,9 +298,10 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
 
 def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], need_w: bool,
                need_b: bool, dz_out: Optional[torch.Tensor] = None,
-               mask: Optional[torch.Tensor] = None):
+               mask: Optional[torch.Tensor] = None, dx_add: Sequence[bool] = ()):
     """K3 backward; ``dz_out`` (optional [n, h]) receives the masked dz as well; ``mask``: the
-    forward's ReLU bits (read instead of ``out_act`` by the persistent kernels)."""
+    forward's ReLU bits (read instead of ``out_act`` by the persistent kernels); ``dx_add[s]``:
+    segment s's input gradient is added into what ``dxs[s]`` holds (``hgnn_linear_bwd_ex``)."""
     n = int(segs[0].shape[0])
     h = int(w.shape[0])
     ks = [int(s.shape[1]) for s in segs]
@@ -328,12 +329,17 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     nb = 4 * n * (h + (h if out_act is not None and not bits else 0) + sum(ks) + k_dx) + \
         (16 * n if bits else 0)
     fl = 2 * n * h * k_dx + (2 * n * sum(ks) * h if need_w else 0)   # dgrad + wgrad
+    acc = 0
+    for i, on in enumerate(dx_add):
+        if on and dxs[i] is not None:
+            acc |= 1 << i
+            nb += 4 * n * ks[i]          # the gradient already there is read back
     with _timed(f"linear_bwd[{n}x{sum(ks)}->{h}]", nb, flops=fl):
-        N.check(N.lib().hgnn_linear_bwd_mask(
+        N.check(N.lib().hgnn_linear_bwd_ex(
             len(segs), N.ptr_array(segs), N.int_array(ks), n, N.ptr(w), h, N.ptr(dout),
             N.ptr(out_act), N.ptr(mask if out_act is not None else None), N.ptr_array(dxs),
-            N.ptr(dw), N.ptr(db), N.ptr(dz_out), N.ptr(ws), 0 if ws is None else ws.numel(),
-            N.stream_ptr(dev)), "hgnn_linear_bwd_mask")
+            acc, N.ptr(dw), N.ptr(db), N.ptr(dz_out), N.ptr(ws), 0 if ws is None else ws.numel(),
+            N.stream_ptr(dev)), "hgnn_linear_bwd_ex")
     return dw, db
 
 
@@ -729,43 +735,46 @@ def _pre_group_backward(g: DstGroup, xs, aggrs, w, dout, y, need_x, need_w, need
             pending.setdefault(src, []).append((dA, csr))
         else:
             dxs.append(None)
+    dx_add = [False] * len(dxs)
     if g.root:
         segs.append(_root(g, xs))
         o = cols[-1][0] + cols[-1][1] if cols else 0
         seg_cols.append((o, int(w.shape[1]) - o))
         if need_x[g.dst]:
-            d_root = torch.empty_like(segs[-1])
-            dxs.append(d_root)
+            # the root gradient is added into the destination table's gradient in the dgrad pass
+            # when another update already wrote it (no separate add); else it is that gradient
+            # (a block's prefix of a zeroed table: its other rows wait for the K2s)
+            dx_add.append(gx[g.dst] is not None)
+            if gx[g.dst] is None:
+                gx[g.dst] = (torch.empty_like(xs[g.dst]) if g.n_root is None
+                             else torch.zeros_like(xs[g.dst]))
+            dxs.append(gx[g.dst] if g.n_root is None else gx[g.dst][:g.n_root])
         else:
-            d_root = None
             dxs.append(None)
+            dx_add.append(False)
     dw = torch.empty_like(w) if need_w else None
     dw_main, db = linear_bwd(segs, _main_weight(g, w, cols), dout, y if g.relu else None, dxs,
-                             need_w, need_b, dz_out=dz if g.relu else None, mask=mask)
+                             need_w, need_b, dz_out=dz if g.relu else None, mask=mask,
+                             dx_add=dx_add)
     if dw is not None:
         o = 0
         for (co, k) in seg_cols:
             dw[:, co:co + k].copy_(dw_main[:, o:o + k])
             o += k
-    if g.root and d_root is not None:
-        if g.n_root is not None:
-            if gx[g.dst] is None:
-                gx[g.dst] = torch.zeros_like(xs[g.dst])
-            gx[g.dst][:g.n_root].add_(d_root)
-        else:
-            gx[g.dst] = d_root if gx[g.dst] is None else gx[g.dst].add_(d_root)
     # pre-projected relations: dP = K2(dz) over the CSC, then P = x_src W_r^T's backward
     for (src, csr), pre, (o, k) in zip(g.rels, g.pre, cols):
         if not pre:
             continue
         x_src = xs[src]
         dP = scatter_mean_bwd(dz, csr)
-        dxp = torch.empty_like(x_src) if need_x[src] else None
-        dwp, _ = linear_bwd([x_src], w[:, o:o + k].contiguous(), dP, None, [dxp], need_w, False)
+        add = need_x[src] and gx[src] is not None   # added into the table's gradient in place
+        dxp = (gx[src] if add else torch.empty_like(x_src)) if need_x[src] else None
+        dwp, _ = linear_bwd([x_src], w[:, o:o + k].contiguous(), dP, None, [dxp], need_w, False,
+                            dx_add=[add])
         if dw is not None:
             dw[:, o:o + k].copy_(dwp)
         if dxp is not None:
-            gx[src] = dxp if gx[src] is None else gx[src].add_(dxp)
+            gx[src] = dxp
     return dw, db
 
 
