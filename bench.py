@@ -96,7 +96,11 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=None,
                    help="default: the box's allotted CPUs (OMP_NUM_THREADS / affinity)")
-    p.add_argument("--cpu-sample-scale", type=float, default=None)
+    p.add_argument("--cpu-sample-scale", type=float, default=None,
+                   help="cfg5: the CPU baseline's down-scaled sample")
+    p.add_argument("--cpu-shard", type=int, default=None,
+                   help="full-batch configs: time rank 0's 1/S destination shard on the CPU oracle "
+                        "(default: cfg4 64, cfg2/cfg3 1 = the whole graph)")
     p.add_argument("--profile-steps", action="store_true",
                    help="no per-kernel-event run (for rocprofv3 runs)")
     p.add_argument("--dist-backend", default="nccl",
@@ -143,7 +147,8 @@ def host_cores():
 def cpu_baseline(cfg, threads=None, scale=None):
     """The plain-torch CPU oracle (PyG's op pattern: materialised ``index_select``,
     ``scatter_reduce`` mean, ``addmm``) running the same training step on a down-scaled graph of
-    the same family; edges/s = median over 5 steps after 2 warm-ups."""
+    the same family; edges/s = median over 5 steps after 2 warm-ups.  (The cfg5 mini-batch
+    line's comparison; the full-batch lines use :func:`cpu_baseline_shard`.)"""
     from oracle import sage_ref
     phys, allotted = host_cores()
     threads = threads or allotted
@@ -192,6 +197,96 @@ def cpu_baseline(cfg, threads=None, scale=None):
                       f"CPU with {threads} threads = the CPUs allotted to this job "
                       f"(host has {phys} physical cores); edges/s extrapolates linearly "
                       f"(per-edge work is scale-free, the sample's smaller tables favour the CPU)"}
+
+
+# SURVEY §8d's CPU baseline for the full-batch configs: cfg2 / cfg3 whole, cfg4 (which needs
+# >100 GB per materialised [E, d] relation on the oracle) as a destination shard.  The default
+# cfg4 shard keeps the bench's CPU leg to ~30 s; `--cpu-shard 8` is the verdict's 1/8 shard
+# (about 2 minutes, recorded separately under profiles/).
+CPU_SHARD = {"cfg4": 64}
+
+
+def cpu_baseline_shard(cfg, g, rels, threads=None, shard=None, steps=3, warmup=1):
+    """The oracle's training step (oracle/sage_ref.py: PyG's op pattern, materialised
+    ``index_select`` + ``scatter_reduce`` mean + ``addmm``; train_gnn.py:242-285) over rank 0's
+    DESTINATION SHARD of the graph the GPU line timed, at ``shard`` ranks: users [0, U/S) and post
+    rows [0, P/S) are the destinations, each with ALL of its in-edges (rev_engages into the users,
+    engages into the posts), read from the full 9M / 1M-row source tables; rows a shard does not
+    own stand in for the tables the other ranks would provide (values irrelevant to the timing).
+    The loss is the reference's over the shard users' positive edges.  2 layers fwd + loss + bwd
+    + Adam; edges/s = the shard's edges per step (layers x in-edges of its destinations) / the
+    median step time, which is the whole graph's rate when the S shards run one after another on
+    these cores.  S = 1 is the whole graph (cfg2, cfg3)."""
+    from oracle import sage_ref
+    import torch.nn.functional as F
+    phys, allotted = host_cores()
+    threads = threads or allotted
+    torch.set_num_threads(threads)
+    S = shard if shard is not None else CPU_SHARD.get(cfg.name.split("x")[0], 1)
+    U, P = cfg.num_users, cfg.num_posts
+    nu, npo = -(-U // S), -(-P // S)
+    e = g.edge_index_dict[synth.ENGAGES]
+    # the shard's edges, selected where the graph lives, then moved to the host
+    m_u = e[0] < nu                                  # rev_engages into own users
+    m_p = e[1] < npo                                 # engages into own posts
+    rev = torch.stack([e[1][m_u], e[0][m_u]]).cpu()  # (post -> own user)
+    eng = torch.stack([e[0][m_p], e[1][m_p]]).cpu()  # (user -> own post)
+    pw = synth.interaction_weights(P)[rev[0]]        # the own users' positive edges
+    x_user, x_post = g.x_dict["user"].cpu(), g.x_dict["post"].cpu()
+    names = []
+    for l in range(cfg.layers):
+        cin = cfg.dim if l == 0 else cfg.hidden
+        for et, _ in rels:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (cfg.hidden, cin)), (f"{p}.lin_l.bias", (cfg.hidden,)),
+                      (f"{p}.lin_r.weight", (cfg.hidden, cin))]
+    params = {k: v.requires_grad_() for k, v in sage_ref.init_params(names).items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    ru, rp = "__".join(synth.REV_ENGAGES), "__".join(synth.ENGAGES)
+    own_u, own_p = torch.arange(nu), torch.arange(npo)
+    pos = torch.stack([rev[1], rev[0]])              # (own user, post)
+    gen = torch.Generator().manual_seed(synth.NEG_SEED)
+
+    def conv(l, rel, x_src, x_dst, ei):
+        return sage_ref.sage_conv(x_src, x_dst, ei, *sage_ref._conv_params(params, f"layers.{l}.{rel}"))
+
+    def step():
+        opt.zero_grad()
+        tab_u, tab_p = x_user, x_post
+        h_u, h_p = x_user[:nu], x_post[:npo]
+        for l in range(cfg.layers):
+            h_u = F.relu(conv(l, ru, tab_p, h_u, rev))
+            h_p = F.relu(conv(l, rp, tab_u, h_p, eng))
+            # the next layer's source tables: the shard's own rows, the rest stand-ins
+            tab_u = x_user.index_copy(0, own_u, h_u)
+            tab_p = x_post.index_copy(0, own_p, h_p)
+        neg = torch.randint(0, P, (pos.shape[1],), generator=gen)
+        loss = sage_ref.link_loss(h_u, tab_p, pos, neg, pw)
+        loss.backward()
+        opt.step()
+
+    for _ in range(warmup):
+        step()
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    dt = statistics.median(times)
+    edges = cfg.layers * (int(rev.shape[1]) + int(eng.shape[1]))
+    total = cfg.layers * 2 * int(e.shape[1])
+    return {"value": round(edges / dt, 1), "unit": "edges/s", "cores": threads,
+            "host_physical_cores": phys, "kind": "port",
+            "sample": (f"{cfg.name}: " + ("the whole graph" if S == 1 else
+                       f"rank 0's 1/{S} destination shard (users [0,{nu}), post rows [0,{npo}) "
+                       f"with all their in-edges: {int(rev.shape[1])} rev_engages + "
+                       f"{int(eng.shape[1])} engages, full {U}/{P}-row source tables)")
+                       + f", d=h={cfg.dim}, {cfg.layers}-layer fwd+loss+bwd+Adam, {edges} edges/step"
+                       + ("" if S == 1 else f" ({edges / total:.4f} of the graph's {total}; "
+                          f"x{S} extrapolation: the whole step ~{dt * S:.0f} s on these cores)")
+                       + f"; median of {steps} steps after {warmup} warm-up ({dt:.2f} s/step), "
+                       f"oracle/sage_ref.py op pattern on torch CPU, {threads} threads = the CPUs "
+                       f"allotted to this job (host has {phys} physical cores)")}
 
 
 # ----------------------------------------------------------------------------- launcher
@@ -357,7 +452,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     rels = relations_of(cfg)
     t_setup = time.perf_counter()
     if not sharded:
-        g = synth.make_graph(cfg, device=dev)
+        g = synth.make_graph(cfg, device=dev, device_gen=True)   # the graph the shards hold
         pos = g.edge_index_dict[synth.ENGAGES]
         pw = synth.interaction_weights(cfg.num_posts).to(dev)[pos[1]]
         # BCEWithLogitsLoss() collapses the per-edge interaction weights to their mean
@@ -375,21 +470,26 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                                      check=False, cscale=cscale)
     else:
         env = parallel.DistEnv.from_torch()
-        # every rank generates the identical seeded global graph on its own device (a few
-        # hundred ms on the GPU, cheaper than broadcasting 6.4 GB of edges), keeps its shard's
-        # CSRs and drops the global tensors before the timed region
-        g = synth.make_graph(cfg, device=dev, device_gen=not on_cpu)
-        pos_g = g.edge_index_dict[synth.ENGAGES]
-        pw_g = synth.interaction_weights(cfg.num_posts).to(dev)[pos_g[1]]
+        # every rank generates the seeded global graph's edges chunk by chunk on its own device
+        # (counter-based draws: the same graph on every rank and at every N) and keeps only its
+        # shard's (parallel.shard_edge_filter): the 200M-edge list never exists on one rank.
         # slice_inputs: every rank keeps the whole static input user table, so layer 1's post
         # slice mean is computed locally (no partial sums, no reduce-scatter at layer 1)
+        keep = parallel.shard_edge_filter(cfg.num_users, cfg.num_posts, env.world, env.rank,
+                                          slice_inputs=True)
+        g = synth.make_graph(cfg, device=dev, device_gen=True, keep=keep)
+        pos_g = g.edge_index_dict[synth.ENGAGES]
+        pw_g = synth.interaction_weights(cfg.num_posts).to(dev)[pos_g[1]]
+        n_eng = cfg.num_engages if cfg.num_engages else cfg.num_posts
         shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in rels}, cfg.num_users,
                                    cfg.num_posts, env, impl=impl, pos_weights=pw_g,
-                                   slice_inputs=True)
+                                   slice_inputs=True, num_edges_global=n_eng)
         x_user = g.x_dict["user"][shard.lo:shard.hi].contiguous()
         x_user_full = g.x_dict["user"]
         x_post = g.x_dict["post"]
-        edges_step = cfg.layers * sum(int(g.edge_index_dict[et].shape[1]) for et, _ in rels)
+        n_rel = {synth.ENGAGES: n_eng, synth.REV_ENGAGES: n_eng, synth.SOCIAL: cfg.num_social,
+                 synth.POST_POST: cfg.num_post_post}
+        edges_step = cfg.layers * sum(n_rel[et] for et, _ in rels)
         del g, pos_g, pw_g
         if not on_cpu:
             torch.cuda.empty_cache()
@@ -453,8 +553,11 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     roof = _roofline(kern, cfg, world)
     proj = _projection(kern)
     cpu = None
-    if not args.no_cpu_baseline and world == 1 and not on_cpu:
-        cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
+    if not args.no_cpu_baseline and world == 1 and not on_cpu and not sharded:
+        if set(et for et, _ in rels) == {synth.ENGAGES, synth.REV_ENGAGES}:
+            cpu = cpu_baseline_shard(cfg, g, rels, args.cpu_threads, args.cpu_shard)
+        else:
+            cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
     strong = world == 1 or not args.weak
     return {
         "metric": "edges/s (fwd+bwd) hetero message-passing",

@@ -23,8 +23,30 @@ from truth_recommendation_gnn_amd import HeteroSAGE, ops, parallel, synth  # noq
 RELATIONS = [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)]
 
 
+XGMI_LINK_GBS = 153.0        # one xGMI link per direction (a ring step is bound by one link)
+XGMI_LINKS = 7               # peer links per GPU (a direct all-to-all pattern uses all of them)
+
+
+class _Issued:
+    """A stand-in collective's handle: records, on the stream, when its consumer waits."""
+
+    def __init__(self, log, rec):
+        self.log, self.rec = log, rec
+
+    def wait(self):
+        if self.rec is not None and "wait" not in self.rec:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.rec["wait"] = ev
+        return True
+
+
 class EmulEnv(parallel.DistEnv):
-    """``world`` ranks seen from ``rank``, every collective a local stand-in (timing only)."""
+    """``world`` ranks seen from ``rank``, every collective a local stand-in (timing only).
+    With ``log`` (a list) each collective records an event on the main stream when it is issued
+    (after its stand-in copy) and one when its consumer waits for it: the time between the two
+    is the compute the real collective runs under."""
+    log = None
 
     def use_side_adjoint(self, t):
         return False
@@ -32,18 +54,32 @@ class EmulEnv(parallel.DistEnv):
     def all_reduce_(self, t):
         return t
 
+    def _issued(self, name, recv_bytes):
+        if self.log is None:
+            return parallel._Done()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        rec = {"op": name, "recv_bytes": int(recv_bytes), "issue": ev}
+        self.log.append(rec)
+        return _Issued(self.log, rec)
+
     def reduce_scatter_async(self, full):
         S = full.shape[0] // self.world
-        return full[self.rank * S:(self.rank + 1) * S].clone(), parallel._Done()
+        out = full[self.rank * S:(self.rank + 1) * S].clone()
+        nbytes = full.numel() * full.element_size() * (self.world - 1) // self.world
+        return out, self._issued("reduce_scatter", nbytes)
 
     def all_gather_async(self, own):
-        return own.repeat(self.world, *([1] * (own.dim() - 1))), parallel._Done()
+        out = own.repeat(self.world, *([1] * (own.dim() - 1)))
+        return out, self._issued("all_gather", own.numel() * own.element_size() * (self.world - 1))
 
     def all_to_all_async(self, inp, send_splits, recv_splits):
-        return inp.new_zeros((int(sum(recv_splits)),) + tuple(inp.shape[1:])), parallel._Done()
+        out = inp.new_zeros((int(sum(recv_splits)),) + tuple(inp.shape[1:]))
+        return out, self._issued("all_to_all", out.numel() * out.element_size())
 
     def all_reduce_async(self, t):
-        return parallel._Done()
+        return self._issued("all_reduce", 2 * t.numel() * t.element_size() * (self.world - 1)
+                            // self.world)
 
 
 def main():
@@ -97,7 +133,25 @@ def main():
         step()
     ops.set_timer(None)
     kern = {k: round(v["ms"] / args.steps, 4) for k, v in sorted(timer.summary().items())}
+    # one more step with the collectives' issue / consumer-wait points recorded
+    env.log = []
+    step()
+    flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])   # sync_grads' all-reduce
+    env.all_reduce_async(flat).wait()
+    torch.cuda.synchronize()
+    colls = []
+    for r in env.log:
+        cover = r["issue"].elapsed_time(r["wait"]) if "wait" in r else None
+        t1 = r["recv_bytes"] / (XGMI_LINK_GBS * 1e9) * 1e3
+        t7 = t1 / XGMI_LINKS
+        colls.append({"op": r["op"], "recv_MB_per_rank": round(r["recv_bytes"] / 1e6, 1),
+                      "cover_ms": None if cover is None else round(cover, 3),
+                      "est_ms_1link_ring": round(t1, 3), "est_ms_7links": round(t7, 3),
+                      "cover_over_1link": None if cover is None else round(cover / t1, 2) if t1 else None,
+                      "cover_over_7links": None if cover is None else round(cover / t7, 2) if t7 else None})
+    env.log = None
     print(json.dumps({"world": args.world, "rank": 0, "config": gcfg.name,
+                      "collectives": colls,
                       "scaling": "strong" if args.strong else "weak",
                       "users_own": shard.n_own, "posts_padded": shard.n_posts_pad,
                       "local_edges_per_step": edges_local,

@@ -124,3 +124,92 @@ def test_user_range_partitions_exactly():
         rs = [user_range(n, w, r) for r in range(w)]
         assert rs[0][0] == 0 and rs[-1][1] == n
         assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+
+
+def _shard_build_worker(rank, world, port, q, kind):
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from dist_torch_impl import TorchImpl
+    from truth_recommendation_gnn_amd import HeteroSAGE, parallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(1)
+        env = DistEnv.from_torch()
+        base = synth.scaled("cfg5" if kind == "rel4" else "cfg2", 0.0002 if kind == "rel4" else 0.0005)
+        cfg = synth.dataclasses.replace(base, dim=16, hidden=16)
+        rels = ([(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
+                 (synth.POST_POST, 0.5)] if kind == "rel4"
+                else [(synth.REV_ENGAGES, 1.0), (synth.ENGAGES, 1.0)])
+        res = []
+        for sharded in (False, True):
+            keep = (parallel.shard_edge_filter(cfg.num_users, cfg.num_posts, world, rank, True)
+                    if sharded else (lambda et, s, d: torch.ones_like(s, dtype=torch.bool)))
+            g = synth.make_graph(cfg, "cpu", keep=keep)       # counter-based, chunked
+            pos = g.edge_index_dict[synth.ENGAGES]
+            pw = synth.interaction_weights(cfg.num_posts)[pos[1]]
+            torch.manual_seed(3)
+            model = HeteroSAGE(cfg.hidden, rels, num_layers=2, in_channels=cfg.dim)
+            shard = UserShard({et: g.edge_index_dict[et] for et, _ in rels}, cfg.num_users,
+                              cfg.num_posts, env, impl=TorchImpl(), pos_weights=pw,
+                              slice_inputs=True, num_edges_global=cfg.num_engages)
+            neg = torch.randint(0, cfg.num_posts, (shard.pos_local.shape[1],),
+                                generator=torch.Generator().manual_seed(7 + rank))
+            lo, hi = user_range(cfg.num_users, world, rank)
+            loss = shard.step(model, g.x_dict["user"][lo:hi], g.x_dict["post"], neg,
+                              x_user_full=g.x_dict["user"])
+            sync_grads(model, env)
+            res.append((float(env.all_reduce_(loss.clone())),
+                        {n: p.grad.clone() for n, p in model.named_parameters()},
+                        int(g.edge_index_dict[synth.ENGAGES].shape[1])))
+        (l0, g0, e0), (l1, g1, e1) = res
+        q.put({"rank": rank, "same_loss": l0 == l1,
+               "same_grads": all(torch.equal(g0[n], g1[n]) for n in g0),
+               "edges_full": e0, "edges_shard": e1})
+    except Exception as e:
+        q.put({"rank": rank, "error": repr(e)})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,kind", [(2, "engage2"), (3, "rel4")])
+def test_shard_only_graph_build_gives_the_same_step(world, kind):
+    """bench.py's N > 1 setup generates only each rank's edges (parallel.shard_edge_filter over
+    the chunked counter-based generator): UserShard.step on that shard equals the step on the
+    global edge list bit for bit, and the shard holds a fraction of the edges."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_build_worker, args=(r, world, port, q, kind))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r["error"] for r in res if "error" in r]
+    assert not errs, errs
+    for r in res:
+        assert r["same_loss"] and r["same_grads"], r
+        assert r["edges_shard"] < r["edges_full"], r
+
+
+def test_counter_generator_is_chunk_invariant_and_matches_its_distributions(monkeypatch):
+    cfg = synth.scaled("cfg4", 0.001)
+    g = synth.make_graph(cfg, "cpu", keep=lambda et, s, d: torch.ones_like(s, dtype=torch.bool))
+    e = g.edge_index_dict[synth.ENGAGES]
+    monkeypatch.setattr(synth, "GEN_CHUNK", 997)
+    g2 = synth.make_graph(cfg, "cpu", keep=lambda et, s, d: torch.ones_like(s, dtype=torch.bool))
+    assert torch.equal(g2.edge_index_dict[synth.ENGAGES], e)
+    assert torch.equal(g.edge_index_dict[synth.REV_ENGAGES], e.flip(0))
+    assert e.shape == (2, cfg.num_engages)
+    assert int(e[0].min()) >= 0 and int(e[0].max()) < cfg.num_users
+    assert int(e[1].min()) >= 0 and int(e[1].max()) < cfg.num_posts
+    deg_u = torch.bincount(e[0], minlength=cfg.num_users).double()
+    deg_p = torch.bincount(e[1], minlength=cfg.num_posts).double()
+    assert abs(float(deg_u.mean()) - 200_000 / 9_000) < 1e-6       # uniform users ...
+    assert float(deg_u.std()) < 2 * float(deg_u.mean()) ** 0.5       # ... Poisson-like
+    top = float(deg_p.max()) / cfg.num_engages                         # Zipf(0.8) head share
+    w = (torch.arange(1, cfg.num_posts + 1, dtype=torch.float64) ** -0.8)
+    assert abs(top - float(w[0] / w.sum())) < 0.1 * float(w[0] / w.sum())

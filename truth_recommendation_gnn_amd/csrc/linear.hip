@@ -645,13 +645,40 @@ __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1
   }
 }
 
+// The added rows of one 16-row tile (hgnn_linear_fwd_add: a pre-projected relation's gathered
+// mean), loaded before the tile's MFMA sweep, which hides their HBM latency; read in the
+// epilogue they stalled every tile (K = 128 + add ran at 0.53 of the fp32 MFMA peak).  Lane
+// (i, g) holds columns 16 tt + 4 g .. +3 of its row.  The bias stays an epilogue read (L1-hot).
+template <int NT, bool ADD>
+struct Epi {
+  float4 d[ADD ? NT : 1];
+  __device__ __forceinline__ void load(const LinArgs& a, int64_t row, int H, int g) {
+    if constexpr (ADD) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt)
+        d[tt] = row < a.n ? *reinterpret_cast<const float4*>(a.add + row * H + tt * 16 + 4 * g)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // (acc + bias) + add: the order of the unfused expression
+  __device__ __forceinline__ float4 sum(const f32x4& acc, int tt, const LinArgs& a, int g) const {
+    const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = make_float4(acc[0] + bb.x, acc[1] + bb.y, acc[2] + bb.z, acc[3] + bb.w);
+    if constexpr (ADD) {
+      v.x += d[tt].x; v.y += d[tt].y; v.z += d[tt].z; v.w += d[tt].w;
+    }
+    return v;
+  }
+};
+
 // Forward v4: persistent.  W is staged into LDS once per block; then each of the 8 waves streams
 // its own 16-row tiles (no further barriers), with the next tile's A fragments in flight during
 // the current tile's MFMAs.  (Measured and rejected: MFMAs interleaved across accumulators —
 // the 4-deep dependent chains are already covered by 4 waves per SIMD — and a two-stage register
 // ping-pong instead of the copy, which spills: 193-200 us vs 202-205 and 227 at N=1M, K=128.)  Output tiles are computed transposed (out^T = W X^T) so every lane
 // stores one float4 per 16 output columns.
-template <int H, int K>
+template <int H, int K, bool ADD>
 __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 : 2))) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
                                                        int64_t n_tiles) {
   constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
@@ -685,6 +712,9 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
     int wo = wl0;
     asm volatile("" : "+v"(wo));
     const float* wl = ws + wo;
+    const int64_t row = t * 16 + i;
+    Epi<NT, ADD> ep;               // the added rows, in flight during the sweep
+    ep.load(a, row, H, g);
     f32x4 acc[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -698,20 +728,11 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
         acc[tt] = mfma4(bv.z, av[c].z, acc[tt]);
         acc[tt] = mfma4(bv.w, av[c].w, acc[tt]);
       }
-    const int64_t row = t * 16 + i;
     if (row < a.n) {
       uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        // bias re-read per tile (L1-resident) rather than held in 4*NT VGPRs for the whole loop
-        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 v = make_float4(acc[tt][0] + bb.x, acc[tt][1] + bb.y, acc[tt][2] + bb.z,
-                               acc[tt][3] + bb.w);
-        if (a.add) {
-          const float4 ad = *reinterpret_cast<const float4*>(a.add + row * H + tt * 16 + 4 * g);
-          v.x += ad.x; v.y += ad.y; v.z += ad.z; v.w += ad.w;
-        }
+        float4 v = ep.sum(acc[tt], tt, a, g);
         if (a.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
@@ -736,7 +757,7 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
 //    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
 //    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
 //    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
-template <int H, int K>
+template <int H, int K, bool ADD>
 __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const ChunkTab tab,
                                                           int64_t n_tiles) {
   constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
@@ -768,6 +789,9 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
     int wo = wl0;
     asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
     const float* wl = ws + wo;
+    const int64_t row = t * 16 + i;
+    Epi<NT, ADD> ep;               // the added rows, in flight during the sweep (see v4)
+    ep.load(a, row, H, g);
     f32x4 acc[NT];
 #pragma unroll
     for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -790,19 +814,88 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
       }
       av[c] = *src(tn, c);
     }
-    const int64_t row = t * 16 + i;
     if (row < a.n) {
       uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
-        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + tt * 16 + 4 * g)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 v = make_float4(acc[tt][0] + bb.x, acc[tt][1] + bb.y, acc[tt][2] + bb.z,
-                               acc[tt][3] + bb.w);
-        if (a.add) {
-          const float4 ad = *reinterpret_cast<const float4*>(a.add + row * H + tt * 16 + 4 * g);
-          v.x += ad.x; v.y += ad.y; v.z += ad.z; v.w += ad.w;
+        float4 v = ep.sum(acc[tt], tt, a, g);
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
+        mbits |= relu_bits(v, 4 * tt);
+        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
+      }
+      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
+    }
+  }
+}
+
+// Forward v6 (persistent, same tiling and W image): v5's in-place reload of the next tile's X
+// chunk (one tile of X registers) with W fragments read per PAIR of column tiles right before
+// their MFMAs (8 VGPRs instead of v5's one-chunk-ahead copy of all NT, 4 NT) — the register room
+// that lets the added rows of the tile (ADD) be loaded ahead of the sweep at 4 waves per SIMD
+// (two blocks per CU at H = K = 128).  The pair's k-steps alternate between two accumulators,
+// so dependent MFMAs are two apart; the other waves of the SIMD cover the rest.
+template <int H, int K, bool ADD>
+__global__ void __launch_bounds__(512, K <= 128 ? 4 : 2) k_linear_fwd_v6(const LinArgs a, const ChunkTab tab,
+                                                          int64_t n_tiles) {
+  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
+  static_assert(NT % 2 == 0, "column tiles in pairs");
+  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
+  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
+    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
+    *reinterpret_cast<float4*>(ws + j * LDW + k) =
+        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  const int64_t last = a.n - 1;
+  auto src = [&](int64_t t, int c) {
+    const int64_t row = min<int64_t>(t * 16 + i, last);
+    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  float4 av[KC];
+  if (t < n_tiles) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
+  }
+  __syncthreads();
+  const int wl0 = i * LDW + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    const int64_t tn = t + nw < n_tiles ? t + nw : t;
+    int wo = wl0;
+    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
+    const float* wl = ws + wo;
+    const int64_t row = t * 16 + i;
+    Epi<NT, ADD> ep;
+    ep.load(a, row, H, g);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+#pragma unroll
+      for (int tt = 0; tt < NT; tt += 2) {
+        const float4 b0 = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + c * 16);
+        const float4 b1 = *reinterpret_cast<const float4*>(wl + (tt + 1) * 16 * LDW + c * 16);
+        acc[tt] = mfma4(b0.x, av[c].x, acc[tt]);
+        acc[tt + 1] = mfma4(b1.x, av[c].x, acc[tt + 1]);
+        acc[tt] = mfma4(b0.y, av[c].y, acc[tt]);
+        acc[tt + 1] = mfma4(b1.y, av[c].y, acc[tt + 1]);
+        acc[tt] = mfma4(b0.z, av[c].z, acc[tt]);
+        acc[tt + 1] = mfma4(b1.z, av[c].z, acc[tt + 1]);
+        acc[tt] = mfma4(b0.w, av[c].w, acc[tt]);
+        acc[tt + 1] = mfma4(b1.w, av[c].w, acc[tt + 1]);
+      }
+      av[c] = *src(tn, c);
+    }
+    if (row < a.n) {
+      uint32_t mbits = 0;
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        float4 v = ep.sum(acc[tt], tt, a, g);
         if (a.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
@@ -1491,11 +1584,15 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     // 5.12 vs 5.45 ms; H = 64, K = 128: 1.61 vs 1.65 ms at N = 1M)
     static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
     const int fwd_ver = fwd_env ? fwd_env : (h == 128 && a.k_total == 128 ? 5 : 4);
-#define HGNN_FWD4(HV, KV)                                                                        \
+#define HGNN_FWD4A(HV, KV, AV)                                                                   \
   if (fwd_ver == 4)                                                                              \
-    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV>), grid, block, 0, stream, a, tab, n_tiles);      \
+    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
+  else if (fwd_ver == 6)                                                                         \
+    hipLaunchKernelGGL((k_linear_fwd_v6<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
   else                                                                                           \
-    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV>), grid, block, 0, stream, a, tab, n_tiles);
+    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);
+#define HGNN_FWD4(HV, KV) \
+  if (add) { HGNN_FWD4A(HV, KV, true) } else { HGNN_FWD4A(HV, KV, false) }
     switch (h * 1000 + a.k_total) {
       case 64064: HGNN_FWD4(64, 64); break;
       case 64128: HGNN_FWD4(64, 128); break;
@@ -1505,6 +1602,7 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
       default: HGNN_FWD4(128, 256); break;
     }
 #undef HGNN_FWD4
+#undef HGNN_FWD4A
     return check_launch("k_linear_fwd_v4");
   }
   // v2 (W in LDS, A prefetched): 279 vs 321 us at N=1M, K=128, h=64 — the default when it fits

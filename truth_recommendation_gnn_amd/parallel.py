@@ -309,6 +309,30 @@ def user_range(n_users: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, min(n_users, lo + m)
 
 
+def shard_edge_filter(n_users: int, n_posts: int, world: int, rank: int,
+                      slice_inputs: bool = False):
+    """``keep(edge_type, src, dst) -> bool mask``: the edges rank ``rank`` of ``UserShard`` reads
+    (``synth.make_graph(keep=...)`` generates only those): edges into its users (post -> user,
+    user -> user), out of its users (user -> post; with ``slice_inputs`` also every edge into its
+    post slice), into its post slice (post -> post).  UserShard's own selection from these is the
+    one it makes from the global edges, in the same order, so the step is the same bit for bit
+    (tests/test_distributed.py)."""
+    lo, hi = user_range(n_users, world, rank)
+    S = -(-n_posts // world) if n_posts else 0
+    p_lo, p_hi = rank * S, rank * S + S
+
+    def keep(et, src, dst):
+        if (et[0], et[2]) == ("user", "post"):
+            m = (src >= lo) & (src < hi)
+            if slice_inputs:
+                m |= (dst >= p_lo) & (dst < p_hi)
+            return m
+        if et[2] == "user":
+            return (dst >= lo) & (dst < hi)
+        return (dst >= p_lo) & (dst < p_hi)
+    return keep
+
+
 class HipImpl:
     """The MI355X kernels behind the partitioned step."""
 
@@ -445,10 +469,14 @@ class UserShard:
       partial sums over the padded table, one reduce-scatter per relation gives the exact
       mean of the owned slice;
     * post->post: edges into owned post rows, sources from the full post table.
+
+    ``edges`` may also hold only this rank's share (``shard_edge_filter``) with the global
+    positive-edge count as ``num_edges_global``; ``pos_weights`` are then the shard edges'.
     """
 
     def __init__(self, edges, n_users: int, n_posts: int, env: DistEnv, impl=None,
-                 pos_weights: Optional[torch.Tensor] = None, slice_inputs: bool = False):
+                 pos_weights: Optional[torch.Tensor] = None, slice_inputs: bool = False,
+                 num_edges_global: Optional[int] = None):
         impl = impl or HipImpl()
         self.env, self.impl = env, impl
         self.slice_inputs = slice_inputs
@@ -479,7 +507,10 @@ class UserShard:
         for et, ei in edges.items():
             self.rels[et] = self._local_relation(et, ei, remote)
         if ENGAGES in edges:
-            self.num_edges_global = int(edges[ENGAGES].shape[1])
+            # (edges may be this rank's shard only — shard_edge_filter — with the global count
+            # given; the loss is normalised by it)
+            self.num_edges_global = (int(num_edges_global) if num_edges_global is not None
+                                     else int(edges[ENGAGES].shape[1]))
         self.cscale = None
         if pos_weights is not None:   # global mean of the interaction weights (static)
             if self.mask is None:

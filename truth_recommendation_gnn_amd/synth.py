@@ -120,13 +120,18 @@ def _features_np(rng: np.random.Generator, n: int, d: int) -> np.ndarray:
 
 
 def make_graph(cfg: GraphConfig | str, device: str | torch.device = "cpu",
-               device_gen: Optional[bool] = None) -> SynthGraph:
+               device_gen: Optional[bool] = None, keep=None) -> SynthGraph:
     """Build the seeded graph.  CPU generation is numpy PCG64 (bit-reproducible everywhere).
 
-    With a CUDA ``device`` and more than 50M edges (or ``device_gen=True``), generation runs on
-    the GPU with a seeded torch generator (reproducible on the same device type — every rank of a
-    multi-GPU run builds the identical global graph — not equal to the numpy stream); only
-    benches use that, parity tests stay on the numpy path.
+    With a CUDA ``device`` and more than 50M edges (or ``device_gen=True``), the edges come from
+    a counter-based generator (``_make_graph_counter``: edge e's endpoints are a hash of (seed,
+    e), generated in chunks on the device, the same values on any device) and the features from
+    a seeded torch generator (the same on every GPU): every rank of a multi-GPU run builds the
+    identical global graph.  ``keep(edge_type, src, dst) -> bool mask`` (optional) filters each
+    chunk as it is generated, so a rank can hold only its shard's edges
+    (``parallel.shard_edge_filter``) without the global edge list ever existing on it; the kept
+    edges keep their global order.  Only benches use this path; the parity tests' small graphs
+    stay on numpy.
     """
     if isinstance(cfg, str):
         cfg = CONFIGS[cfg]
@@ -134,8 +139,10 @@ def make_graph(cfg: GraphConfig | str, device: str | torch.device = "cpu",
     big = dev.type == "cuda" and (cfg.num_engages + cfg.num_social) > 50_000_000
     if device_gen is not None:
         big = device_gen and dev.type == "cuda"
-    if big:
-        return _make_graph_torch(cfg, dev)
+    if keep is not None and not big and dev.type == "cuda":
+        raise ValueError("make_graph(keep=...) filters the counter-based device generator")
+    if big or keep is not None:
+        return _make_graph_counter(cfg, dev, keep)
     U, P = cfg.num_users, cfg.num_posts
     g = np.random.Generator(np.random.PCG64(GRAPH_SEED))
     if cfg.num_engages == 0:       # one engager per post (build_graph.py:390-394)
@@ -167,31 +174,89 @@ def make_graph(cfg: GraphConfig | str, device: str | torch.device = "cpu",
     return sg.to(dev) if dev.type != "cpu" else sg
 
 
-def _make_graph_torch(cfg: GraphConfig, dev: torch.device) -> SynthGraph:
-    U, P = cfg.num_users, cfg.num_posts
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(GRAPH_SEED)
+# ----------------------------------------------------------------------------- counter-based
+_GOLDEN = 0x9E3779B97F4A7C15 - (1 << 64)          # as int64 (wrapping arithmetic)
+_M1 = 0xBF58476D1CE4E5B9 - (1 << 64)
+_M2 = 0x94D049BB133111EB - (1 << 64)
+GEN_CHUNK = 1 << 24                                 # edges generated per step
 
-    def zipf(n, size):
-        cdf = torch.from_numpy(_zipf_cdf(n, cfg.zipf_s)).to(dev)
-        r = torch.searchsorted(cdf, torch.rand(size, generator=gen, device=dev,
-                                                dtype=torch.float64), right=True)
-        r.clamp_(max=n - 1)
-        perm = torch.randperm(n, generator=gen, device=dev)
-        return perm[r]
+
+def _lsr(x: torch.Tensor, k: int) -> torch.Tensor:
+    """Logical right shift of int64 (torch's >> is arithmetic)."""
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def _hash64(stream: int, idx: torch.Tensor) -> torch.Tensor:
+    """splitmix64 of (stream seed + idx * golden ratio): the counter-based draw of csrc's
+    uniform_draw, in int64 torch ops (wrapping, bit-identical on CPU and GPU)."""
+    x = idx * _GOLDEN + stream
+    x = (x ^ _lsr(x, 30)) * _M1
+    x = (x ^ _lsr(x, 27)) * _M2
+    return x ^ _lsr(x, 31)
+
+
+def _uniform_int(stream: int, idx: torch.Tensor, n: int) -> torch.Tensor:
+    return (_lsr(_hash64(stream, idx), 32) * n) >> 32
+
+
+def _uniform01(stream: int, idx: torch.Tensor) -> torch.Tensor:
+    return _lsr(_hash64(stream, idx), 11).to(torch.float64) * (2.0 ** -53)
+
+
+def _stream(name: str) -> int:
+    """A fixed 63-bit seed per draw stream, derived from GRAPH_SEED."""
+    h = GRAPH_SEED * 0x100000001B3 + sum((i + 1) * 131 ** i * ord(c) for i, c in enumerate(name))
+    return h % (1 << 63)
+
+
+def _make_graph_counter(cfg: GraphConfig, dev: torch.device, keep=None) -> SynthGraph:
+    """Edges from counter-based draws (the distributions of the numpy path: uniform users,
+    Zipf-like (rank+1)^-s post / followee ids over a shuffled rank order), chunk by chunk, each
+    chunk filtered by ``keep``; features N(0,1) row-normalised from a seeded torch generator."""
+    U, P = cfg.num_users, cfg.num_posts
+
+    def perm(n, name):      # a random permutation of [0, n): argsort of hashed keys
+        return torch.argsort(_hash64(_stream(name), torch.arange(n, device=dev)))
+
+    cdf_cache = {}
+
+    def zipf(n, name, idx):
+        if n not in cdf_cache:
+            cdf_cache[n] = (torch.from_numpy(_zipf_cdf(n, cfg.zipf_s)).to(dev), perm(n, name + "/perm"))
+        cdf, pm = cdf_cache[n]
+        r = torch.searchsorted(cdf, _uniform01(_stream(name), idx), right=True).clamp_(max=n - 1)
+        return pm[r]
+
+    def relation(et, n_edges, src_fn, dst_fn):
+        parts = []
+        for e0 in range(0, n_edges, GEN_CHUNK):
+            idx = torch.arange(e0, min(e0 + GEN_CHUNK, n_edges), device=dev, dtype=torch.int64)
+            src, dst = src_fn(idx), dst_fn(idx)
+            if keep is not None:
+                m = keep(et, src, dst)
+                src, dst = src[m], dst[m]
+            parts.append(torch.stack([src, dst]))
+            del idx
+        if not parts:
+            return torch.empty(2, 0, dtype=torch.int64, device=dev)
+        return torch.cat(parts, dim=1) if len(parts) > 1 else parts[0]
 
     eid: Dict[EdgeType, torch.Tensor] = {}
-    eu = torch.randint(0, U, (cfg.num_engages,), generator=gen, device=dev)
-    ep = zipf(P, cfg.num_engages)
+    if cfg.num_engages == 0:
+        engage = relation(ENGAGES, P, lambda i: _uniform_int(_stream("eu"), i, U), lambda i: i)
+    else:
+        engage = relation(ENGAGES, cfg.num_engages, lambda i: _uniform_int(_stream("eu"), i, U),
+                          lambda i: zipf(P, "ep", i))
     if cfg.num_social:
-        fs = torch.randint(0, U, (cfg.num_social,), generator=gen, device=dev)
-        eid[SOCIAL] = torch.stack([fs, zipf(U, cfg.num_social)])
-    engage = torch.stack([eu, ep])
+        eid[SOCIAL] = relation(SOCIAL, cfg.num_social, lambda i: _uniform_int(_stream("fs"), i, U),
+                               lambda i: zipf(U, "ft", i))
     eid[ENGAGES] = engage
-    eid[REV_ENGAGES] = engage.flip(0)
+    eid[REV_ENGAGES] = engage.flip(0)           # train_gnn.py:142
     if cfg.num_post_post:
-        ps = torch.randint(0, P, (cfg.num_post_post,), generator=gen, device=dev)
-        eid[POST_POST] = torch.stack([ps, zipf(P, cfg.num_post_post)])
+        eid[POST_POST] = relation(POST_POST, cfg.num_post_post,
+                                  lambda i: _uniform_int(_stream("ps"), i, P),
+                                  lambda i: zipf(P, "pt", i))
+    gen = torch.Generator(device=dev)
     gen.manual_seed(FEAT_SEED)
 
     def feats(n):
