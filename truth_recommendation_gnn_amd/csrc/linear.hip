@@ -830,6 +830,95 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
   }
 }
 
+// Forward v7: v5 under LLVM's MFMA / LDS-read interleave strategy (__builtin_amdgcn_iglp_opt(0))
+// per chunk: the default schedule of v5 leaves back-to-back dependent MFMAs (40-cycle latency
+// against a 32-cycle issue) and LDS reads right before the MFMAs that consume them.
+// v5's description:
+// Forward v5 (persistent, same tiling and W image as v4), reorganised for 2 waves per SIMD (the
+// K = 256 W image takes 135 KB of LDS, so one 8-wave block per CU):
+//  * k-step-major over the NT accumulators: consecutive MFMAs are independent, so no MFMA waits
+//    on the 40-cycle dependent-accumulator latency (v4's 4-deep chains did, with LDS reads issued
+//    just before their use);
+//  * each W fragment of chunk c+1 is read from LDS right after its last use in chunk c, a whole
+//    k-sweep (NT MFMAs) ahead of its first use;
+//  * the next tile's X chunk c is loaded into av[c] as soon as chunk c has been consumed (no second
+//    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
+//    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
+//    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
+template <int H, int K, bool ADD>
+__global__ void __launch_bounds__(512, 2) k_linear_fwd_v7(const LinArgs a, const ChunkTab tab,
+                                                          int64_t n_tiles) {
+  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
+  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
+  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
+    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
+    *reinterpret_cast<float4*>(ws + j * LDW + k) =
+        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)gridDim.x * 8;
+  const int64_t last = a.n - 1;
+  auto src = [&](int64_t t, int c) {
+    const int64_t row = min<int64_t>(t * 16 + i, last);
+    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
+  };
+  int64_t t = (int64_t)blockIdx.x * 8 + wave;
+  float4 av[KC];
+  if (t < n_tiles) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
+  }
+  __syncthreads();
+  const int wl0 = i * LDW + 4 * g;
+  for (; t < n_tiles; t += nw) {
+    // the last tile of a wave re-loads itself (cached, never used) instead of branching
+    const int64_t tn = t + nw < n_tiles ? t + nw : t;
+    int wo = wl0;
+    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
+    const float* wl = ws + wo;
+    const int64_t row = t * 16 + i;
+    Epi<NT, ADD> ep;               // the added rows, in flight during the sweep (see v4)
+    ep.load(a, row, H, g);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float4 bw[NT];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW);
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].x, av[c].x, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].y, av[c].y, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].z, av[c].z, acc[tt]);
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        acc[tt] = mfma4(bw[tt].w, av[c].w, acc[tt]);
+        if (c + 1 < KC)
+          bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + (c + 1) * 16);
+      }
+      av[c] = *src(tn, c);
+      __builtin_amdgcn_iglp_opt(0);   // LLVM's MFMA / LDS-read interleave for small GEMMs
+    }
+    if (row < a.n) {
+      uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) {
+        float4 v = ep.sum(acc[tt], tt, a, g);
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        mbits |= relu_bits(v, 4 * tt);
+        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
+      }
+      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
+    }
+  }
+}
+
 // Forward v6 (persistent, same tiling and W image): v5's in-place reload of the next tile's X
 // chunk (one tile of X registers) with W fragments read per PAIR of column tiles right before
 // their MFMAs (8 VGPRs instead of v5's one-chunk-ahead copy of all NT, 4 NT) — the register room
@@ -1589,6 +1678,8 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
   else if (fwd_ver == 6)                                                                         \
     hipLaunchKernelGGL((k_linear_fwd_v6<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
+  else if (fwd_ver == 7)                                                                         \
+    hipLaunchKernelGGL((k_linear_fwd_v7<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
   else                                                                                           \
     hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);
 #define HGNN_FWD4(HV, KV) \
