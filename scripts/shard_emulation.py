@@ -73,6 +73,12 @@ class EmulEnv(parallel.DistEnv):
         out = own.repeat(self.world, *([1] * (own.dim() - 1)))
         return out, self._issued("all_gather", own.numel() * own.element_size() * (self.world - 1))
 
+    def broadcast_slices_async(self, own):
+        out = own.repeat(self.world, *([1] * (own.dim() - 1)))
+        nb = own.numel() * own.element_size()
+        return out, [parallel._Done() if q == self.rank else self._issued(f"broadcast[{q}]", nb)
+                     for q in range(self.world)]
+
     def all_to_all_async(self, inp, send_splits, recv_splits):
         out = inp.new_zeros((int(sum(recv_splits)),) + tuple(inp.shape[1:]))
         return out, self._issued("all_to_all", out.numel() * out.element_size())
@@ -85,6 +91,7 @@ class EmulEnv(parallel.DistEnv):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0, help="the rank whose share is emulated")
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--no-slice-inputs", action="store_true",
@@ -97,7 +104,7 @@ def main():
     g = synth.make_graph(gcfg, device=dev, device_gen=True)
     pos_g = g.edge_index_dict[synth.ENGAGES]
     pw_g = synth.interaction_weights(gcfg.num_posts).to(dev)[pos_g[1]]
-    env = EmulEnv(world=args.world, rank=0)
+    env = EmulEnv(world=args.world, rank=args.rank)
     shard = parallel.UserShard({et: g.edge_index_dict[et] for et, _ in RELATIONS},
                                gcfg.num_users, gcfg.num_posts, env, pos_weights=pw_g,
                                slice_inputs=not args.no_slice_inputs)
@@ -150,7 +157,8 @@ def main():
                       "cover_over_1link": None if cover is None else round(cover / t1, 2) if t1 else None,
                       "cover_over_7links": None if cover is None else round(cover / t7, 2) if t7 else None})
     env.log = None
-    print(json.dumps({"world": args.world, "rank": 0, "config": gcfg.name,
+    print(json.dumps({"world": args.world, "rank": args.rank, "config": gcfg.name,
+                      "chunked_last_gather": parallel.CHUNKED_LAST_GATHER,
                       "collectives": colls,
                       "scaling": "strong" if args.strong else "weak",
                       "users_own": shard.n_own, "posts_padded": shard.n_posts_pad,

@@ -135,7 +135,10 @@ class TorchImpl:
         return (dz.T @ x if need_w else None), (dz.sum(0) if need_b else None)
 
     def edge_bce_loss_raw(self, U, P, pos, neg, n_total, cscale, neg_order="edge", ready=None,
-                          on_dP=None):
+                          on_dP=None, p_chunks=None):
+        for _, _, rdy in (p_chunks or ()):
+            if rdy is not None:
+                rdy()
         if ready is not None:
             ready()
         U2, P2 = U.detach().requires_grad_(), P.detach().requires_grad_()

@@ -833,11 +833,29 @@ def negatives_in_user_order(csr: RelationCSR, neg_p: torch.Tensor) -> torch.Tens
     return neg_p.to(torch.int64)[csr.bwd.perm.long()].contiguous()
 
 
+def _row_range(grouped, lo: int, hi: int):
+    """Rows [lo, hi) of a grouping as a grouping of their own (rowptr slice with absolute offsets
+    into the shared col), with its own skew plan — built once and cached on the grouping."""
+    from .graph import GroupedEdges, _plan
+    cache = grouped.__dict__.setdefault("_ranges", {})
+    g = cache.get((lo, hi))
+    if g is None:
+        rp = grouped.rowptr[lo:hi + 1]
+        g = cache[(lo, hi)] = GroupedEdges(rp, grouped.col, None, _plan(rp, hi - lo,
+                                                                         grouped.plan.chunk),
+                                           hi - lo)
+    return g
+
+
 def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
-              ready=None, on_dP=None):
+              ready=None, on_dP=None, p_chunks=None):
     """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP).  ``on_dP(dP)``,
     if given, is called once dP's kernels are enqueued and before the scoring pass (dU, the loss)
-    is: the sharded step starts dP's reduce-scatter there, under the scoring pass."""
+    is: the sharded step starts dP's reduce-scatter there, under the scoring pass.
+    ``p_chunks`` (the sharded step): [(lo, hi, ready_fn)] — the post table arrives in row blocks
+    (parallel.DistEnv.broadcast_slices_async); dP's rows [lo, hi) need only those rows of P, so
+    the dP gather runs block by block as each lands (ready_fn: a stream wait), and the scoring
+    pass, which reads all of P, after the last."""
     U = _check_f32(U, "edge_bce_loss user_emb")
     P = _check_f32(P, "edge_bce_loss post_emb")
     draw = neg_u_order if isinstance(neg_u_order, NegativeDraw) else None
@@ -901,7 +919,7 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
                     "hgnn_sort_pairs_i64")
     if draw is not None and lanes.side is not None:
         lanes.main.wait_stream(lanes.side)    # the scoring pass reads the sort's `neg`
-    if ready is not None:
+    if ready is not None and p_chunks is None:
         # P is still arriving (parallel.py's all-gather of the post table): the sort above
         # needs only the edges, so it ran ahead; every kernel below reads P
         ready()
@@ -910,13 +928,23 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     with lanes.ctx(1):
         from .graph import NO_SPLIT, GroupedEdges, Plan
         negs = GroupedEdges(rowptr_n, nu_s, nu_s, Plan(NO_SPLIT, 0, 0, None, None), np_)
-        if _SCORE2:
+        if p_chunks is not None:
+            for lo, hi, rdy in p_chunks:
+                if rdy is not None:
+                    rdy()
+                if hi > lo:
+                    ng = GroupedEdges(rowptr_n[lo:hi + 1], nu_s, None,
+                                      Plan(NO_SPLIT, 0, 0, None, None), hi - lo)
+                    _score_gather2(U, P[lo:hi], _row_range(pf, lo, hi), ng, c, inv_e, dP[lo:hi])
+        elif _SCORE2:
             _score_gather2(U, P, pf, negs, c, inv_e, dP)
         else:
             _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
             _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
         if on_dP is not None:
             on_dP(dP)
+    if ready is not None and p_chunks is not None:
+        ready()                                 # all of P, for the scoring pass
     with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
         if neg32:
             N.check(lib.hgnn_edge_score_fwd_i32(
@@ -994,14 +1022,14 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
 
 def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
                       neg_p: torch.Tensor, n_edges_total: int, cscale: torch.Tensor,
-                      neg_order: str = "user", ready=None, on_dP=None):
+                      neg_order: str = "user", ready=None, on_dP=None, p_chunks=None):
     """:func:`edge_bce_loss` outside autograd: (loss, dL/dU, dL/dP) from the same kernels, for
-    callers that run their own backward schedule (``parallel.UserShard.step``; ``on_dP``: see
-    ``_edge_bce``)."""
+    callers that run their own backward schedule (``parallel.UserShard.step``; ``on_dP``,
+    ``p_chunks``: see ``_edge_bce``)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     neg_u = _negatives_user_order(csr, neg_p, neg_order)
     return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready,
-                     on_dP)
+                     on_dP, p_chunks)
 
 
 def _negatives_user_order(csr, neg_p, neg_order):

@@ -31,6 +31,7 @@ logic).
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -102,6 +103,26 @@ class DistEnv:
         dist.all_gather(list(full.chunk(self.world)), own, group=self.group)
         return full, _Done()
 
+    def broadcast_slices_async(self, own: torch.Tensor):
+        """The all-gather of ``own`` [S, ...] as one broadcast per source rank, each straight
+        into its row block of the full table (no copy back); returns (full [world*S, ...],
+        [work per source rank]).  A consumer that needs only some row blocks waits for those
+        (the loss's dP gather runs block by block as they land).  Every rank issues the
+        broadcasts in source-rank order."""
+        S = own.shape[0]
+        full = torch.empty((S * self.world,) + tuple(own.shape[1:]), dtype=own.dtype,
+                           device=own.device)
+        if not self._direct(own):
+            dist.all_gather(list(full.chunk(self.world)), own, group=self.group)
+            return full, [_Done() for _ in range(self.world)]
+        full[self.rank * S:(self.rank + 1) * S].copy_(own)
+        works = []
+        for q in range(self.world):
+            blk = full[q * S:(q + 1) * S]
+            w = dist.broadcast(blk, src=q, group=self.group, async_op=True)
+            works.append(_Done() if q == self.rank and w is None else _Held(w, own, full))
+        return full, works
+
     def all_to_all_async(self, inp: torch.Tensor, send_splits, recv_splits):
         """Rows ``inp[sum(send_splits[:q]) : ...]`` go to rank q; returns (received rows, in rank
         order, work).  Split lists are host ints (static per graph: no size exchange per call)."""
@@ -144,6 +165,25 @@ class _Held:
             self.work.wait()
         self.refs = None
         return True
+
+
+class _AllOf:
+    """Waits for every handle in a list (the per-source broadcasts of the post table)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        return True
+
+
+# The last forward gather of the post table (the loss's input) as per-source broadcasts whose
+# row blocks the loss's dP gather consumes as they land (DistEnv.broadcast_slices_async):
+# HGNN_CHUNKED_GATHER=1 one dP launch per block, 2 three launches (own block, the blocks below,
+# the blocks above), 0 one all-gather and one dP launch.
+CHUNKED_LAST_GATHER = int(os.environ.get("HGNN_CHUNKED_GATHER", "2"))
 
 
 class Pending:
@@ -845,7 +885,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             ag = None
         Wu_main = _without_block(Wu, col_pre) if jp is not None else Wu
         st = {"x_ext": None, "a_u": [], "add": None, "y_u": h_u, "a_p": [],
-              "y_p_own": h_p_own, "y_p": h_p, "m_u": None, "m_p": None}
+              "y_p_own": h_p_own, "y_p": h_p, "m_u": None, "m_p": None, "p_chunks": None}
 
         def user_gathers():
             # F4 user side (a pre-projected relation's mean of projected rows enters the epilogue)
@@ -895,7 +935,23 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     table = impl.linear_fwd_raw([y_p_own], block, None, False)
                     proj[nxt] = (block, (o, k))
             st["y_p_own"] = y_p_own
-            st["y_p"], ag = env.all_gather_async(table) if multi else (table, None)
+            if multi and nxt == L and CHUNKED_LAST_GATHER:
+                # the loss's post table: one broadcast per source rank, so the dP gather can run
+                # on each row block as it lands (own block first) instead of after all of them
+                st["y_p"], works = env.broadcast_slices_async(table)
+                S, r, W = shard.post_rows, env.rank, env.world
+                if CHUNKED_LAST_GATHER == 1:      # one dP launch per source block
+                    order = [r] + [q for q in range(W) if q != r]   # own, then as they land
+                    st["p_chunks"] = [(q * S, (q + 1) * S, None if q == r else works[q].wait)
+                                      for q in order]
+                else:                             # own block, blocks below it, blocks above it
+                    st["p_chunks"] = [(r * S, (r + 1) * S, None),
+                                      (0, r * S, works[r - 1].wait if r > 0 else None),
+                                      ((r + 1) * S, W * S, works[W - 1].wait if r + 1 < W
+                                       else None)]
+                ag = _AllOf(works)
+            else:
+                st["y_p"], ag = env.all_gather_async(table) if multi else (table, None)
 
         if multi and pm and not rs_issued:
             # no reduce-scatter to wait for (layer 1 with the static inputs held whole): the post
@@ -909,14 +965,17 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             # the last layer's user projection waits until the post table's all-gather is
             # issued: the loss needs that table at once, so the projection and the negatives
             # sort both run under the collective (the reduce-scatter still has the user-side
-            # gathers under it)
-            late_u = multi and bool(pm) and bool(um) and li == L - 1
+            # gathers under it).  With the chunked gather the loss's dP gather covers it, and the
+            # projection goes first, under the reduce-scatter.
+            late_u = (multi and bool(pm) and bool(um) and li == L - 1
+                      and not CHUNKED_LAST_GATHER)
             if not late_u:
                 user_projection()
             post_side()
             if late_u:
                 user_projection()
         x_ext, a_u, add, y_u = st["x_ext"], st["a_u"], st["add"], st["y_u"]
+        p_chunks = st["p_chunks"]
         a_p, y_p_own, y_p = st["a_p"], st["y_p_own"], st["y_p"]
         masks = (st["m_u"], st["m_p"])
         saved.append((convs, um, pm, h_u, h_p, h_p_own, x_ext, a_u, a_p, y_u, y_p_own, Wu_main,
@@ -936,7 +995,7 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
     loss, G_u, G_full = impl.edge_bce_loss_raw(h_u, h_p, shard.pos_local, neg_local,
                                                shard.num_edges_global, shard.cscale, neg_order,
                                                ag.wait if ag is not None else None,
-                                               on_dP=issue_b1)
+                                               on_dP=issue_b1, p_chunks=p_chunks)
     G_own = None
     R_proj = None                               # (block, cols, grads to finish) if R carries dP
     for li in reversed(range(L)):
