@@ -47,6 +47,17 @@ class MiniBatch:
     nodes: List[Dict[str, torch.Tensor]]   # nodes[0]: input nodes per type ... nodes[L]: seeds
     blocks: List[Block]                    # blocks[l]: nodes[l] -> nodes[l+1]
 
+    def record_stream(self, stream: torch.cuda.Stream) -> None:
+        """The batch was sampled on another stream and is consumed on ``stream``: keep its
+        device buffers from being reused by the sampling stream until ``stream`` is done."""
+        for nd in self.nodes:
+            for t in nd.values():
+                t.record_stream(stream)
+        for blk in self.blocks:
+            for c in blk.csr.values():
+                c.fwd.rowptr.record_stream(stream)
+                c.fwd.col.record_stream(stream)
+
 
 _MAX_GROUP = 8     # relations per hop / node types per relabel / relations per CSC group
 
