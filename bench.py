@@ -100,6 +100,8 @@ def parse(argv=None):
                    help="default: the box's allotted CPUs (OMP_NUM_THREADS / affinity)")
     p.add_argument("--cpu-sample-scale", type=float, default=None,
                    help="cfg5: the CPU baseline's down-scaled sample")
+    p.add_argument("--cpu-steps", type=int, default=3,
+                   help="timed CPU-baseline steps (median; after one warm-up)")
     p.add_argument("--cpu-shard", type=int, default=None,
                    help="full-batch configs: time rank 0's 1/S destination shard on the CPU oracle "
                         "(default: cfg4 64, cfg2/cfg3 1 = the whole graph)")
@@ -268,12 +270,16 @@ def cpu_baseline_shard(cfg, g, rels, threads=None, shard=None, steps=3, warmup=1
         opt.step()
 
     for _ in range(warmup):
+        t0 = time.perf_counter()
         step()
+        print(f"cpu_baseline: warm-up step {time.perf_counter() - t0:.1f} s", file=sys.stderr,
+              flush=True)
     times = []
     for _ in range(steps):
         t0 = time.perf_counter()
         step()
         times.append(time.perf_counter() - t0)
+        print(f"cpu_baseline: step {times[-1]:.1f} s", file=sys.stderr, flush=True)
     dt = statistics.median(times)
     edges = cfg.layers * (int(rev.shape[1]) + int(eng.shape[1]))
     total = cfg.layers * 2 * int(e.shape[1])
@@ -557,7 +563,8 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     cpu = None
     if not args.no_cpu_baseline and world == 1 and not on_cpu and not sharded:
         if set(et for et, _ in rels) == {synth.ENGAGES, synth.REV_ENGAGES}:
-            cpu = cpu_baseline_shard(cfg, g, rels, args.cpu_threads, args.cpu_shard)
+            cpu = cpu_baseline_shard(cfg, g, rels, args.cpu_threads, args.cpu_shard,
+                                     steps=args.cpu_steps)
         else:
             cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
     strong = world == 1 or not args.weak

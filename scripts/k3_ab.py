@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """K3 forward/backward A/B at one cfg4 shape (HIP events): the kernel version comes from the
-environment (HGNN_K3_FWD=4|5|6, HGNN_K3_DGRAD, HGNN_K3_WGRAD: read once per process), so run one
+environment (HGNN_K3_FWD=4..11, HGNN_K3_DGRAD, HGNN_K3_WGRAD: read once per process), so run one
 process per version.  python scripts/k3_ab.py --rows 9000000 --k 128 --h 128 [--add] [--bwd]"""
 import argparse
 import json
@@ -44,11 +44,18 @@ def main():
     add = torch.randn(n, h, device=dev, generator=g) if a.add else None
     mk = ops.relu_mask_for(n, h, True, dev)
     out = ops.linear_fwd(segs, w, b, True, add=add, mask_out=mk)
+    ref = torch.addmm(b, torch.cat(segs, 1), w.t())
+    if add is not None:
+        ref += add
+    ref.relu_()
+    err = float((out - ref).abs().max() / ref.abs().max())
+    del ref
     ms = timeit(lambda: ops.linear_fwd(segs, w, b, True, add=add, mask_out=mk), a.reps)
     fl = 2 * n * k * h
     rec = {"shape": f"{n}x{k}->{h}" + ("+add" if a.add else ""),
            "fwd_ver": os.environ.get("HGNN_K3_FWD", "default"), "fwd_ms": round(ms, 3),
-           "fwd_TFs": round(fl / ms / 1e9, 1), "fwd_frac_of_155": round(fl / ms / 1e9 / 155.1, 3)}
+           "fwd_TFs": round(fl / ms / 1e9, 1), "fwd_frac_of_155": round(fl / ms / 1e9 / 155.1, 3),
+           "max_rel_err_vs_torch": float(f"{err:.2e}")}
     if a.bwd:
         dout = torch.randn(n, h, device=dev, generator=g)
         dxs = [torch.empty_like(s) for s in segs]

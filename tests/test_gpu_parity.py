@@ -194,7 +194,7 @@ def test_gather_is_deterministic_bitwise():
                                   ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100),
                                   ([64], 128), ([32], 16), ([64, 32], 32), ([64, 64], 128),
                                   ([16, 48, 64], 64), ([32, 96], 64), ([48, 16], 128),
-                                  ([128, 128], 64), ([64, 64, 128], 128)])
+                                  ([128, 128], 64), ([64, 64, 128], 128), ([128], 128)])
 @pytest.mark.parametrize("n", [1, 37, 1000, 20000])
 def test_linear_fwd_bwd_matches_torch(ks, h, n):
     gen = torch.Generator().manual_seed(n + h)

@@ -645,6 +645,21 @@ __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1
   }
 }
 
+// Address of row `row`'s float4 at columns 16 c + 4 g .. +3 of the concatenated input.  S8: every
+// 8 consecutive chunks are one segment (segments 128 columns wide, as at cfg3/cfg4), so with c
+// unrolled the row offset is one multiply per segment and the chunks are immediates off it
+// (the general form keeps a 64-bit address per chunk live across the MFMA sweep).
+template <bool S8>
+__device__ __forceinline__ const float4* x_chunk(const ChunkTab& tab, int64_t row, int c, int g) {
+  if constexpr (S8) {
+    const int s = c & ~7;
+    return reinterpret_cast<const float4*>(tab.x[s] + row * tab.ld[s] + tab.col[s] +
+                                           (c & 7) * 16 + 4 * g);
+  } else {
+    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
+  }
+}
+
 // The added rows of one 16-row tile (hgnn_linear_fwd_add: a pre-projected relation's gathered
 // mean), loaded before the tile's MFMA sweep, which hides their HBM latency; read in the
 // epilogue they stalled every tile (K = 128 + add ran at 0.53 of the fp32 MFMA peak).  Lane
@@ -678,7 +693,7 @@ struct Epi {
 // the 4-deep dependent chains are already covered by 4 waves per SIMD — and a two-stage register
 // ping-pong instead of the copy, which spills: 193-200 us vs 202-205 and 227 at N=1M, K=128.)  Output tiles are computed transposed (out^T = W X^T) so every lane
 // stores one float4 per 16 output columns.
-template <int H, int K, bool ADD>
+template <int H, int K, bool ADD, bool S8 = false>
 __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 : 2))) k_linear_fwd_v4(const LinArgs a, const ChunkTab tab,
                                                        int64_t n_tiles) {
   constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
@@ -695,9 +710,7 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
     const int64_t row = t * 16 + i;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
-      v[c] = row < a.n ? *reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] +
-                                                          tab.col[c] + 4 * g)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[c] = row < a.n ? *x_chunk<S8>(tab, row, c, g) : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   int64_t t = (int64_t)blockIdx.x * 8 + wave;
   float4 av[KC], an[KC];
@@ -757,7 +770,7 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
 //    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
 //    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
 //    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
-template <int H, int K, bool ADD>
+template <int H, int K, bool ADD, bool S8 = false>
 __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const ChunkTab tab,
                                                           int64_t n_tiles) {
   constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
@@ -771,10 +784,7 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
   const int i = lane & 15, g = lane >> 4;
   const int64_t nw = (int64_t)gridDim.x * 8;
   const int64_t last = a.n - 1;
-  auto src = [&](int64_t t, int c) {
-    const int64_t row = min<int64_t>(t * 16 + i, last);
-    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
-  };
+  auto src = [&](int64_t t, int c) { return x_chunk<S8>(tab, min<int64_t>(t * 16 + i, last), c, g); };
   int64_t t = (int64_t)blockIdx.x * 8 + wave;
   float4 av[KC];
   if (t < n_tiles) {
@@ -816,172 +826,6 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
     }
     if (row < a.n) {
       uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        float4 v = ep.sum(acc[tt], tt, a, g);
-        if (a.relu) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        mbits |= relu_bits(v, 4 * tt);
-        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
-      }
-      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
-    }
-  }
-}
-
-// Forward v7: v5 under LLVM's MFMA / LDS-read interleave strategy (__builtin_amdgcn_iglp_opt(0))
-// per chunk: the default schedule of v5 leaves back-to-back dependent MFMAs (40-cycle latency
-// against a 32-cycle issue) and LDS reads right before the MFMAs that consume them.
-// v5's description:
-// Forward v5 (persistent, same tiling and W image as v4), reorganised for 2 waves per SIMD (the
-// K = 256 W image takes 135 KB of LDS, so one 8-wave block per CU):
-//  * k-step-major over the NT accumulators: consecutive MFMAs are independent, so no MFMA waits
-//    on the 40-cycle dependent-accumulator latency (v4's 4-deep chains did, with LDS reads issued
-//    just before their use);
-//  * each W fragment of chunk c+1 is read from LDS right after its last use in chunk c, a whole
-//    k-sweep (NT MFMAs) ahead of its first use;
-//  * the next tile's X chunk c is loaded into av[c] as soon as chunk c has been consumed (no second
-//    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
-//    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
-//    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
-template <int H, int K, bool ADD>
-__global__ void __launch_bounds__(512, 2) k_linear_fwd_v7(const LinArgs a, const ChunkTab tab,
-                                                          int64_t n_tiles) {
-  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
-  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
-  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
-    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
-    *reinterpret_cast<float4*>(ws + j * LDW + k) =
-        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t nw = (int64_t)gridDim.x * 8;
-  const int64_t last = a.n - 1;
-  auto src = [&](int64_t t, int c) {
-    const int64_t row = min<int64_t>(t * 16 + i, last);
-    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
-  };
-  int64_t t = (int64_t)blockIdx.x * 8 + wave;
-  float4 av[KC];
-  if (t < n_tiles) {
-#pragma unroll
-    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
-  }
-  __syncthreads();
-  const int wl0 = i * LDW + 4 * g;
-  for (; t < n_tiles; t += nw) {
-    // the last tile of a wave re-loads itself (cached, never used) instead of branching
-    const int64_t tn = t + nw < n_tiles ? t + nw : t;
-    int wo = wl0;
-    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
-    const float* wl = ws + wo;
-    const int64_t row = t * 16 + i;
-    Epi<NT, ADD> ep;               // the added rows, in flight during the sweep (see v4)
-    ep.load(a, row, H, g);
-    f32x4 acc[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 bw[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW);
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].x, av[c].x, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].y, av[c].y, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].z, av[c].z, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        acc[tt] = mfma4(bw[tt].w, av[c].w, acc[tt]);
-        if (c + 1 < KC)
-          bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + (c + 1) * 16);
-      }
-      av[c] = *src(tn, c);
-      __builtin_amdgcn_iglp_opt(0);   // LLVM's MFMA / LDS-read interleave for small GEMMs
-    }
-    if (row < a.n) {
-      uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        float4 v = ep.sum(acc[tt], tt, a, g);
-        if (a.relu) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        mbits |= relu_bits(v, 4 * tt);
-        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
-      }
-      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
-    }
-  }
-}
-
-// Forward v6 (persistent, same tiling and W image): v5's in-place reload of the next tile's X
-// chunk (one tile of X registers) with W fragments read per PAIR of column tiles right before
-// their MFMAs (8 VGPRs instead of v5's one-chunk-ahead copy of all NT, 4 NT) — the register room
-// that lets the added rows of the tile (ADD) be loaded ahead of the sweep at 4 waves per SIMD
-// (two blocks per CU at H = K = 128).  The pair's k-steps alternate between two accumulators,
-// so dependent MFMAs are two apart; the other waves of the SIMD cover the rest.
-template <int H, int K, bool ADD>
-__global__ void __launch_bounds__(512, K <= 128 ? 4 : 2) k_linear_fwd_v6(const LinArgs a, const ChunkTab tab,
-                                                          int64_t n_tiles) {
-  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
-  static_assert(NT % 2 == 0, "column tiles in pairs");
-  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
-  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
-    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
-    *reinterpret_cast<float4*>(ws + j * LDW + k) =
-        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t nw = (int64_t)gridDim.x * 8;
-  const int64_t last = a.n - 1;
-  auto src = [&](int64_t t, int c) {
-    const int64_t row = min<int64_t>(t * 16 + i, last);
-    return reinterpret_cast<const float4*>(tab.x[c] + row * tab.ld[c] + tab.col[c] + 4 * g);
-  };
-  int64_t t = (int64_t)blockIdx.x * 8 + wave;
-  float4 av[KC];
-  if (t < n_tiles) {
-#pragma unroll
-    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
-  }
-  __syncthreads();
-  const int wl0 = i * LDW + 4 * g;
-  for (; t < n_tiles; t += nw) {
-    const int64_t tn = t + nw < n_tiles ? t + nw : t;
-    int wo = wl0;
-    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
-    const float* wl = ws + wo;
-    const int64_t row = t * 16 + i;
-    Epi<NT, ADD> ep;
-    ep.load(a, row, H, g);
-    f32x4 acc[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-#pragma unroll
-      for (int tt = 0; tt < NT; tt += 2) {
-        const float4 b0 = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + c * 16);
-        const float4 b1 = *reinterpret_cast<const float4*>(wl + (tt + 1) * 16 * LDW + c * 16);
-        acc[tt] = mfma4(b0.x, av[c].x, acc[tt]);
-        acc[tt + 1] = mfma4(b1.x, av[c].x, acc[tt + 1]);
-        acc[tt] = mfma4(b0.y, av[c].y, acc[tt]);
-        acc[tt + 1] = mfma4(b1.y, av[c].y, acc[tt + 1]);
-        acc[tt] = mfma4(b0.z, av[c].z, acc[tt]);
-        acc[tt + 1] = mfma4(b1.z, av[c].z, acc[tt + 1]);
-        acc[tt] = mfma4(b0.w, av[c].w, acc[tt]);
-        acc[tt + 1] = mfma4(b1.w, av[c].w, acc[tt + 1]);
-      }
-      av[c] = *src(tn, c);
-    }
-    if (row < a.n) {
-      uint32_t mbits = 0;
 #pragma unroll
       for (int tt = 0; tt < NT; ++tt) {
         float4 v = ep.sum(acc[tt], tt, a, g);
@@ -1579,6 +1423,16 @@ static ChunkTab chunk_table(const LinArgs& a) {
   return t;
 }
 
+// every 8 consecutive 16-column chunks one 128-column segment (x_chunk<true>'s addressing)
+static bool chunks_in_segments_of_8(const ChunkTab& tab, int k_total) {
+  for (int c = 0; c < k_total / 16; ++c) {
+    const int s = c & ~7;
+    if (tab.x[c] != tab.x[s] || tab.ld[c] != tab.ld[s] || tab.col[c] != tab.col[s] + (c & 7) * 16)
+      return false;
+  }
+  return true;
+}
+
 static int fill_args(LinArgs& a, int32_t n_seg, const float* const* xs, const int32_t* ks,
                      float* const* dxs, int64_t n_rows, const float* w, int32_t h, bool* vec) {
   if (n_seg < 1 || n_seg > HGNN_MAX_SEG) return fail(HGNN_E_ARG, "linear: n_seg=%d", n_seg);
@@ -1670,18 +1524,23 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
                                                                       256 * per_cu))),
         block(512);
     // v5 measured faster only at H = K = 128 (2.87 vs 3.24 ms at N = 9M); v4 elsewhere (K = 256:
-    // 5.12 vs 5.45 ms; H = 64, K = 128: 1.61 vs 1.65 ms at N = 1M)
+    // 5.12 vs 5.45 ms; H = 64, K = 128: 1.61 vs 1.65 ms at N = 1M).  With the 128-column segment
+    // addressing (S8, round 3) v4 wins at every cfg3/cfg4 shape (N = 9M: K = 128 2.94 vs v5's
+    // 3.01-3.03 ms, + add 3.42-3.45 vs 3.44-3.46, K = 256 5.27-5.32 vs 5.32-5.36); v5 with S8
+    // crosses 128 VGPRs at K = 128 (3.27 ms), so S8 shapes take v4.
     static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
-    const int fwd_ver = fwd_env ? fwd_env : (h == 128 && a.k_total == 128 ? 5 : 4);
-#define HGNN_FWD4A(HV, KV, AV)                                                                   \
+    static const bool s8_env = !getenv("HGNN_K3_S8") || atoi(getenv("HGNN_K3_S8")) != 0;
+    const bool s8 = s8_env && h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
+    const int fwd_ver = fwd_env ? fwd_env : (!s8 && h == 128 && a.k_total == 128 ? 5 : 4);
+#define HGNN_FWD4S(HV, KV, AV, SV)                                                               \
   if (fwd_ver == 4)                                                                              \
-    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
-  else if (fwd_ver == 6)                                                                         \
-    hipLaunchKernelGGL((k_linear_fwd_v6<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
-  else if (fwd_ver == 7)                                                                         \
-    hipLaunchKernelGGL((k_linear_fwd_v7<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);  \
+    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV, SV>), grid, block, 0, stream, a, tab,        \
+                       n_tiles);                                                                 \
   else                                                                                           \
-    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV, AV>), grid, block, 0, stream, a, tab, n_tiles);
+    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV, AV, SV>), grid, block, 0, stream, a, tab,        \
+                       n_tiles);
+#define HGNN_FWD4A(HV, KV, AV) \
+  if (s8) { HGNN_FWD4S(HV, KV, AV, true) } else { HGNN_FWD4S(HV, KV, AV, false) }
 #define HGNN_FWD4(HV, KV) \
   if (add) { HGNN_FWD4A(HV, KV, true) } else { HGNN_FWD4A(HV, KV, false) }
     switch (h * 1000 + a.k_total) {
@@ -1694,6 +1553,7 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     }
 #undef HGNN_FWD4
 #undef HGNN_FWD4A
+#undef HGNN_FWD4S
     return check_launch("k_linear_fwd_v4");
   }
   // v2 (W in LDS, A prefetched): 279 vs 321 us at N=1M, K=128, h=64 — the default when it fits
