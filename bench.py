@@ -90,6 +90,10 @@ def parse(argv=None):
                    help="cfg5: the full-graph 4-relation step instead of the sampled mini-batches")
     p.add_argument("--batch-seeds", type=int, default=1024,
                    help="cfg5 mini-batch: seed users and seed posts per batch per rank")
+    p.add_argument("--no-graph", action="store_true",
+                   help="cfg5 mini-batch: run the step eagerly instead of replaying its HIP graph")
+    p.add_argument("--no-prefetch", action="store_true",
+                   help="cfg5 mini-batch: no side-stream sampling of the next batch")
     p.add_argument("--prefetch", action="store_true",
                    help="cfg5 mini-batch: sample the next batch on a side stream under this one")
     p.add_argument("--scale", type=float, default=1.0, help="shrink the config (debug only)")
@@ -671,7 +675,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     N ranks are data-parallel (each holds the graph, samples its own slice of the epoch's seed
     order; one RCCL all-reduce of the weight gradients per step).  Edges = the sampled message
     edges of every block and relation (what the gathers aggregate), summed over ranks."""
-    from truth_recommendation_gnn_amd import ops, sampler
+    from truth_recommendation_gnn_amd import minibatch, ops, sampler
     if dev.type == "cpu":
         raise SystemExit("the cfg5 mini-batch bench runs the HIP sampler: no CPU rehearsal")
     cfg = synth.CONFIGS["cfg5"] if args.scale == 1.0 else synth.scaled("cfg5", args.scale)
@@ -687,7 +691,10 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     if sharded:
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    # one rank: the step (forward, loss, backward, Adam) replayed as a HIP graph over
+    # static-capacity blocks (minibatch.py); the sampler stays eager (two syncs per hop)
+    use_graph = not args.no_graph and world == 1
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
     gen = torch.Generator(device=dev).manual_seed(0)
     # one shuffle per epoch, as a loader over the seed nodes does; batches are slices of it
     order = {"user": torch.randperm(cfg.num_users, device=dev, generator=gen),
@@ -698,9 +705,11 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     # the next batch is sampled on a side stream while this one's forward / backward runs: the
     # sampler's two host syncs per hop then wait for the sampling kernels only, not for the
     # previous step's GPU work queued ahead of them on one stream (a data loader's prefetch)
-    # (A/B on one box, round 3: 2.08 / 2.16 ms per step with it against 2.00 / 1.91 without — the
-    # step is bound by host issue, not by waits on the GPU — so it is off by default)
-    side = torch.cuda.Stream(dev) if args.prefetch else None
+    # Eager, A/B on one box (round 3): 2.08 / 2.16 ms per step with it against 2.00 / 1.91
+    # without — that step is bound by host issue, so it is off there.  Replaying the graph the
+    # host is free during the step: 1.04 ms with it, 1.29-1.32 without — on by default.
+    prefetch = args.prefetch or (use_graph and not args.no_prefetch)
+    side = torch.cuda.Stream(dev) if prefetch else None
 
     def sample(b):
         gb = (b % max(per_epoch, 1)) * world + rank            # this rank's slice of the order
@@ -715,7 +724,31 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
     nxt = [None]
 
-    def step():
+    def loss_of(out):
+        # link loss on (seed user i, seed post i) pairs against the next seed post as negative
+        u, p = out["user"], out["post"]
+        pos = (u * p).sum(1)
+        neg = (u * p.roll(1, 0)).sum(1)
+        return (torch.nn.functional.softplus(-pos).mean()
+                + torch.nn.functional.softplus(neg).mean())
+
+    captured = None
+    if use_graph:
+        # the capture's two warm-up passes are training steps on batch 0 (then recorded once)
+        captured = minibatch.CapturedStep(model, g.x_dict, s, {"user": nb, "post": nb}, loss_of,
+                                          opt)
+        captured.capture(sample(0)[0], warmup=2)
+
+    def eager(mb):
+        out = sampler.forward_blocks(model, mb, g.x_dict)
+        loss = loss_of(out)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        parallel.sync_grads(model, env)          # no-op at world size 1
+        opt.step()
+        return loss
+
+    def step(graph=True):
         mb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
         state["b"] += 1
         if ev is not None:
@@ -723,17 +756,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
             main.wait_event(ev)
             mb.record_stream(main)
         state["edges"] += sum(blk.csr[et].num_edges for blk in mb.blocks for et in blk.csr)
-        out = sampler.forward_blocks(model, mb, g.x_dict)
-        # link loss on (seed user i, seed post i) pairs against the next seed post as negative
-        u, p = out["user"], out["post"]
-        pos = (u * p).sum(1)
-        neg = (u * p.roll(1, 0)).sum(1)
-        loss = (torch.nn.functional.softplus(-pos).mean()
-                + torch.nn.functional.softplus(neg).mean())
-        opt.zero_grad(set_to_none=True)
-        loss.backward()
-        parallel.sync_grads(model, env)          # no-op at world size 1
-        opt.step()
+        loss = captured.step(mb) if (graph and captured is not None) else eager(mb)
         if side is not None:
             nxt[0] = sample(state["b"])          # under this step's GPU work
         return loss
@@ -750,9 +773,11 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     edges = float(edges)
     kern = {}
     if not args.profile_steps and args.timer_steps > 0:
+        # per-kernel events need the eager launches: the timer steps run the same kernels
+        # without the graph (on each batch's real sizes, not the static capacities)
         timer = ops.KernelTimer()
         ops.set_timer(timer)
-        clock.time(step, args.timer_steps)
+        clock.time(lambda: step(graph=False), args.timer_steps)
         ops.set_timer(None)
         kern = timer.summary()
     if rank != 0:
@@ -778,7 +803,10 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    "edges_per_step": round(edges / args.steps),
                    "global_batch": 2 * nb * world,
                    "batches_per_s": round(world * args.steps / elapsed, 1),
-                   "parallelism": f"data-parallel x{world}" if world > 1 else "single"},
+                   "parallelism": f"data-parallel x{world}" if world > 1 else "single",
+                   "execution": ("one HIP graph replay per step over static-capacity blocks "
+                                 "(sampler eager)" if captured is not None else "eager")
+                   + (", next batch sampled on a side stream" if side is not None else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),
         "cpu_baseline": cpu,
         "kernels": {k: {"launches": v["launches"],

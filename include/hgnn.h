@@ -373,6 +373,22 @@ int hgnn_relabel_multi(int32_t n_types, const int32_t* const* prefix, const int6
                        int32_t* local_out, int32_t* const* nodes_out, int32_t* d_count2,
                        int32_t check, void* ws, size_t ws_bytes, hgnn_stream_t stream);
 
+/* Static-capacity copies of sampled blocks (a captured mini-batch step replays one HIP graph over
+ * fixed buffers).  Item i (n_items <= 16): the CSR rowptr[i] (n_dst[i] + 1) / col[i] (e[i]) into
+ * rowptr_out[i] (d_cap[i] + 1) / col_out[i] (e_cap[i]); the e_cap - e padding entries get sources
+ * dummy[i] + (k mod spread[i]) (spread optional, >= 1: padded source rows taken in turn, so the
+ * transposed grouping has no long row) and are spread over the padded rows n_dst .. d_cap - 1
+ * (d_cap > n_dst required when
+ * e_cap > e), so the copy is a valid CSR of d_cap rows whose first n_dst rows are the input's.
+ * map[i] (optional): real entries become map[i][col] (a block's local ids -> global ids).
+ * d_cap[i] < 0: col only (a node-id list padded with dummy[i]).  Replaces nothing in the
+ * reference (which trains full-batch); it feeds forward_blocks' static form (minibatch.py). */
+int hgnn_pad_csr_multi(int32_t n_items, const int32_t* const* rowptr, const int32_t* const* col,
+                       const int32_t* const* map, const int64_t* n_dst, const int64_t* e,
+                       int32_t* const* rowptr_out, int32_t* const* col_out, const int64_t* d_cap,
+                       const int64_t* e_cap, const int32_t* dummy, const int32_t* spread,
+                       hgnn_stream_t stream);
+
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of
  * user and candidate embeddings, computed by the caller).  Per row:

@@ -87,5 +87,8 @@ def test_source_block_count_follows_the_table_size(monkeypatch):
     assert ops.gather_blocks(big) == 8
     assert ops.gather_blocks(torch.empty(1_000_000, 128, device="meta")) == 1   # 512 MB
     assert ops.gather_blocks(torch.empty(4_500_000, 128, device="meta")) == 4   # 2.3 GB
+    # cfg4's 200M-edge gather is blocked; a sampled block's 300k edges over the same table not
+    assert ops.gather_blocks(big, 200_000_000) == 8
+    assert ops.gather_blocks(big, 317_440) == 1
     monkeypatch.setattr(ops, "GATHER_BLOCK_BYTES", 0)
     assert ops.gather_blocks(big) == 1

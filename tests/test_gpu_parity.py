@@ -214,6 +214,27 @@ def test_linear_fwd_bwd_matches_torch(ks, h, n):
     close(db, ref_db)
 
 
+def test_linear_general_kernels_at_many_row_blocks():
+    """The general K3 kernels with 128-column tiles (>= 1024 workgroups: large N at shapes the
+    compile-time kernels do not cover); smaller grids take 32-column tiles (the test above)."""
+    n, ks, h = 140_000, [3, 5], 7
+    gen = torch.Generator().manual_seed(5)
+    segs = [torch.randn(n, k, generator=gen) for k in ks] + [torch.randn(n, 64, generator=gen)]
+    w = torch.randn(200, 72, generator=gen) * 0.2
+    b = torch.randn(200, generator=gen)
+    dout = torch.randn(n, 200, generator=gen)
+    dsegs = [s.to(DEV) for s in segs]
+    out = ops.linear_fwd(dsegs, w.to(DEV), b.to(DEV), relu=True)
+    close(out, torch.relu(torch.cat(segs, 1) @ w.T + b))
+    dxs = [torch.empty_like(s) for s in dsegs]
+    dw, db = ops.linear_bwd(dsegs, w.to(DEV), dout.to(DEV), out, dxs, True, True)
+    ref_dx, ref_dw, ref_db = _linear_bwd_ref(segs, w, dout, out)
+    for gx, r in zip(dxs, ref_dx):
+        close(gx, r)
+    close(dw, ref_dw)
+    close(db, ref_db)
+
+
 def _linear_bwd_ref(segs, w, dout, out_act):
     """float64 backward of relu(X W^T + b) given the kernel's forward output: the ReLU mask is
     taken from ``out_act`` itself, since a pre-activation within rounding of 0 may legitimately

@@ -1,0 +1,157 @@
+"""The captured mini-batch step (minibatch.py: static-capacity blocks replayed as one HIP graph)
+against the eager step on the same sampled batches (sampler.forward_blocks, itself checked
+against plain torch on the blocks in test_sampler.py): seed outputs, loss and every parameter
+gradient, then whole Adam training steps.  Plus the padding kernel's invariants."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _csr(rng, n_dst, n_src, max_deg):
+    deg = rng.integers(0, max_deg + 1, n_dst)
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    col = rng.integers(0, n_src, int(rowptr[-1])).astype(np.int32)
+    return torch.from_numpy(rowptr).to(DEV), torch.from_numpy(col).to(DEV)
+
+
+def test_pad_csr_multi_keeps_real_rows_and_spreads_padding():
+    from truth_recommendation_gnn_amd import _native as N
+    rng = np.random.default_rng(3)
+    items = []
+    for n_dst, n_src, max_deg, d_cap, e_cap, mapped in [(300, 50, 6, 340, 2000, False),
+                                                        (100, 70, 3, 101, 400, True),
+                                                        (0, 10, 0, 16, 64, False),
+                                                        (64, 64, 5, 64 + 1, 64 * 5, False)]:
+        rp, col = _csr(rng, n_dst, n_src, max_deg)
+        mp = torch.from_numpy(rng.permutation(10_000)[:n_src].astype(np.int32)).to(DEV) \
+            if mapped else None
+        items.append((rp, col, mp, n_dst, int(col.numel()), d_cap, e_cap, 7))
+    ids = torch.arange(5, 25, dtype=torch.int32, device=DEV)
+    outs = [(torch.full((it[5] + 1,), -9, dtype=torch.int32, device=DEV),
+             torch.full((it[6],), -9, dtype=torch.int32, device=DEV)) for it in items]
+    ids_out = torch.full((32,), -9, dtype=torch.int32, device=DEV)
+    n = len(items) + 1
+    N.check(N.lib().hgnn_pad_csr_multi(
+        n, N.ptr_array([it[0] for it in items] + [None]),
+        N.ptr_array([it[1] if it[4] else None for it in items] + [ids]),
+        N.ptr_array([it[2] for it in items] + [None]),
+        N.i64_array([it[3] for it in items] + [0]), N.i64_array([it[4] for it in items] + [20]),
+        N.ptr_array([o[0] for o in outs] + [None]), N.ptr_array([o[1] for o in outs] + [ids_out]),
+        N.i64_array([it[5] for it in items] + [-1]), N.i64_array([it[6] for it in items] + [32]),
+        N.int_array([it[7] for it in items] + [0]), N.int_array([1, 3, 1, 2, 1]),
+        N.stream_ptr(DEV)), "pad")
+    for (rp, col, mp, n_dst, E, d_cap, e_cap, dummy), (rpo, colo), spread in zip(items, outs,
+                                                                                 [1, 3, 1, 2]):
+        rpo, colo = rpo.cpu(), colo.cpu()
+        assert torch.equal(rpo[:n_dst + 1], rp.cpu())                 # real rows untouched
+        assert int(rpo[-1]) == e_cap and bool((rpo[1:] >= rpo[:-1]).all())
+        want = col.cpu().long() if mp is None else mp.cpu()[col.cpu().long()]
+        assert torch.equal(colo[:E].long(), want.long())
+        assert torch.equal(colo[E:].long(), dummy + torch.arange(e_cap - E) % spread)
+        lens = (rpo[n_dst + 1:] - rpo[n_dst:-1]).numpy()                 # padded rows balanced
+        assert lens.sum() == e_cap - E and lens.max() - lens.min() <= 1
+    assert ids_out[:20].tolist() == list(range(5, 25)) and ids_out[20:].eq(0).all()
+    # a batch larger than the capacity is refused, not written out of bounds
+    rp, col = _csr(rng, 10, 5, 4)
+    with pytest.raises(N.NativeError, match="capacity"):
+        N.check(N.lib().hgnn_pad_csr_multi(
+            1, N.ptr_array([rp]), N.ptr_array([col]), N.ptr_array([None]), N.i64_array([10]),
+            N.i64_array([int(col.numel())]), N.ptr_array([outs[0][0]]),
+            N.ptr_array([outs[0][1]]), N.i64_array([10]), N.i64_array([400]),
+            N.int_array([0]), None, N.stream_ptr(DEV)), "pad")
+
+
+def _setup(seed_n=24, fanouts=(5, 3)):
+    from truth_recommendation_gnn_amd import HeteroSAGE, sampler, synth
+    cfg = synth.dataclasses.replace(synth.scaled("cfg5", 0.0002), dim=16, hidden=16)
+    g = synth.make_graph(cfg, device=DEV)
+    rels = [(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0),
+            (synth.POST_POST, 0.5)]
+    num = {"user": cfg.num_users, "post": cfg.num_posts}
+    s = sampler.NeighborSampler(num, g.edge_index_dict, [et for et, _ in rels], list(fanouts))
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    order = {"user": torch.randperm(cfg.num_users, device=DEV, generator=gen),
+             "post": torch.randperm(cfg.num_posts, device=DEV, generator=gen)}
+
+    def batch(b):
+        return s.sample({t: o[b * seed_n:(b + 1) * seed_n] for t, o in order.items()}, seed=b)
+
+    def make_model():
+        torch.manual_seed(synth.WEIGHT_SEED)
+        return HeteroSAGE(cfg.hidden, rels, num_layers=2, in_channels=cfg.dim).to(DEV)
+
+    return g, s, batch, make_model, {"user": seed_n, "post": seed_n}
+
+
+def _loss(out):
+    u, p = out["user"], out["post"]
+    pos = (u * p).sum(1)
+    neg = (u * p.roll(1, 0)).sum(1)
+    return torch.nn.functional.softplus(-pos).mean() + torch.nn.functional.softplus(neg).mean()
+
+
+def _close(got, ref, what):
+    scale = float(ref.abs().max())
+    err = float((got - ref).abs().max()) / max(scale, 1e-30)
+    assert err < 1e-4, (what, err)
+
+
+def test_captured_step_matches_eager_blocks():
+    """Forward + loss + backward on static blocks, replayed for new batches, against the eager
+    block step on the same batches: seed outputs, loss and every gradient (rtol 1e-4 of each
+    tensor's max; the padded rows only change the order of fp32 sums in the weight gradients)."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, batch, make_model, n_seeds = _setup()
+    model = make_model()
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, _loss, None, slack=16)
+    step.capture(batch(0))
+    caps = step.blocks.cap
+    for b in (1, 2, 5):
+        mb = batch(b)
+        # the batch fits the static layout with room to spare (the slack rows stay padding)
+        for h, blk in enumerate(mb.blocks[::-1]):
+            for t, n in blk.n_dst.items():
+                assert n <= caps[h][t] - 16
+        loss = step.step(mb)
+        got_out = {t: v.detach().clone() for t, v in step.out.items()}
+        got_loss = float(loss)
+        got = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+        ref_model = make_model()
+        ref_model.load_state_dict(model.state_dict())
+        out = sampler.forward_blocks(ref_model, mb, g.x_dict)
+        ref_loss = _loss(out)
+        ref_loss.backward()
+        for t in out:
+            _close(got_out[t], out[t].detach(), f"out {t}")
+        assert abs(got_loss - float(ref_loss)) <= 1e-5 * abs(float(ref_loss)), (got_loss, ref_loss)
+        for n, p in ref_model.named_parameters():
+            _close(got[n], p.grad, n)
+
+
+def test_captured_adam_steps_match_eager_training():
+    """Whole training steps (forward, loss, backward, Adam) replayed from the graph against the
+    same steps run eagerly from the same initial weights: the capture's own warm-up steps (on
+    the first batch) and then one replay per batch."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, batch, make_model, n_seeds = _setup()
+    model, ref = make_model(), make_model()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=True)
+    ref_opt = torch.optim.Adam(ref.parameters(), lr=1e-3, fused=True)
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, _loss, opt, slack=16)
+    step.capture(batch(0), warmup=2)
+    for b in (0, 0):                                  # the eager twin of the warm-up steps
+        ref_opt.zero_grad(set_to_none=True)
+        _loss(sampler.forward_blocks(ref, batch(b), g.x_dict)).backward()
+        ref_opt.step()
+    for b in (1, 2, 3):
+        step.step(batch(b))
+        ref_opt.zero_grad(set_to_none=True)
+        _loss(sampler.forward_blocks(ref, batch(b), g.x_dict)).backward()
+        ref_opt.step()
+    torch.cuda.synchronize()
+    for (n, p), (_, r) in zip(model.named_parameters(), ref.named_parameters()):
+        _close(p.detach(), r.detach(), n)
+        assert not torch.equal(p.detach(), make_model().state_dict()[n])   # it trained

@@ -1576,7 +1576,13 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     return check_launch("k_linear_fwd_v2");
   }
 v1:
-  if (h <= 64) {
+  // few row blocks (a sampled block's 2k-32k destination rows at K = 384): 32-column tiles give
+  // 4x the workgroups (measured 47 us for 2048 rows on 16 workgroups of 128 columns)
+  if ((int64_t)gx * cdiv(h, 128) < 1024) {
+    const dim3 grid(gx, (unsigned)cdiv(h, 32));
+    if (vec) hipLaunchKernelGGL((k_linear_fwd<2, true>), grid, dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL((k_linear_fwd<2, false>), grid, dim3(256), 0, stream, a);
+  } else if (h <= 64) {
     const dim3 grid(gx, 1);
     if (vec) hipLaunchKernelGGL((k_linear_fwd<4, true>), grid, dim3(256), 0, stream, a);
     else hipLaunchKernelGGL((k_linear_fwd<4, false>), grid, dim3(256), 0, stream, a);
@@ -1807,9 +1813,16 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     return check_launch("k_wgrad_reduce");
   }
   if (any_dx) {
-    const dim3 grid((unsigned)cdiv(n_rows, kRowsPerBlock), (unsigned)cdiv(a.k_total, 128));
-    if (vec) hipLaunchKernelGGL((k_linear_dgrad<8, true>), grid, dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL((k_linear_dgrad<8, false>), grid, dim3(256), 0, stream, a);
+    const int64_t gxd = cdiv(n_rows, kRowsPerBlock);
+    if (gxd * cdiv(a.k_total, 128) < 1024) {   // few row blocks: 32-column tiles (see forward)
+      const dim3 grid((unsigned)gxd, (unsigned)cdiv(a.k_total, 32));
+      if (vec) hipLaunchKernelGGL((k_linear_dgrad<2, true>), grid, dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((k_linear_dgrad<2, false>), grid, dim3(256), 0, stream, a);
+    } else {
+      const dim3 grid((unsigned)gxd, (unsigned)cdiv(a.k_total, 128));
+      if (vec) hipLaunchKernelGGL((k_linear_dgrad<8, true>), grid, dim3(256), 0, stream, a);
+      else hipLaunchKernelGGL((k_linear_dgrad<8, false>), grid, dim3(256), 0, stream, a);
+    }
     if (int rc = check_launch("k_linear_dgrad")) return rc;
   }
   if (dw || db) {

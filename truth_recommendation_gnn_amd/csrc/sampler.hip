@@ -451,6 +451,87 @@ int hgnn_relabel_multi(int32_t n_types, const int32_t* const* prefix, const int6
                  d_count2, check != 0, ws, ws_bytes, as_stream(stream_));
 }
 
+
+// ------------------------------------------------------------ static-capacity blocks (graphs)
+// hgnn_pad_csr_multi: item i copies a sampled block relation's CSR (rowptr over n_dst rows,
+// col[E]) into capacity buffers of d_cap + 1 / e_cap entries.  The e_cap - E padding entries
+// point at sources dummy .. dummy + spread - 1 in turn (padded source rows: spread over many, so
+// the transposed grouping the backward builds has no long padded row — one source row holding
+// every padding entry made its K2 wave 0.5 ms) and are spread over the padded rows
+// n_dst .. d_cap - 1 (row n_dst + j
+// gets positions E + j (e_cap - E) / P .. E + (j + 1) (e_cap - E) / P, P = d_cap - n_dst), so the
+// result is a valid CSR of exactly d_cap rows and e_cap entries whose real rows are untouched and
+// no padded row is long.  With `map`, real entries become map[col] (local -> global ids).  An
+// item with d_cap < 0 copies (and maps) col only: a node-id list padded with `dummy`.
+constexpr int kPadMaxItems = 16;
+struct PadItems {
+  const int32_t* rowptr[kPadMaxItems];
+  const int32_t* col[kPadMaxItems];
+  const int32_t* map[kPadMaxItems];
+  int32_t* rowptr_out[kPadMaxItems];
+  int32_t* col_out[kPadMaxItems];
+  int64_t n_dst[kPadMaxItems], e[kPadMaxItems], d_cap[kPadMaxItems], e_cap[kPadMaxItems];
+  int32_t dummy[kPadMaxItems], spread[kPadMaxItems];
+};
+
+__global__ void __launch_bounds__(256) k_pad_csr(const PadItems a) {
+  const int it = blockIdx.y;
+  const int64_t n_dst = a.n_dst[it], E = a.e[it], D = a.d_cap[it], EC = a.e_cap[it];
+  const int64_t span = (D + 1 > EC ? D + 1 : EC);
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < span;
+       idx += (int64_t)gridDim.x * 256) {
+    if (D >= 0 && idx <= D)
+      a.rowptr_out[it][idx] = idx <= n_dst ? a.rowptr[it][idx]
+                                           : (int32_t)(E + (idx - n_dst) * (EC - E) / (D - n_dst));
+    if (idx < EC) {
+      int32_t v = a.dummy[it] + (int32_t)((idx - E) % a.spread[it]);
+      if (idx < E) {
+        v = a.col[it][idx];
+        if (a.map[it]) v = a.map[it][v];
+      }
+      a.col_out[it][idx] = v;
+    }
+  }
+}
+
+int hgnn_pad_csr_multi(int32_t n_items, const int32_t* const* rowptr, const int32_t* const* col,
+                       const int32_t* const* map, const int64_t* n_dst, const int64_t* e,
+                       int32_t* const* rowptr_out, int32_t* const* col_out, const int64_t* d_cap,
+                       const int64_t* e_cap, const int32_t* dummy, const int32_t* spread,
+                       hgnn_stream_t stream_) {
+  if (n_items < 1 || n_items > kPadMaxItems)
+    return fail(HGNN_E_ARG, "pad_csr_multi: n_items=%d (1..%d)", n_items, kPadMaxItems);
+  PadItems a{};
+  int64_t span = 1;
+  for (int i = 0; i < n_items; ++i) {
+    const bool csr = d_cap[i] >= 0;
+    if (e[i] < 0 || e[i] > e_cap[i] || (e[i] > 0 && !col[i]) || !col_out[i] ||
+        (csr && (n_dst[i] < 0 || n_dst[i] >= d_cap[i] || !rowptr[i] || !rowptr_out[i])) ||
+        (!csr && e_cap[i] < 1) || (csr && e_cap[i] > e[i] && d_cap[i] <= n_dst[i]) ||
+        e_cap[i] >= INT32_MAX || (spread && spread[i] < 1))
+      return fail(HGNN_E_ARG,
+                  "pad_csr_multi: item %d: n_dst=%lld E=%lld into capacity %lld rows / %lld "
+                  "entries (a sampled block larger than its static capacity, or no padded row)",
+                  i, (long long)n_dst[i], (long long)e[i], (long long)d_cap[i],
+                  (long long)e_cap[i]);
+    a.rowptr[i] = rowptr[i];
+    a.col[i] = col[i];
+    a.map[i] = map ? map[i] : nullptr;
+    a.rowptr_out[i] = rowptr_out[i];
+    a.col_out[i] = col_out[i];
+    a.n_dst[i] = n_dst[i];
+    a.e[i] = e[i];
+    a.d_cap[i] = d_cap[i];
+    a.e_cap[i] = e_cap[i];
+    a.dummy[i] = dummy[i];
+    a.spread[i] = spread ? spread[i] : 1;
+    span = std::max<int64_t>(span, std::max<int64_t>(d_cap[i] + 1, e_cap[i]));
+  }
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(span, 256), 1024);
+  hipLaunchKernelGGL(k_pad_csr, dim3(gx, (unsigned)n_items), dim3(256), 0, as_stream(stream_), a);
+  return check_launch("k_pad_csr");
+}
+
 }  // extern "C"
 
 static int relabel(int32_t T, const int32_t* const* prefix, const int64_t* n_prefix,

@@ -111,10 +111,15 @@ GATHER_BLOCK_BYTES = int(float(os.environ.get("HGNN_GATHER_BLOCK_GB", "2")) * 2*
 GATHER_BLOCK_SLICE = int(float(os.environ.get("HGNN_GATHER_BLOCK_MB", "600")) * 2**20)
 
 
-def gather_blocks(x: torch.Tensor) -> int:
-    """Number of source-block passes for a gather reading table ``x`` (1: one plain pass)."""
+def gather_blocks(x: torch.Tensor, n_edges: Optional[int] = None) -> int:
+    """Number of source-block passes for a gather reading table ``x`` (1: one plain pass).  A
+    gather of fewer edges than the table has rows (a sampled block reading the global tables)
+    reads a thin random subset at latency-bound rates, where the passes' locality buys nothing
+    and their (block, row) CSR would cost a sort per block: one pass."""
     nbytes = x.numel() * x.element_size()
     if GATHER_BLOCK_BYTES <= 0 or nbytes < GATHER_BLOCK_BYTES:
+        return 1
+    if n_edges is not None and n_edges < x.shape[0]:
         return 1
     return int(-(-nbytes // GATHER_BLOCK_SLICE))
 
@@ -149,7 +154,7 @@ def gather_mean(x_src: torch.Tensor, csr: RelationCSR,
     acc = out is not None
     if out is None:
         out = torch.empty(csr.n_dst, d, dtype=torch.float32, device=dev)
-    B = gather_blocks(x_src) if csr.num_edges else 1
+    B = gather_blocks(x_src, csr.num_edges) if csr.num_edges else 1
     if B > 1:
         passes, _ = csr.blocks("fwd", B)
         E = csr.num_edges
@@ -237,7 +242,7 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
     acc = out is not None
     if out is None:
         out = torch.empty(csr.n_src, d, dtype=torch.float32, device=dev)
-    B = gather_blocks(grad_aggr) if csr.num_edges else 1
+    B = gather_blocks(grad_aggr, csr.num_edges) if csr.num_edges else 1
     if B > 1:
         passes, w = csr.blocks("bwd", B)
         E = csr.num_edges
@@ -463,10 +468,19 @@ class DstGroup:
     # destinations = the first n_root rows of the dst type's table (a sampled block: the next
     # layer's nodes lead the current ones); None: the whole table
     n_root: Optional[int] = None
+    # the root segment is the whole input ``root_src`` instead (a block whose relations gather
+    # from the global tables: its destinations' own rows come as a separate input)
+    root_src: Optional[str] = None
+
+
+def _root_type(g: DstGroup) -> str:
+    return g.dst if g.root_src is None else g.root_src
 
 
 def _root(g: DstGroup, xs) -> torch.Tensor:
     """The destination rows' own features (the root segment): a prefix view in a block."""
+    if g.root_src is not None:
+        return xs[g.root_src]
     x = xs[g.dst]
     return x if g.n_root is None else x[:g.n_root]
 
@@ -474,10 +488,10 @@ def _root(g: DstGroup, xs) -> torch.Tensor:
 def _root_grad_buffer(g: DstGroup, xs, gx) -> torch.Tensor:
     """Allocates gx[dst] and returns the view the root segment's dgrad writes (a block's prefix;
     the rows after it are zero until the K2s add into them)."""
-    x = xs[g.dst]
-    if g.n_root is None:
-        gx[g.dst] = torch.empty_like(x)
-        return gx[g.dst]
+    x = xs[_root_type(g)]
+    if g.n_root is None or g.root_src is not None:
+        gx[_root_type(g)] = torch.empty_like(x)
+        return gx[_root_type(g)]
     gx[g.dst] = torch.zeros_like(x)
     return gx[g.dst][:g.n_root]
 
@@ -649,7 +663,7 @@ class _HeteroLayer(torch.autograd.Function):
             segs = list(aggrs)
             if g.root:
                 segs.append(_root(g, xs))
-                dxs.append(_root_grad_buffer(g, xs, gx) if need_x[g.dst] else None)
+                dxs.append(_root_grad_buffer(g, xs, gx) if need_x[_root_type(g)] else None)
             jobs.append((gi, g, segs, w, dout.contiguous(), dxs, need_w, need_b))
         lanes = _Lanes(saved[0].device, len(jobs))
         for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
@@ -788,7 +802,13 @@ def hetero_layer(spec: LayerSpec, x_dict: Dict[str, torch.Tensor],
     for t in flat[:len(spec.types)]:
         _check_f32(t, "node features")
     for g in spec.groups:
-        n = int(x_dict[g.dst].shape[0]) if g.n_root is None else int(g.n_root)
+        if g.root_src is not None:
+            if any(g.pre) or g.n_root is not None or not g.root:
+                raise ValueError("hetero_layer: root_src takes a root segment, no n_root and no "
+                                 "pre-projected relation")
+            n = int(x_dict[g.root_src].shape[0])
+        else:
+            n = int(x_dict[g.dst].shape[0]) if g.n_root is None else int(g.n_root)
         for src, csr in g.rels:
             if csr.n_dst != n or csr.n_src != int(x_dict[src].shape[0]):
                 raise ValueError(f"hetero_layer: relation {src}->{g.dst} is {csr.n_src}->"
@@ -1153,7 +1173,7 @@ def weighted_gather_raw(x_src: torch.Tensor, csr: RelationCSR, w_fwd: torch.Tens
     source-block passes scaled per row (see :func:`gather_blocks`)."""
     x_src = _check_f32(x_src, "weighted_gather")
     out = torch.empty(csr.n_dst, x_src.shape[1], dtype=torch.float32, device=x_src.device)
-    B = gather_blocks(x_src) if (row_w is not None and csr.num_edges) else 1
+    B = gather_blocks(x_src, csr.num_edges) if (row_w is not None and csr.num_edges) else 1
     if B > 1:
         passes, _ = csr.blocks("fwd", B)
         d, E = int(x_src.shape[1]), csr.num_edges
