@@ -155,3 +155,37 @@ def test_captured_adam_steps_match_eager_training():
     for (n, p), (_, r) in zip(model.named_parameters(), ref.named_parameters()):
         _close(p.detach(), r.detach(), n)
         assert not torch.equal(p.detach(), make_model().state_dict()[n])   # it trained
+
+
+@pytest.mark.parametrize("case", ["one_layer", "one_relation"])
+def test_captured_step_layouts(case):
+    """One layer (the outermost block is also the seeds' block), and a single relation (posts
+    have no incoming relation: their rows pass through as roots); plus the seed-count guard."""
+    from truth_recommendation_gnn_amd import HeteroSAGE, minibatch, sampler, synth
+    cfg = synth.dataclasses.replace(synth.scaled("cfg5", 0.0002), dim=16, hidden=16)
+    g = synth.make_graph(cfg, device=DEV)
+    rels = ([(synth.REV_ENGAGES, 1.0), (synth.SOCIAL, 0.75), (synth.ENGAGES, 1.0)]
+            if case == "one_layer" else [(synth.REV_ENGAGES, 1.0)])
+    layers, fanouts = (1, [6]) if case == "one_layer" else (2, [4, 2])
+    num = {"user": cfg.num_users, "post": cfg.num_posts}
+    s = sampler.NeighborSampler(num, g.edge_index_dict, [et for et, _ in rels], fanouts)
+    n = 20
+    seeds = lambda b: {"user": torch.arange(b * n, (b + 1) * n, device=DEV),   # noqa: E731
+                       "post": torch.arange(b * n, (b + 1) * n, device=DEV)}
+    torch.manual_seed(3)
+    model = HeteroSAGE(cfg.hidden, rels, num_layers=layers, in_channels=cfg.dim).to(DEV)
+    step = minibatch.CapturedStep(model, g.x_dict, s, {"user": n, "post": n}, _loss, None, slack=8)
+    step.capture(s.sample(seeds(0), seed=0))
+    mb = s.sample(seeds(3), seed=3)
+    got_loss = float(step.step(mb))
+    got = {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+    model.zero_grad(set_to_none=True)
+    ref = _loss(sampler.forward_blocks(model, mb, g.x_dict))
+    ref.backward()
+    assert abs(got_loss - float(ref)) <= 1e-5 * abs(float(ref))
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            _close(got[k], p.grad, k)
+    with pytest.raises(ValueError, match="seeds"):
+        step.step(s.sample({"user": torch.arange(n - 1, device=DEV),
+                            "post": torch.arange(n, device=DEV)}))

@@ -92,6 +92,11 @@ class StaticBlocks:
         """The batch's blocks into the fixed buffers: one launch, no sync."""
         if len(mb.blocks) != self.L:
             raise ValueError(f"{len(mb.blocks)} blocks for {self.L} static levels")
+        seeds = mb.nodes[-1]
+        if {t: int(v.numel()) for t, v in seeds.items()} != self.n_seeds:
+            # the loss reads the first n_seeds rows per type: a short batch would feed it padding
+            raise ValueError(f"batch seeds {({t: int(v.numel()) for t, v in seeds.items()})} "
+                             f"!= the captured {self.n_seeds}")
         L = self.L
         rp, col, mp, nd, e, rpo, colo, dcap, ecap, dummy, spread = ([] for _ in range(11))
         for h in range(L):
