@@ -238,7 +238,12 @@ class CapturedStep:
         self._zero_grad()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self.out, self.loss = self._body()
+            out, loss = self._body()
+        # the static outputs without the recorded autograd graph (kept alive, its AccumulateGrad
+        # nodes would tie later eager backwards of the same parameters to the capture stream)
+        self.out = {t: v.detach() for t, v in out.items()}
+        self.loss = loss.detach()
+        del out, loss
         self.graph = g
 
     def _zero_grad(self):
