@@ -28,7 +28,7 @@ barrier + device synchronise, with NO per-kernel events inside.  A second, separ
 of ``--timer-steps`` steps records HIP events around every kernel (on the stream it is launched
 on) for ``roofline`` — the dominant HBM kernel, the K1 forward gather over the largest source
 table: algorithmic bytes per launch / average launch time, ``traffic`` from the committed PMC
-passes of the same launch (``profiles/pmc_r2.json``) — and for ``projection`` (K3 vs the fp32
+passes of the same launch (the newest ``profiles/pmc_r*.json``) — and for ``projection`` (K3 vs the fp32
 MFMA peak).  ``cpu_baseline`` (rank 0, N=1 only): the plain-torch CPU oracle (PyG's op pattern)
 on the box's allotted host cores, median of 5 steps after 2 warm-ups, on a stated down-scaled
 sample of the same graph family (same degree distributions, so per-edge work is the same).
@@ -354,24 +354,33 @@ def _pg_options(args):
         return None
 
 
+def _pmc_file():
+    """The newest committed PMC summary (profiles/pmc_r<round>.json, scripts/pmc_r2.sh)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r[0-9]*.json")),
+                   key=lambda f: int("".join(ch for ch in os.path.basename(f) if ch.isdigit())))
+    return files[-1] if files else None
+
+
 def _pmc_traffic(cfg_name, world, kernel):
-    """Per-launch HBM bytes of ``kernel`` from the committed PMC passes (scripts/pmc_round.sh
-    -> profiles/pmc_r2.json), for the same config and world size; (None, None) if absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_r2.json")
-    if not os.path.exists(path):
+    """Per-launch HBM bytes of ``kernel`` from the committed PMC passes (scripts/pmc_r2.sh ->
+    profiles/pmc_r<round>.json), for the same config and world size; (None, None) if absent."""
+    path = _pmc_file()
+    if path is None:
         return None, None
     with open(path) as f:
         pm = json.load(f)
     rec = pm.get("launches", {}).get(f"{cfg_name}|n{world}|{kernel}")
     if not rec:
         return None, None
-    return rec.get("hbm_bytes_per_launch"), f"profiles/pmc_r2.json ({rec.get('source', '')})"
+    return (rec.get("hbm_bytes_per_launch"),
+            f"profiles/{os.path.basename(path)} ({rec.get('source', '')})")
 
 
 def _pmc_ratio(cfg_name, world, kernel):
-    """PMC HBM bytes / algorithmic bytes of ``kernel`` (profiles/pmc_r2.json), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_r2.json")
-    if not os.path.exists(path):
+    """PMC HBM bytes / algorithmic bytes of ``kernel`` (the newest profiles/pmc_r*.json)."""
+    path = _pmc_file()
+    if path is None:
         return None
     with open(path) as f:
         rec = json.load(f).get("launches", {}).get(f"{cfg_name}|n{world}|{kernel}")

@@ -256,11 +256,16 @@ def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
     return out
 
 
-def relu_mask_for(n: int, h: int, relu: bool, dev) -> Optional[torch.Tensor]:
+def relu_mask_for(n: int, h: int, relu: bool, dev, k: Optional[int] = None
+                  ) -> Optional[torch.Tensor]:
     """The bit form of a K3 output's ReLU mask (``hgnn_linear_fwd_mask``: 16 B per row, the
     backward reads it instead of the 4h-byte output), or None where the kernels have no bit form
-    (no ReLU, h not a multiple of 16 or above 128, or ``HGNN_RELU_BITS=0``)."""
+    (no ReLU, h not a multiple of 16 or above 128, or ``HGNN_RELU_BITS=0``) or where no kernel
+    would read it: an input width ``k`` outside the persistent kernels' {64, 128, 256} (the
+    general kernels read the output, and the bits would cost a separate launch)."""
     if not (RELU_BITS and relu and h % 16 == 0 and h <= 128):
+        return None
+    if k is not None and k not in (64, 128, 256):
         return None
     return torch.empty((n, 4), dtype=torch.int32, device=dev)
 
@@ -592,7 +597,8 @@ class _HeteroLayer(torch.autograd.Function):
                         else:
                             aggrs.append(gather_mean(xs[src], csr))
                     segs = aggrs + ([_root(g, xs)] if g.root else [])
-                    mk = relu_mask_for(_root(g, xs).shape[0], int(w.shape[0]), g.relu, dev)
+                    mk = relu_mask_for(_root(g, xs).shape[0], int(w.shape[0]), g.relu, dev,
+                                       sum(int(t.shape[1]) for t in segs))
                     y = linear_fwd(segs, _main_weight(g, w, cols),
                                    None if b is None else b.contiguous(), g.relu, add=add,
                                    mask_out=mk)
@@ -600,7 +606,8 @@ class _HeteroLayer(torch.autograd.Function):
                 else:
                     aggrs = [gather_mean(xs[src], csr) for src, csr in g.rels]
                     segs = aggrs + ([_root(g, xs)] if g.root else [])
-                    mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev)
+                    mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev,
+                                       sum(int(t.shape[1]) for t in segs))
                     y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
                                    g.relu, mask_out=mk)
             lanes.escape(gi, y, mk, *aggrs)
