@@ -90,6 +90,8 @@ def parse(argv=None):
                    help="cfg5: the full-graph 4-relation step instead of the sampled mini-batches")
     p.add_argument("--batch-seeds", type=int, default=1024,
                    help="cfg5 mini-batch: seed users and seed posts per batch per rank")
+    p.add_argument("--torch-loss", action="store_true",
+                   help="cfg5 mini-batch: the link loss as torch ops instead of the fused kernels")
     p.add_argument("--no-graph", action="store_true",
                    help="cfg5 mini-batch: run the step eagerly instead of replaying its HIP graph")
     p.add_argument("--no-prefetch", action="store_true",
@@ -733,13 +735,23 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
     nxt = [None]
 
+    # link loss on the (seed user i, seed post i) pairs with seed post i - 1 as the negative:
+    # the reference's loss (train_gnn.py:259-281, BCE-with-logits means, unit edge weights) through
+    # the library's fused loss kernels (a dozen launches where the torch expression took ~25)
+    pairs = torch.arange(nb, device=dev)
+    pos_pairs = torch.stack([pairs, pairs])
+    neg_pairs = ((pairs - 1) % nb).to(torch.int32)
+    one = torch.ones((), device=dev)
+
     def loss_of(out):
-        # link loss on (seed user i, seed post i) pairs against the next seed post as negative
-        u, p = out["user"], out["post"]
-        pos = (u * p).sum(1)
-        neg = (u * p.roll(1, 0)).sum(1)
-        return (torch.nn.functional.softplus(-pos).mean()
-                + torch.nn.functional.softplus(neg).mean())
+        if args.torch_loss:
+            u, p = out["user"], out["post"]
+            pos = (u * p).sum(1)
+            neg = (u * p.roll(1, 0)).sum(1)
+            return (torch.nn.functional.softplus(-pos).mean()
+                    + torch.nn.functional.softplus(neg).mean())
+        return ops.edge_bce_loss(out["user"], out["post"], pos_pairs, neg_pairs, None,
+                                 neg_order="user", check=False, cscale=one)
 
     captured = None
     if use_graph:
