@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--segs", type=int, default=1, help="input split into this many segments")
     ap.add_argument("--add", action="store_true")
     ap.add_argument("--bwd", action="store_true")
+    ap.add_argument("--no-mask", action="store_true", help="no ReLU bit mask output")
     ap.add_argument("--reps", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda")
@@ -42,7 +43,7 @@ def main():
     w = torch.randn(h, k, device=dev, generator=g) * 0.1
     b = torch.randn(h, device=dev, generator=g)
     add = torch.randn(n, h, device=dev, generator=g) if a.add else None
-    mk = ops.relu_mask_for(n, h, True, dev)
+    mk = None if a.no_mask else ops.relu_mask_for(n, h, True, dev)
     out = ops.linear_fwd(segs, w, b, True, add=add, mask_out=mk)
     ref = torch.addmm(b, torch.cat(segs, 1), w.t())
     if add is not None:

@@ -13,6 +13,8 @@
 // contiguous 16-B loads (the k order inside a chunk is permuted, which only moves rounding).
 #include "hgnn_common.h"
 
+#include <hip/hip_bf16.h>
+
 #include <algorithm>
 #include <stdlib.h>
 
@@ -840,6 +842,160 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
   }
 }
 
+// ================================================================ bf16x6: fp32-exact split
+// gfx950 runs bf16 MFMA at 16x the fp32 MFMA rate (2.5 PF vs 157 TF dense).  Every fp32 value
+// v splits exactly-enough into three bf16 pieces, v1 = bf16(v), v2 = bf16(v - v1),
+// v3 = bf16(v - v1 - v2) (|v - v1 - v2 - v3| <= ~2^-24 |v|), and a product x w becomes the six
+// piece products whose orders add to <= 4: x1w1 | x1w2 + x2w1 + x1w3 + x3w1 + x2w2 (the dropped
+// x2w3, x3w2, x3w3 are <= ~2^-24 |x w|).  Each piece product is exact in f32 and accumulates in
+// f32, so the result has fp32 accuracy: measured at most 0.68 f32 ulp of sum |x w| against
+// double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
+// accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
+// 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ unsigned short x6_bf16(float f) {
+  return __bfloat16_as_ushort(__float2bfloat16(f));   // round to nearest even (v_cvt_pk_bf16_f32)
+}
+__device__ __forceinline__ float x6_f32(unsigned short b) {
+  return __uint_as_float(((unsigned)b) << 16);
+}
+__device__ __forceinline__ void x6_split8(const float4& u, const float4& v, bf16x8_t& p1,
+                                          bf16x8_t& p2, bf16x8_t& p3) {
+  const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned short a1 = x6_bf16(f[j]);
+    const float r1 = f[j] - x6_f32(a1);
+    const unsigned short a2 = x6_bf16(r1);
+    p1[j] = (short)a1;
+    p2[j] = (short)a2;
+    p3[j] = (short)x6_bf16(r1 - x6_f32(a2));
+  }
+}
+// acc_hi += w1 x1; acc_lo += w2 x2 + w3 x1 + w1 x3 + w2 x1 + w1 x2 (small terms first)
+__device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x1,
+                                       const bf16x8_t& x2, const bf16x8_t& x3, f32x4& hi,
+                                       f32x4& lo) {
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x2, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], x1, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x3, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x1, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x2, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x1, hi, 0, 0, 0);
+}
+
+// Forward on the split: persistent, one 8-wave block per CU.  The block's HB output columns of
+// W (HB = 128, or 64 for K = 256, whose three planes for all 128 columns would not fit in LDS:
+// then two blocks take the two column halves of the same tiles, in step, so the second read of
+// a tile's rows mostly hits the caches) are split once into three bf16 planes in LDS; each wave
+// streams 16-row tiles.  Lane (i, g) loads row i's columns 32 s + 8 g .. +7 for k-step s, splits
+// them in registers and re-loads the slot with the next tile's as soon as it is split.  MFMA
+// operands: A = the W planes (rows = output columns), B = X^T, so the lane ends with columns
+// 16 c + 4 g .. +3 of row i: the v4/v5 layout (float4 stores, the same ReLU mask words).
+template <int K, int HB, bool ADD, bool S8>
+__global__ void __launch_bounds__(512, 1) k_linear_fwd_x6(const LinArgs a, const ChunkTab tab,
+                                                          int64_t n_tiles) {
+  constexpr int NT = HB / 16, KS = K / 32, LDB = K + 8, NH = 128 / HB;
+  __shared__ __attribute__((aligned(16))) unsigned short wp[3][HB * LDB];
+  // NH = 2: blocks b and b + 8 (the same XCD: hardware block b runs on XCD b % 8) take the two
+  // column halves of one tile stream, so the second read of a tile's rows can hit that L2
+  const int hb = NH == 1 ? 0 : (int)((blockIdx.x >> 3) & 1), col0 = hb * HB;
+  const int64_t stream_id = NH == 1 ? blockIdx.x : (blockIdx.x & 7) + 8 * (blockIdx.x >> 4);
+  for (int idx = threadIdx.x; idx < HB * K; idx += 512) {
+    const int j = idx / K, k = idx % K;
+    const float v = a.w[(int64_t)(col0 + j) * K + k];
+    const unsigned short a1 = x6_bf16(v);
+    const float r1 = v - x6_f32(a1);
+    const unsigned short a2 = x6_bf16(r1);
+    wp[0][j * LDB + k] = a1;
+    wp[1][j * LDB + k] = a2;
+    wp[2][j * LDB + k] = x6_bf16(r1 - x6_f32(a2));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)(gridDim.x / NH) * 8;
+  const int64_t last = a.n - 1;
+  int64_t t = stream_id * 8 + wave;
+  float4 xv[KS][2];
+  auto load_s = [&](int64_t tt, int s) {
+    const float4* p = x_chunk<S8>(tab, min<int64_t>(tt * 16 + i, last), 2 * s + (g >> 1), 0) +
+                      2 * (g & 1);
+    xv[s][0] = p[0];
+    xv[s][1] = p[1];
+  };
+  if (t < n_tiles) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) load_s(t, s);
+  }
+  __syncthreads();
+  for (; t < n_tiles; t += nw) {
+    const int64_t tn = t + nw < n_tiles ? t + nw : t;
+    const int64_t row = t * 16 + i;
+    int wo = i * LDB + 8 * g;
+    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
+    float4 ad[ADD ? NT : 1];       // the added rows, in flight during the sweep (see Epi)
+    if constexpr (ADD) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+        ad[c] = row < a.n ? *reinterpret_cast<const float4*>(a.add + row * 128 + col0 + 16 * c +
+                                                             4 * g)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    f32x4 hi[NT], lo[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) hi[c] = lo[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t cw[3], nx[3];
+    auto rd = [&](int s, int c, bf16x8_t (&f)[3]) {
+      const int off = wo + 16 * c * LDB + 32 * s;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8_t*>(&wp[q][off]);
+    };
+    rd(0, 0, cw);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8_t x1, x2, x3;
+      x6_split8(xv[s][0], xv[s][1], x1, x2, x3);
+      load_s(tn, s);   // the next tile's k-step s, a whole tile of MFMAs ahead of its use
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        if (c + 1 < NT) rd(s, c + 1, nx);
+        else if (s + 1 < KS) rd(s + 1, 0, nx);
+        x6_mma(cw, x1, x2, x3, hi[c], lo[c]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cw[q] = nx[q];
+      }
+    }
+    if (row < a.n) {
+      uint32_t mbits = 0;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + col0 + 16 * c + 4 * g)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = make_float4((hi[c][0] + lo[c][0]) + bb.x, (hi[c][1] + lo[c][1]) + bb.y,
+                               (hi[c][2] + lo[c][2]) + bb.z, (hi[c][3] + lo[c][3]) + bb.w);
+        if constexpr (ADD) {
+          v.x += ad[c].x; v.y += ad[c].y; v.z += ad[c].z; v.w += ad[c].w;
+        }
+        if (a.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        mbits |= relu_bits(v, 4 * c);
+        *reinterpret_cast<float4*>(a.out + row * 128 + col0 + 16 * c + 4 * g) = v;
+      }
+      if (a.mask_out) {
+        // word row * 4 + g holds bit 4 c + e of column tile c (0..7); a column half owns its
+        // 16-bit half of it (no two blocks write the same bytes)
+        if constexpr (NH == 1)
+          a.mask_out[row * 4 + g] = mbits;
+        else
+          reinterpret_cast<unsigned short*>(a.mask_out)[(row * 4 + g) * 2 + hb] =
+              (unsigned short)mbits;
+      }
+    }
+  }
+}
+
 // Backward v4: two roles per SIMD.  512 threads; waves 0-3 ("dz waves") load the masked dz
 // fragments of 16 rows each, run dgrad (dX^T = W^T dz^T, straight from registers) and the bias
 // sums, and publish dz to LDS; waves 4-7 ("X waves") stage the X tile and run wgrad.  dz / X
@@ -1531,6 +1687,29 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
     static const bool s8_env = !getenv("HGNN_K3_S8") || atoi(getenv("HGNN_K3_S8")) != 0;
     const bool s8 = s8_env && h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
+    // the fp32-exact bf16x6 split (k_linear_fwd_x6) at H = 128, K = 128 / 256: default
+    // (HGNN_K3_X6=0: the f32-input MFMA kernels below)
+    static const bool x6_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
+    if (x6_env && h == 128 && (a.k_total == 128 || a.k_total == 256)) {
+      int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
+                                                               a.k_total == 128 ? 256 : 128));
+      if (a.k_total != 128) streams = cdiv(streams, 8) * 8;   // column-half pairs b, b + 8
+#define HGNN_FWDX6(KV, HBV, AV)                                                                  \
+  {                                                                                              \
+    const dim3 gx6((unsigned)(streams * (128 / HBV)));                                           \
+    if (s8) hipLaunchKernelGGL((k_linear_fwd_x6<KV, HBV, AV, true>), gx6, block, 0, stream, a,   \
+                               tab, n_tiles);                                                    \
+    else hipLaunchKernelGGL((k_linear_fwd_x6<KV, HBV, AV, false>), gx6, block, 0, stream, a,     \
+                            tab, n_tiles);                                                       \
+  }
+      if (a.k_total == 128) {
+        if (add) HGNN_FWDX6(128, 128, true) else HGNN_FWDX6(128, 128, false)
+      } else {
+        if (add) HGNN_FWDX6(256, 64, true) else HGNN_FWDX6(256, 64, false)
+      }
+#undef HGNN_FWDX6
+      return check_launch("k_linear_fwd_x6");
+    }
     const int fwd_ver = fwd_env ? fwd_env : (!s8 && h == 128 && a.k_total == 128 ? 5 : 4);
 #define HGNN_FWD4S(HV, KV, AV, SV)                                                               \
   if (fwd_ver == 4)                                                                              \
