@@ -1438,6 +1438,118 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
   }
 }
 
+// dgrad on the bf16x6 split (H = 128): dX = dz W, out^T = W^T dz^T.  The block's KB output
+// columns of W^T (KB = 128, or 64 for K = 256: two blocks b, b + 8 take the two halves of one tile
+// stream, as the forward) are split once into three bf16 planes in LDS; lane (i, g) loads row i's
+// dout at h = 32 s + 8 g .. +7, masks it (ReLU bits: words row * 4 + 2 (g & 1) and + 1, or the
+// forward output), writes the masked dz once when asked (column half 0), splits it and re-loads
+// the slot with the next tile's.  The lane ends with dX[row i][16 c + 4 g .. +3]: store_dx4
+// through the segment table (stored, or added where dx_acc says).
+template <int K, int KB>
+__global__ void __launch_bounds__(512, 1) k_linear_dgrad_x6(const LinArgs a, const ChunkTab tab,
+                                                            int64_t n_tiles) {
+  constexpr int H = 128, NT = KB / 16, HS = H / 32, LDB = H + 8, NH = K / KB;
+  __shared__ __attribute__((aligned(16))) unsigned short wp[3][KB * LDB];
+  const int hb = NH == 1 ? 0 : (int)((blockIdx.x >> 3) & 1), col0 = hb * KB;
+  const int64_t stream_id = NH == 1 ? blockIdx.x : (blockIdx.x & 7) + 8 * (blockIdx.x >> 4);
+  for (int idx = threadIdx.x; idx < H * KB; idx += 512) {
+    const int j = idx / KB, kk = idx % KB;      // W[j][col0 + kk] -> W^T row kk, column j
+    const float v = a.w[(int64_t)j * K + col0 + kk];
+    const unsigned short a1 = x6_bf16(v);
+    const float r1 = v - x6_f32(a1);
+    const unsigned short a2 = x6_bf16(r1);
+    wp[0][kk * LDB + j] = a1;
+    wp[1][kk * LDB + j] = a2;
+    wp[2][kk * LDB + j] = x6_bf16(r1 - x6_f32(a2));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int64_t nw = (int64_t)(gridDim.x / NH) * 8;
+  const int64_t last = a.n - 1;
+  const bool bits = a.mask_in != nullptr;
+  const bool masked = !bits && a.out_act != nullptr;
+  int64_t t = stream_id * 8 + wave;
+  float4 zv[HS][2], mv[HS][2];
+  uint2 mw = make_uint2(0u, 0u);
+  auto load_s = [&](int64_t tt, int s) {
+    const int64_t row = min<int64_t>(tt * 16 + i, last);
+    const float4* p = reinterpret_cast<const float4*>(a.dout + row * H + 32 * s + 8 * g);
+    zv[s][0] = p[0];
+    zv[s][1] = p[1];
+    if (masked) {
+      const float4* q = reinterpret_cast<const float4*>(a.out_act + row * H + 32 * s + 8 * g);
+      mv[s][0] = q[0];
+      mv[s][1] = q[1];
+    }
+    if (bits && s == 0) mw = *reinterpret_cast<const uint2*>(a.mask_in + row * 4 + 2 * (g & 1));
+  };
+  if (t < n_tiles) {
+#pragma unroll
+    for (int s = 0; s < HS; ++s) load_s(t, s);
+  }
+  __syncthreads();
+  for (; t < n_tiles; t += nw) {
+    const int64_t tn = t + nw < n_tiles ? t + nw : t;
+    const int64_t row = t * 16 + i;
+    int wo = i * LDB + 8 * g;
+    asm volatile("" : "+v"(wo));   // W^T fragments stay per-tile LDS reads (see fwd v4)
+    f32x4 hi[NT], lo[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) hi[c] = lo[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8_t cw[3], nx[3];
+    auto rd = [&](int s, int c, bf16x8_t (&f)[3]) {
+      const int off = wo + 16 * c * LDB + 32 * s;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8_t*>(&wp[q][off]);
+    };
+    rd(0, 0, cw);
+    const uint2 mcur = mw;
+#pragma unroll
+    for (int s = 0; s < HS; ++s) {
+      float4 z0 = zv[s][0], z1 = zv[s][1];
+      if (bits) {   // element j of k-step s: column tile 2 s + (g >> 1), word j / 4, bit j % 4
+        const int sh = 4 * (2 * s + (g >> 1));
+        z0 = mask4(z0, mcur.x, sh);
+        z1 = mask4(z1, mcur.y, sh);
+      }
+      if (masked) {
+        const float4 m0 = mv[s][0], m1 = mv[s][1];
+        z0.x = m0.x > 0.f ? z0.x : 0.f; z0.y = m0.y > 0.f ? z0.y : 0.f;
+        z0.z = m0.z > 0.f ? z0.z : 0.f; z0.w = m0.w > 0.f ? z0.w : 0.f;
+        z1.x = m1.x > 0.f ? z1.x : 0.f; z1.y = m1.y > 0.f ? z1.y : 0.f;
+        z1.z = m1.z > 0.f ? z1.z : 0.f; z1.w = m1.w > 0.f ? z1.w : 0.f;
+      }
+      if (a.dz_out && hb == 0 && row < a.n) {
+        float4* q = reinterpret_cast<float4*>(a.dz_out + row * H + 32 * s + 8 * g);
+        q[0] = z0;
+        q[1] = z1;
+      }
+      bf16x8_t x1, x2, x3;
+      x6_split8(z0, z1, x1, x2, x3);
+      load_s(tn, s);   // the next tile's k-step s (and at s = 0 its mask words)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        if (c + 1 < NT) rd(s, c + 1, nx);
+        else if (s + 1 < HS) rd(s + 1, 0, nx);
+        x6_mma(cw, x1, x2, x3, hi[c], lo[c]);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cw[q] = nx[q];
+      }
+    }
+    if (row < a.n) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        const int ct = hb * NT + c;
+        float* dx = tab.dx[ct];
+        if (dx)
+          store_dx4(dx + row * tab.ld[ct] + tab.col[ct] + 4 * g, (tab.dx_acc >> ct) & 1u,
+                    hi[c][0] + lo[c][0], hi[c][1] + lo[c][1], hi[c][2] + lo[c][2],
+                    hi[c][3] + lo[c][3]);
+      }
+    }
+  }
+}
+
 static size_t dgrad4_lds(int h, int k) { return (size_t)k * (h + 8) * 4; }
 
 // dgrad v5: v4's tiling and W^T image, reorganised like fwd v5 for 2 waves per SIMD: G column
@@ -1873,6 +1985,21 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
           block(512);
       const size_t lds = dgrad4_lds(h, K);
+      static const bool x6_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
+      if (x6_env && h == 128 && (K == 128 || K == 256)) {   // the bf16x6 split (see forward)
+        int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8),
+                                                                 K == 128 ? 256 : 128));
+        if (K != 128) streams = cdiv(streams, 8) * 8;
+        if (K == 128)
+          hipLaunchKernelGGL((k_linear_dgrad_x6<128, 128>), dim3((unsigned)streams), block, 0,
+                             stream, a, tab, n16);
+        else
+          hipLaunchKernelGGL((k_linear_dgrad_x6<256, 128>), dim3((unsigned)(2 * streams)), block,
+                             0, stream, a, tab, n16);
+        if (int rc = check_launch("k_linear_dgrad_x6")) return rc;
+        goto dgrad_done;
+      }
+      {
       // v5 at H = 128 (K = 256: 5.06 vs 5.70 ms; K = 128: 3.22 vs 3.25 ms at N = 9M)
       static const int dg_env = getenv("HGNN_K3_DGRAD") ? atoi(getenv("HGNN_K3_DGRAD")) : 0;
       const int dg_ver = dg_env ? dg_env : (h == 128 ? 5 : 4);
@@ -1891,7 +2018,9 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       }
 #undef HGNN_DG4
       if (int rc = check_launch("k_linear_dgrad_v4")) return rc;
+      }
     }
+  dgrad_done:
     if (!(dw || db)) return HGNN_OK;
     if (!ws) return fail(HGNN_E_WS, "linear_bwd: weight gradients need the workspace");
     if (a.dz_out && !fused) {   // the dgrad kernel wrote the masked dz: wgrad streams it alone
