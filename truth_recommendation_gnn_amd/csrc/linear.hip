@@ -1325,6 +1325,118 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
   }
 }
 
+// wgrad on the bf16x6 split (H = 128, K = 128 / 256): dW = dz^T X, db = colsum(dz), 32-row tiles
+// (one k-step of v_mfma_f32_16x16x32_bf16 runs over 32 rows).  Staging: thread (column c, row
+// block rb) loads 8 rows of one column of dz (masked) and of X with dword loads (a wave covers 64
+// consecutive columns of a row: coalesced), splits them and writes each piece plane as one 16-B
+// run of the TRANSPOSED image zt[q][h][row] / xt[q][k][row] (row pitch 40 bf16 = 80 B: the
+// b128 fragment reads of 16 lanes land on 16 distinct 4-bank groups).  Wave w owns output rows
+// h in [16 w, 16 w + 16) and every k tile: per tile 3 + 3 KT fragment reads feed 6 KT MFMAs.
+// NB = 2: double-buffered image, one barrier per tile (K = 128); NB = 1: two (K = 256, whose
+// double image would not fit).  The block's partial dW / db goes to its slab (k_wgrad_reduce).
+template <int K, int NB>
+__global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, const ChunkTab tab,
+                                                            int64_t n_tiles) {
+  constexpr int H = 128, T = 32, KT = K / 16, ZP = T + 8;
+  constexpr int XR = 512 / K;          // row blocks of 8 over X's K columns (4 or 2)
+  constexpr int XJ = T / XR / 8;       // 8-row groups per thread for X (1 or 2)
+  __shared__ __attribute__((aligned(16))) unsigned short zt[NB][3][H * ZP];
+  __shared__ __attribute__((aligned(16))) unsigned short xt[NB][3][K * ZP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int zc = threadIdx.x & 127, zrb = threadIdx.x >> 7;     // dz: column, 8-row block
+  const int xc = threadIdx.x % K, xrb = threadIdx.x / K;        // X: column, first 8-row block
+  const float* xseg = tab.x[xc >> 4] + tab.col[xc >> 4] + (xc & 15);
+  const int64_t xld = tab.ld[xc >> 4];
+  const bool bits = a.mask_in != nullptr;
+  const bool masked = !bits && a.out_act != nullptr;
+  const int64_t n_my = (n_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
+  const int64_t last = a.n - 1;
+  float zr[8], mr[8], xr[XJ][8];
+  uint32_t br[8];
+  auto issue = [&](int64_t it) {
+    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t row = min<int64_t>(r0 + zrb * 8 + j, last);
+      zr[j] = a.dout[row * H + zc];
+      if (bits) br[j] = a.mask_in[row * 4 + ((zc & 15) >> 2)];
+      if (masked) mr[j] = a.out_act[row * H + zc];
+    }
+#pragma unroll
+    for (int q = 0; q < XJ; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t row = min<int64_t>(r0 + (xrb + q * XR) * 8 + j, last);
+        xr[q][j] = xseg[row * xld];
+      }
+  };
+  f32x4 hi[KT], lo[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) hi[k] = lo[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbacc = 0.f;
+  const int bsh = 4 * (zc >> 4) + (zc & 3);
+  auto put8 = [&](unsigned short* plane0, int pstride, const float (&v)[8]) {
+    bf16x8_t p1, p2, p3;
+    x6_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p1, p2,
+              p3);
+    *reinterpret_cast<bf16x8_t*>(plane0) = p1;
+    *reinterpret_cast<bf16x8_t*>(plane0 + pstride) = p2;
+    *reinterpret_cast<bf16x8_t*>(plane0 + 2 * pstride) = p3;
+  };
+  if (n_my > 0) issue(0);
+  for (int64_t it = 0; it < n_my; ++it) {
+    const int b = NB == 2 ? (int)(it & 1) : 0;
+    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
+    if (NB == 1 && it > 0) __syncthreads();   // the previous tile's MFMA reads are done
+    {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float z = zr[j];
+        if (bits) z = (br[j] >> bsh) & 1u ? z : 0.f;
+        if (masked) z = mr[j] > 0.f ? z : 0.f;
+        if (r0 + zrb * 8 + j >= a.n) z = 0.f;   // clamped rows contribute 0
+        dbacc += z;
+        v[j] = z;
+      }
+      put8(&zt[b][0][zc * ZP + zrb * 8], H * ZP, v);
+#pragma unroll
+      for (int q = 0; q < XJ; ++q) put8(&xt[b][0][xc * ZP + (xrb + q * XR) * 8], K * ZP, xr[q]);
+    }
+    if (it + 1 < n_my) issue(it + 1);
+    __syncthreads();
+    bf16x8_t af[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      af[q] = *reinterpret_cast<const bf16x8_t*>(&zt[b][q][(16 * wave + i) * ZP + 8 * g]);
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      const int off = (16 * k + i) * ZP + 8 * g;
+      const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(&xt[b][0][off]);
+      const bf16x8_t b2 = *reinterpret_cast<const bf16x8_t*>(&xt[b][1][off]);
+      const bf16x8_t b3 = *reinterpret_cast<const bf16x8_t*>(&xt[b][2][off]);
+      x6_mma(af, b1, b2, b3, hi[k], lo[k]);
+    }
+  }
+  constexpr int KEXT = K + 1;
+  float* slab = a.slab + (int64_t)blockIdx.x * H * KEXT;
+#pragma unroll
+  for (int k = 0; k < KT; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      slab[(int64_t)(16 * wave + 4 * g + r) * KEXT + 16 * k + i] = hi[k][r] + lo[k][r];
+  // db: the four row blocks' column partials, summed in a fixed order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(&zt[0][0][0]);
+  red[threadIdx.x] = dbacc;
+  __syncthreads();
+  if (threadIdx.x < H)
+    slab[(int64_t)threadIdx.x * KEXT + K] =
+        ((red[threadIdx.x] + red[H + threadIdx.x]) + red[2 * H + threadIdx.x]) +
+        red[3 * H + threadIdx.x];
+}
+
 // T-row tiles need every one of the 512 threads to stage at least one float4 of dz and of X
 template <int H, int K, int T>
 constexpr bool wgrad5_valid() { return T * H / 4 >= 512 && T * K / 4 >= 512; }
@@ -2032,6 +2144,25 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;
     // v4 kept elsewhere (K = 256: v5 6.44 / 9.51 ms at T = 16 / 32 vs 5.65; H = 64 needs T >= 32,
     // which measured slower than v4: 2.44 vs 1.94 ms)
+    static const bool x6w_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
+    if (!fused && x6w_env && h == 128 && (K == 128 || K == 256)) {   // bf16x6 split (see fwd)
+      const int64_t n_tiles = cdiv(n_rows, 32);
+      const int G = (int)std::min<int64_t>(n_tiles, 256);
+      const size_t need = (size_t)G * h * (K + 1) * 4;
+      if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+      a.slab = static_cast<float*>(ws);
+      if (K == 128)
+        hipLaunchKernelGGL((k_linear_wgrad_x6<128, 2>), dim3(G), dim3(512), 0, stream, a, tab,
+                           n_tiles);
+      else
+        hipLaunchKernelGGL((k_linear_wgrad_x6<256, 1>), dim3(G), dim3(512), 0, stream, a, tab,
+                           n_tiles);
+      if (int rc = check_launch("k_linear_wgrad_x6")) return rc;
+      const int64_t total = (int64_t)h * (K + 1);
+      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
+                         a.slab, (int64_t)G, h, K + 1, dw, db);
+      return check_launch("k_wgrad_reduce");
+    }
     static const int wg_env = getenv("HGNN_K3_WGRAD") ? atoi(getenv("HGNN_K3_WGRAD")) : 0;
     const int wg_ver = wg_env ? wg_env : (h == 128 && K == 128 ? 5 : 4);
     static const int wg_t = getenv("HGNN_K3_WGRAD_T") ? atoi(getenv("HGNN_K3_WGRAD_T")) : 16;
