@@ -271,6 +271,13 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
                         int32_t* neg_user, float* neg_w, float* part, float* loss, int32_t* err,
                         hgnn_stream_t stream);
 
+/* K3 at H = 128 and K = 128 / 256 runs on bf16 MFMA as an fp32-exact three-piece split (each
+ * fp32 operand = three bf16 pieces, six piece products per fp32 product, f32 accumulation:
+ * fp32-class error) unless HGNN_K3_X6=0.  on = 1 / 0 selects the split or the
+ * f32-input MFMA kernels for the calls that follow (process-wide, not thread-safe against calls
+ * in flight); on < 0 only queries.  Returns the previous setting. */
+int hgnn_set_k3_split(int32_t on);
+
 /* Single-input forms, one PyG Linear at a time (SURVEY §8b names; same kernels as above):
  *   hgnn_linear_fwd_f32:   out[n,h] = x[n,k] @ w[h,k]^T (+ bias[h] when non-NULL)
  *   hgnn_linear_dgrad_f32: dx[n,k]  = dy[n,h] @ w

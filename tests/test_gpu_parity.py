@@ -3,6 +3,7 @@
 Tolerances: integer CSR work bit-exact; fp32 paths within 1e-4 relative (north_star) — written as
 ``assert_close(rtol=1e-4, atol=1e-5 * scale)``.
 """
+import contextlib
 import pathlib
 
 import numpy as np
@@ -962,3 +963,54 @@ def test_csr_cache_frees_structures_of_dead_edge_tensors():
     close(y.detach().cpu(), ref.detach())
     close(xg.grad.cpu(), xr.grad)
     assert torch.equal(csr.edge_index.cpu(), ei_cpu)
+
+
+# ----------------------------------------------------------------------------- K3 on both paths
+@contextlib.contextmanager
+def _k3_split(on):
+    """The bf16x6 split (on) or the f32-input MFMA kernels (off) for H = 128, K = 128 / 256."""
+    from truth_recommendation_gnn_amd import _native as N
+    prev = N.lib().hgnn_set_k3_split(1 if on else 0)
+    try:
+        yield
+    finally:
+        N.lib().hgnn_set_k3_split(prev)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("ks", [[128], [128, 128], [64, 64, 128], [64, 64]])
+def test_linear_h128_on_both_k3_paths(split, ks):
+    """The H = 128 shapes the split covers (K = 128 and 256, 128-column segments and others),
+    through forward (with the added input and the ReLU bits), every backward mode and the
+    accumulating dX, on the split and on the f32-input MFMA kernels it replaces by default."""
+    with _k3_split(split):
+        for n in (37, 20000):
+            test_linear_fwd_bwd_matches_torch(ks, 128, n)
+        for mode in ("no_relu", "dx_subset", "wgrad_only", "db_only", "dgrad_only"):
+            test_linear_bwd_variants(ks, 128, mode)
+        for masked in (False, True):
+            test_linear_bwd_dx_accumulate_bitwise(ks, 128, masked)
+        for mode in ("all", "wgrad_only", "dz_out"):
+            test_linear_relu_bits_equal_float_mask(ks, 128, mode)
+
+
+def test_k3_split_matches_f32_kernels_closely():
+    """At a cfg4-like K = 256 shape the split and the f32-input kernels agree to fp32 rounding:
+    forward outputs, dX, dW, db within 2e-5 of each tensor's max (dW / db sum 50k rows in
+    different tile orders on the two paths)."""
+    gen = torch.Generator().manual_seed(11)
+    n = 50_000
+    segs = [torch.randn(n, 128, generator=gen).to(DEV) for _ in range(2)]
+    w = (torch.randn(128, 256, generator=gen) * 0.1).to(DEV)
+    b = torch.randn(128, generator=gen).to(DEV)
+    dout = torch.randn(n, 128, generator=gen).to(DEV)
+    res = {}
+    for split in (False, True):
+        with _k3_split(split):
+            out = ops.linear_fwd(segs, w, b, True)
+            dxs = [torch.empty_like(s) for s in segs]
+            dw, db = ops.linear_bwd(segs, w, dout, out, dxs, True, True)
+            res[split] = [out, *dxs, dw, db]
+    for a, c in zip(res[False], res[True]):
+        scale = float(a.abs().max())
+        assert float((a - c).abs().max()) <= 2e-5 * scale, (float((a - c).abs().max()), scale)

@@ -88,6 +88,7 @@ _SIGS = {
     "hgnn_relabel_checked": (_c_i32, [_p, _c_i64, _c_i64, _p, _c_i64, _p, _p, _p, _p, _c_sz,
                                       _p]),
     "hgnn_relabel_multi_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_set_k3_split": (_c_i32, [_c_i32]),
     "hgnn_pad_csr_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "hgnn_relabel_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _c_i32, _p, _c_sz,
                                     _p]),

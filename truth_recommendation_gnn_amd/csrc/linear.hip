@@ -605,6 +605,14 @@ __global__ void __launch_bounds__(256) k_linear_bwd_lds(const LinArgs a, int64_t
   }
 }
 
+// The bf16x6 K3 kernels (H = 128, K = 128 / 256): on unless HGNN_K3_X6=0, or as last set by
+// hgnn_set_k3_split (tests run both paths in one process).
+static int g_k3_x6 = -1;
+static bool x6_enabled() {
+  if (g_k3_x6 < 0) g_k3_x6 = (!getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0) ? 1 : 0;
+  return g_k3_x6 != 0;
+}
+
 static bool fast_path_ok(const LinArgs& a, bool vec) {
   static const int off = getenv("HGNN_LIN_GENERAL") ? atoi(getenv("HGNN_LIN_GENERAL")) : 0;
   if (off) return false;
@@ -1913,8 +1921,7 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     const bool s8 = s8_env && h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
     // the fp32-exact bf16x6 split (k_linear_fwd_x6) at H = 128, K = 128 / 256: default
     // (HGNN_K3_X6=0: the f32-input MFMA kernels below)
-    static const bool x6_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
-    if (x6_env && h == 128 && (a.k_total == 128 || a.k_total == 256)) {
+    if (x6_enabled() && h == 128 && (a.k_total == 128 || a.k_total == 256)) {
       int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
                                                                a.k_total == 128 ? 256 : 128));
       if (a.k_total != 128) streams = cdiv(streams, 8) * 8;   // column-half pairs b, b + 8
@@ -2097,8 +2104,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
           block(512);
       const size_t lds = dgrad4_lds(h, K);
-      static const bool x6_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
-      if (x6_env && h == 128 && (K == 128 || K == 256)) {   // the bf16x6 split (see forward)
+      if (x6_enabled() && h == 128 && (K == 128 || K == 256)) {   // bf16x6 split (see forward)
         int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8),
                                                                  K == 128 ? 256 : 128));
         if (K != 128) streams = cdiv(streams, 8) * 8;
@@ -2144,8 +2150,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;
     // v4 kept elsewhere (K = 256: v5 6.44 / 9.51 ms at T = 16 / 32 vs 5.65; H = 64 needs T >= 32,
     // which measured slower than v4: 2.44 vs 1.94 ms)
-    static const bool x6w_env = !getenv("HGNN_K3_X6") || atoi(getenv("HGNN_K3_X6")) != 0;
-    if (!fused && x6w_env && h == 128 && (K == 128 || K == 256)) {   // bf16x6 split (see fwd)
+    if (!fused && x6_enabled() && h == 128 && (K == 128 || K == 256)) {   // bf16x6 (see fwd)
       const int64_t n_tiles = cdiv(n_rows, 32);
       const int G = (int)std::min<int64_t>(n_tiles, 256);
       const size_t need = (size_t)G * h * (K + 1) * 4;
@@ -2281,6 +2286,12 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     if (int rc = check_launch("k_wgrad_reduce")) return rc;
   }
   return HGNN_OK;
+}
+
+int hgnn_set_k3_split(int32_t on) {
+  const int prev = x6_enabled() ? 1 : 0;
+  if (on >= 0) g_k3_x6 = on ? 1 : 0;
+  return prev;
 }
 
 // ---- single-input forms (the PyG Linear calls one at a time; SURVEY §8b names) ----------------
