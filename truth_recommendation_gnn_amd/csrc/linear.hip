@@ -2156,6 +2156,9 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       const size_t need = (size_t)G * h * (K + 1) * 4;
       if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
       a.slab = static_cast<float*>(ws);
+      // (a variant staging float4 columns on 2-4 of the 8 waves measured slower: 6.34 vs 4.81 ms
+      // and 11.36 vs 8.59 ms for the 9M-row K = 128 / 256 backward — the split work then sits on
+      // fewer waves while the others wait at the barrier)
       if (K == 128)
         hipLaunchKernelGGL((k_linear_wgrad_x6<128, 2>), dim3(G), dim3(512), 0, stream, a, tab,
                            n_tiles);
