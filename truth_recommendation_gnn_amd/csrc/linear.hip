@@ -1337,15 +1337,17 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
 // (one k-step of v_mfma_f32_16x16x32_bf16 runs over 32 rows).  Staging: thread (column c, row
 // block rb) loads 8 rows of one column of dz (masked) and of X with dword loads (a wave covers 64
 // consecutive columns of a row: coalesced), splits them and writes each piece plane as one 16-B
-// run of the TRANSPOSED image zt[q][h][row] / xt[q][k][row] (row pitch 40 bf16 = 80 B: the
-// b128 fragment reads of 16 lanes land on 16 distinct 4-bank groups).  Wave w owns output rows
+// run of the TRANSPOSED image zt[q][h][row] / xt[q][k][row] (64-B rows, the 16-B chunks XOR-
+// swizzled by (c >> 2) & 3 so the b128 fragment reads of 16 lanes hit 16 distinct bank groups).  Wave w owns output rows
 // h in [16 w, 16 w + 16) and every k tile: per tile 3 + 3 KT fragment reads feed 6 KT MFMAs.
-// NB = 2: double-buffered image, one barrier per tile (K = 128); NB = 1: two (K = 256, whose
-// double image would not fit).  The block's partial dW / db goes to its slab (k_wgrad_reduce).
+// NB = 2: double-buffered image, one barrier per tile (144 KB at K = 256); NB = 1: two.  The block's partial dW / db goes to its slab (k_wgrad_reduce).
 template <int K, int NB>
 __global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, const ChunkTab tab,
                                                             int64_t n_tiles) {
-  constexpr int H = 128, T = 32, KT = K / 16, ZP = T + 8;
+  constexpr int H = 128, T = 32, KT = K / 16, ZP = T;
+  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ ((c >> 2) & 3)): the 16 lanes of a
+  // b128 fragment read (16 consecutive c, one r) land on 16 distinct 16-B bank groups
+  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((c >> 2) & 3)); };
   constexpr int XR = 512 / K;          // row blocks of 8 over X's K columns (4 or 2)
   constexpr int XJ = T / XR / 8;       // 8-row groups per thread for X (1 or 2)
   __shared__ __attribute__((aligned(16))) unsigned short zt[NB][3][H * ZP];
@@ -1408,19 +1410,19 @@ __global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, con
         dbacc += z;
         v[j] = z;
       }
-      put8(&zt[b][0][zc * ZP + zrb * 8], H * ZP, v);
+      put8(&zt[b][0][sw(zc, zrb)], H * ZP, v);
 #pragma unroll
-      for (int q = 0; q < XJ; ++q) put8(&xt[b][0][xc * ZP + (xrb + q * XR) * 8], K * ZP, xr[q]);
+      for (int q = 0; q < XJ; ++q) put8(&xt[b][0][sw(xc, xrb + q * XR)], K * ZP, xr[q]);
     }
     if (it + 1 < n_my) issue(it + 1);
     __syncthreads();
     bf16x8_t af[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
-      af[q] = *reinterpret_cast<const bf16x8_t*>(&zt[b][q][(16 * wave + i) * ZP + 8 * g]);
+      af[q] = *reinterpret_cast<const bf16x8_t*>(&zt[b][q][sw(16 * wave + i, g)]);
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
-      const int off = (16 * k + i) * ZP + 8 * g;
+      const int off = sw(16 * k + i, g);
       const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(&xt[b][0][off]);
       const bf16x8_t b2 = *reinterpret_cast<const bf16x8_t*>(&xt[b][1][off]);
       const bf16x8_t b3 = *reinterpret_cast<const bf16x8_t*>(&xt[b][2][off]);
@@ -2163,7 +2165,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
         hipLaunchKernelGGL((k_linear_wgrad_x6<128, 2>), dim3(G), dim3(512), 0, stream, a, tab,
                            n_tiles);
       else
-        hipLaunchKernelGGL((k_linear_wgrad_x6<256, 1>), dim3(G), dim3(512), 0, stream, a, tab,
+        hipLaunchKernelGGL((k_linear_wgrad_x6<256, 2>), dim3(G), dim3(512), 0, stream, a, tab,
                            n_tiles);
       if (int rc = check_launch("k_linear_wgrad_x6")) return rc;
       const int64_t total = (int64_t)h * (K + 1);
