@@ -308,6 +308,15 @@ int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n
                             const int32_t* neg_u_order, int64_t n_edges, const float* cscale,
                             float* dU, float* part, float* loss, int32_t* err,
                             hgnn_stream_t stream);
+/* hgnn_edge_score_fwd_i32 with the negatives drawn in the kernel: the negative of position k is
+ * the draw hgnn_uniform_i32(d_seed, n_edges, n_posts) would write at k (train_gnn.py:272's
+ * torch.randint, one per positive edge), so no position-order array is written or read (the
+ * fused loss passes neg_out = NULL to hgnn_draw_sort_negatives and this the same seed). */
+int hgnn_edge_score_fwd_draw(const float* U, const float* P, int32_t d, int64_t n_users,
+                             int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                             const uint64_t* d_seed, int64_t n_edges, const float* cscale,
+                             float* dU, float* part, float* loss, int32_t* err,
+                             hgnn_stream_t stream);
 /* n uniform int32 draws in [0, hi) (the negatives of train_gnn.py:272), counter-based from the
  * 64-bit seed at d_seed (device memory: a torch Generator draws it without a host sync). */
 int hgnn_uniform_i32(const uint64_t* d_seed, int64_t n, int32_t hi, int32_t* out,

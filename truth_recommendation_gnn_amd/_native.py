@@ -105,6 +105,8 @@ _SIGS = {
                                      _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "hgnn_edge_score_fwd_i32": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _c_i64, _p,
                                          _p, _p, _p, _p, _p]),
+    "hgnn_edge_score_fwd_draw": (_c_i32, [_p, _p, _c_i32, _c_i64, _c_i64, _p, _p, _p, _c_i64,
+                                          _p, _p, _p, _p, _p, _p]),
     "hgnn_uniform_i32": (_c_i32, [_p, _c_i64, _c_i32, _p, _p]),
     "hgnn_scale_unless_one": (_c_i32, [_p, _c_i64, _p, _p]),
     "hgnn_linear_fwd_f32": (_c_i32, [_p, _c_i64, _c_i32, _p, _c_i32, _p, _p, _p]),

@@ -34,7 +34,8 @@ struct ScoreArgs {
   const int32_t* rowptr;       // user-grouped CSR of the positive edges
   const int32_t* col;          // post id per position
   const int64_t* neg;          // negative post id per position (user-grouped order) ...
-  const int32_t* neg32;        // ... or as int32 (exactly one of the two is set)
+  const int32_t* neg32;        // ... or as int32 ...
+  const uint64_t* neg_seed;    // ... or drawn here: uniform_draw(*neg_seed, position, n_posts)
   const int32_t* to_post_pos;  // position -> post-grouped position (for hpos)
   const float* cscale;         // device scalar mean(pos_weights)
   float* dU;
@@ -80,6 +81,10 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
   const int64_t u = (int64_t)blockIdx.x * 4 + wave;
   const float c = *a.cscale;
   const int d = a.d;
+  // drawn negatives (hgnn_edge_score_fwd_draw): the draw of position k is recomputed here, so the
+  // sort that groups them by post writes no position-order copy for this pass to read
+  const bool seed_p = a.neg_seed != nullptr;
+  const uint64_t seed = seed_p ? *a.neg_seed : 0;
   float lpos = 0.f, lneg = 0.f;   // per-lane loss sums (edge = lane)
   if (u < a.n_users) {
     const int64_t beg = a.rowptr[u], end = a.rowptr[u + 1];
@@ -95,7 +100,8 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
       int pid = 0, nid = 0;
       if (lane < n) {
         pid = a.col[base + lane];
-        const int64_t nn = a.neg32 ? (int64_t)a.neg32[base + lane] : a.neg[base + lane];
+        const int64_t nn = seed_p ? (int64_t)uniform_draw(seed, base + lane, (uint32_t)a.n_posts)
+                           : a.neg32 ? (int64_t)a.neg32[base + lane] : a.neg[base + lane];
         if (nn < 0 || nn >= a.n_posts) atomicAdd(a.err, 1);
         else nid = (int)nn;
       }
@@ -264,7 +270,7 @@ int64_t hgnn_edge_score_parts(int64_t n_users) {
 static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
                           int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
                           const int64_t* neg_u_order, const int32_t* neg32,
-                          const int32_t* to_post_pos, int64_t n_edges, const float* cscale,
+                          const uint64_t* neg_seed, const int32_t* to_post_pos, int64_t n_edges, const float* cscale,
                           float* dU, float* hpos, int32_t* neg_key, int32_t* neg_user,
                           float* neg_w, float* part, float* loss, int32_t* err,
                           hgnn_stream_t stream_) {
@@ -278,6 +284,7 @@ static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_u
   (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);
   ScoreArgs a{};
   a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order; a.neg32 = neg32;
+  a.neg_seed = neg_seed;
   a.to_post_pos = to_post_pos; a.cscale = cscale; a.dU = dU; a.hpos = hpos; a.neg_key = neg_key;
   a.neg_u = neg_user; a.neg_w = neg_w; a.part = part; a.err = err; a.n_users = n_users;
   a.n_posts = n_posts; a.inv_e = n_edges > 0 ? 1.f / (float)n_edges : 0.f; a.d = d;
@@ -311,7 +318,7 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
                         hgnn_stream_t stream) {
   if (n_edges > 0 && !neg_u_order) return fail(HGNN_E_ARG, "edge_score: negatives are null");
   return edge_score_fwd(U, P, d, n_users, n_posts, rowptr_u, col_u, neg_u_order, nullptr,
-                        to_post_pos, n_edges, cscale, dU, hpos, neg_key, neg_user, neg_w, part,
+                        nullptr, to_post_pos, n_edges, cscale, dU, hpos, neg_key, neg_user, neg_w, part,
                         loss, err, stream);
 }
 
@@ -322,6 +329,19 @@ int hgnn_edge_score_fwd_i32(const float* U, const float* P, int32_t d, int64_t n
                             hgnn_stream_t stream) {
   if (n_edges > 0 && !neg_u_order) return fail(HGNN_E_ARG, "edge_score: negatives are null");
   return edge_score_fwd(U, P, d, n_users, n_posts, rowptr_u, col_u, nullptr, neg_u_order,
+                        nullptr, nullptr, n_edges, cscale, dU, nullptr, nullptr, nullptr, nullptr, part,
+                        loss, err, stream);
+}
+
+int hgnn_edge_score_fwd_draw(const float* U, const float* P, int32_t d, int64_t n_users,
+                             int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,
+                             const uint64_t* d_seed, int64_t n_edges, const float* cscale,
+                             float* dU, float* part, float* loss, int32_t* err,
+                             hgnn_stream_t stream) {
+  if (n_edges > 0 && !d_seed) return fail(HGNN_E_ARG, "edge_score: the draw's seed is null");
+  if (n_posts < 1 || n_posts >= (int64_t(1) << 31) - 1)
+    return fail(HGNN_E_ARG, "edge_score_draw: n_posts=%lld out of range", (long long)n_posts);
+  return edge_score_fwd(U, P, d, n_users, n_posts, rowptr_u, col_u, nullptr, nullptr, d_seed,
                         nullptr, n_edges, cscale, dU, nullptr, nullptr, nullptr, nullptr, part,
                         loss, err, stream);
 }

@@ -911,7 +911,7 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     if draw is not None:
         if draw.n != E or draw.num_posts != np_:
             raise ValueError("edge_bce_loss: the NegativeDraw does not match the positive edges")
-        neg = torch.empty(E, dtype=torch.int32, device=dev)   # written by the sort's first pass
+        neg = None   # drawn again where read (the sort's first pass, the scoring pass)
     else:
         neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
     rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
@@ -924,10 +924,11 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     with lanes.ctx(1):
         ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
         if draw is not None:
-            # draws computed in the sort's first pass; `neg` (position order) for the scoring pass
-            with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
+            # draws computed in the sort's first pass (and again in the scoring pass: no
+            # position-order copy is written)
+            with _timed("sort_negatives", 4 * E * (2 * 4)):
                 N.check(lib.hgnn_draw_sort_negatives(
-                    N.ptr(draw.seed), N.ptr(uop), E, np_, N.ptr(neg), N.ptr(rowptr_n),
+                    N.ptr(draw.seed), N.ptr(uop), E, np_, None, N.ptr(rowptr_n),
                     N.ptr(nu_s), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
                     "hgnn_draw_sort_negatives")
         elif neg32:
@@ -944,8 +945,6 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
                     N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
                     None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
                     "hgnn_sort_pairs_i64")
-    if draw is not None and lanes.side is not None:
-        lanes.main.wait_stream(lanes.side)    # the scoring pass reads the sort's `neg`
     if ready is not None and p_chunks is None:
         # P is still arriving (parallel.py's all-gather of the post table): the sort above
         # needs only the edges, so it ran ahead; every kernel below reads P
@@ -973,7 +972,12 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     if ready is not None and p_chunks is not None:
         ready()                                 # all of P, for the scoring pass
     with _timed(f"edge_score_d{d}", 4 * E * (2 * d + 1 + 2) + 8 * nu * d):
-        if neg32:
+        if draw is not None:
+            N.check(lib.hgnn_edge_score_fwd_draw(
+                N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
+                N.ptr(draw.seed), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
+                N.ptr(err), s), "hgnn_edge_score_fwd_draw")
+        elif neg32:
             N.check(lib.hgnn_edge_score_fwd_i32(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
                 N.ptr(neg), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
