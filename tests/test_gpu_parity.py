@@ -709,6 +709,50 @@ def test_fused_loss_negative_draw_equals_materialised():
         ops.edge_bce_loss(out["user"], out["post"], pos, dr, pw, neg_order="edge")
 
 
+@pytest.mark.parametrize("nu,npost,E,d", [(3000, 1 << 20, 70_001, 128), (500, 37, 9_000, 64),
+                                           (10, 5, 0, 16)])
+def test_edge_score_draw_entry_equals_materialised_draws(nu, npost, E, d):
+    """hgnn_edge_score_fwd_draw (each position's negative drawn in the kernel) is bit for bit
+    hgnn_edge_score_fwd_i32 over the draws hgnn_uniform_i32 materialises from the same seed."""
+    from truth_recommendation_gnn_amd import _native as Nn
+    lib, s = Nn.lib(), Nn.stream_ptr(torch.device(DEV))
+    g = torch.Generator(device=DEV).manual_seed(5)
+    users = torch.sort(torch.randint(0, nu, (E,), device=DEV, generator=g))[0]
+    rowptr = torch.searchsorted(users, torch.arange(nu + 1, device=DEV)).to(torch.int32)
+    col = torch.randint(0, npost, (E,), device=DEV, generator=g, dtype=torch.int32)
+    U = torch.randn(nu, d, device=DEV, generator=g)
+    P = torch.randn(npost, d, device=DEV, generator=g)
+    c = torch.tensor(1.25, device=DEV)
+    seed = torch.tensor([0x0BAD_5EED_1234], dtype=torch.int64, device=DEV)
+    neg = torch.empty(E, dtype=torch.int32, device=DEV)
+    if E:
+        Nn.check(lib.hgnn_uniform_i32(Nn.ptr(seed), E, npost, Nn.ptr(neg), s), "uniform")
+    outs = []
+    for entry in ("draw", "i32"):
+        dU = torch.full_like(U, float("nan"))
+        part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), device=DEV)
+        loss = torch.empty((), device=DEV)
+        err = torch.zeros(2, dtype=torch.int32, device=DEV)
+        if entry == "draw":
+            rc = lib.hgnn_edge_score_fwd_draw(Nn.ptr(U), Nn.ptr(P), d, nu, npost, Nn.ptr(rowptr),
+                                              Nn.ptr(col), Nn.ptr(seed), E, Nn.ptr(c), Nn.ptr(dU),
+                                              Nn.ptr(part), Nn.ptr(loss), Nn.ptr(err), s)
+        else:
+            rc = lib.hgnn_edge_score_fwd_i32(Nn.ptr(U), Nn.ptr(P), d, nu, npost, Nn.ptr(rowptr),
+                                             Nn.ptr(col), Nn.ptr(neg) if E else None, E,
+                                             Nn.ptr(c), Nn.ptr(dU), Nn.ptr(part), Nn.ptr(loss),
+                                             Nn.ptr(err), s)
+        Nn.check(rc, entry)
+        torch.cuda.synchronize()
+        assert int(err[0]) == 0
+        outs.append((loss, dU))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if E:
+        assert lib.hgnn_edge_score_fwd_draw(Nn.ptr(U), Nn.ptr(P), d, nu, npost, Nn.ptr(rowptr),
+                                            Nn.ptr(col), None, E, Nn.ptr(c), Nn.ptr(dU),
+                                            Nn.ptr(part), Nn.ptr(loss), Nn.ptr(err), s) != 0
+
+
 def test_weighted_rgcn_fused_loss_step_matches_golden():
     z, x, e, params = _fixture_cfg1()
     model = WeightedRGCN(hidden_dim=64).to(DEV)
