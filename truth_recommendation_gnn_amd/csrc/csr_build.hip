@@ -176,6 +176,8 @@ struct KeyGen {
   uint32_t hi;
 };
 
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb);
+
 template <int BITS, int RR = kSortRounds, bool GEN = false>
 __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
                                                                int shift, int32_t* counts,
@@ -183,7 +185,10 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
   constexpr int R = 1 << BITS;
   __shared__ int hist[R];
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) hist[dd] = 0;
-  const int64_t base = (int64_t)blockIdx.x * (kSortThreads * RR);
+  // XCD-aware tile order as in k_digit_scatter: neighbouring tiles' count words (one line holds
+  // 16 tiles' counts of a digit) are written from one XCD's L2 instead of eight
+  const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t base = tile * (kSortThreads * RR);
   int k[RR];
   const uint64_t seed = GEN ? *gen.seed : 0;
 #pragma unroll
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
     if (k[r] >= 0) atomicAdd(&hist[(k[r] >> shift) & (R - 1)], 1);
   __syncthreads();
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads)
-    counts[(int64_t)dd * gridDim.x + blockIdx.x] = hist[dd];
+    counts[(int64_t)dd * gridDim.x + tile] = hist[dd];
 }
 
 // Stable scatter, block-local sort first.  Tile = 4096 items; wave w owns the contiguous
@@ -457,6 +462,11 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
   int32_t* offs = w.take<int32_t>(nb * kMaxRadix + 1);
   int passes, bits;
   radix_plan(n_keys, &passes, &bits);
+  // the last pass takes only the bits left (>= 6: narrower digits measured no faster), e.g. 7 + 7
+  // + 6 for 20-bit keys: fewer ranking ballots and longer runs per digit in its scatter
+  int key_bits = 0;
+  while ((int64_t(1) << key_bits) <= n_keys) ++key_bits;
+  const int last_bits = std::max(6, std::min(bits, key_bits - bits * (passes - 1)));
   const int64_t ncount = nb * ((int64_t)1 << bits);
   size_t scan_b = 0;
   exclusive_scan_i32(nullptr, nullptr, ncount, nullptr, &scan_b, stream);
@@ -467,6 +477,8 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
   const int32_t* bin = b_in;
   for (int p = 0; p < passes; ++p) {
     const int shift = bits * p;
+    const int pbits = p == passes - 1 ? last_bits : bits;
+    const int64_t pcount = nb * ((int64_t)1 << pbits);
     const bool to_out = ((passes - 1 - p) % 2) == 0;
     int32_t* kout = (kin == ka) ? kb : ka;   // (k_in itself is never written)
     int32_t* aout = to_out ? a_out : ta;
@@ -478,10 +490,10 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
                              0, stream, kin, E, shift, counts, gen);                              \
   else hipLaunchKernelGGL((k_digit_counts<BV>), dim3(nb), dim3(kSortThreads), 0, stream, kin, E,  \
                           shift, counts, KeyGen{nullptr, 0})
-    HGNN_BITS_SWITCH(bits, HGNN_COUNTS)
+    HGNN_BITS_SWITCH(pbits, HGNN_COUNTS)
 #undef HGNN_COUNTS
     if (int rc = check_launch("k_digit_counts")) return rc;
-    if (int rc = exclusive_scan_i32(counts, offs, ncount, scan_ws, &scan_b, stream)) return rc;
+    if (int rc = exclusive_scan_i32(counts, offs, pcount, scan_ws, &scan_b, stream)) return rc;
 #define HGNN_SCATTER(BV, HB)                                                                 \
   hipLaunchKernelGGL((k_digit_scatter<BV, HB>), dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, \
                      bin, E, shift, offs, kout, aout, bout, ident)
@@ -491,7 +503,7 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
                        dim3(kSortThreads), 0, stream, kin, ain, bin, E, shift, offs, kout, aout, \
                        bout, ident, gen, gen_out);                                            \
   } else if (b_in) { HGNN_SCATTER(BV, true); } else { HGNN_SCATTER(BV, false); }
-    HGNN_BITS_SWITCH(bits, HGNN_SCATTER_B)
+    HGNN_BITS_SWITCH(pbits, HGNN_SCATTER_B)
 #undef HGNN_SCATTER_B
 #undef HGNN_SCATTER
     if (int rc = check_launch("k_digit_scatter")) return rc;
@@ -802,7 +814,8 @@ int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E
   Workspace w(ws, ws_bytes);
   int32_t* ka = w.take<int32_t>(E);
   const int32_t* sk = nullptr;
-  if (int rc = radix_sort_pairs(nullptr, ka, E, n_keys, a, nullptr, a_sorted, nullptr, w, stream,
+  // the draws are < n_keys by construction: no sentinel value to leave room for
+  if (int rc = radix_sort_pairs(nullptr, ka, E, n_keys - 1, a, nullptr, a_sorted, nullptr, w, stream,
                                 &sk, KeyGen{d_seed, (uint32_t)n_keys}, neg_out))
     return rc;
   hipLaunchKernelGGL(k_rowptr_from_sorted, dim3(cdiv(n_keys + 1, 256)), dim3(256), 0, stream, sk, E,
