@@ -904,7 +904,10 @@ __device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x
 template <int K, int HB, bool ADD, bool S8>
 __global__ void __launch_bounds__(512, 1) k_linear_fwd_x6(const LinArgs a, const ChunkTab tab,
                                                           int64_t n_tiles) {
-  constexpr int NT = HB / 16, KS = K / 32, LDB = K + 8, NH = 128 / HB;
+  // LDB = K + 16 halfwords: rows 32 B apart mod 256, so each 16-lane group of a ds_read_b128
+  // fragment read ({0-3,12-15,20-27}, ...) hits 16 distinct bank quads (K + 8 was 2-way: 4 extra
+  // LDS cycles per read, SQ_LDS_BANK_CONFLICT = 4.0 x SQ_INSTS_LDS in profiles/pmc_k3_cfg4_r3.json)
+  constexpr int NT = HB / 16, KS = K / 32, LDB = K + 16, NH = 128 / HB;
   __shared__ __attribute__((aligned(16))) unsigned short wp[3][HB * LDB];
   // NH = 2: blocks b and b + 8 (the same XCD: hardware block b runs on XCD b % 8) take the two
   // column halves of one tile stream, so the second read of a tile's rows can hit that L2
@@ -1345,9 +1348,11 @@ template <int K, int NB>
 __global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, const ChunkTab tab,
                                                             int64_t n_tiles) {
   constexpr int H = 128, T = 32, KT = K / 16, ZP = T;
-  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ ((c >> 2) & 3)): the 16 lanes of a
-  // b128 fragment read (16 consecutive c, one r) land on 16 distinct 16-B bank groups
-  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((c >> 2) & 3)); };
+  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ T[(c >> 2) & 3]), T = {0, 2, 3, 1}:
+  // each 16-lane group of a b128 fragment read ({0-3,12-15,20-27}, ... : lanes (i, g) reading
+  // c = 16 k + i, r = g) lands on 16 distinct bank quads (T[q] = q left them 2-way), and the
+  // staging stores keep their 2-way pattern
+  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((0x78 >> (2 * ((c >> 2) & 3))) & 3)); };
   constexpr int XR = 512 / K;          // row blocks of 8 over X's K columns (4 or 2)
   constexpr int XJ = T / XR / 8;       // 8-row groups per thread for X (1 or 2)
   __shared__ __attribute__((aligned(16))) unsigned short zt[NB][3][H * ZP];
@@ -1570,7 +1575,7 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
 template <int K, int KB>
 __global__ void __launch_bounds__(512, 1) k_linear_dgrad_x6(const LinArgs a, const ChunkTab tab,
                                                             int64_t n_tiles) {
-  constexpr int H = 128, NT = KB / 16, HS = H / 32, LDB = H + 8, NH = K / KB;
+  constexpr int H = 128, NT = KB / 16, HS = H / 32, LDB = H + 16, NH = K / KB;   // see fwd
   __shared__ __attribute__((aligned(16))) unsigned short wp[3][KB * LDB];
   const int hb = NH == 1 ? 0 : (int)((blockIdx.x >> 3) & 1), col0 = hb * KB;
   const int64_t stream_id = NH == 1 ? blockIdx.x : (blockIdx.x & 7) + 8 * (blockIdx.x >> 4);
