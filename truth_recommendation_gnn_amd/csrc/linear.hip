@@ -1348,11 +1348,11 @@ template <int K, int NB>
 __global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, const ChunkTab tab,
                                                             int64_t n_tiles) {
   constexpr int H = 128, T = 32, KT = K / 16, ZP = T;
-  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ T[(c >> 2) & 3]), T = {0, 2, 3, 1}:
-  // each 16-lane group of a b128 fragment read ({0-3,12-15,20-27}, ... : lanes (i, g) reading
-  // c = 16 k + i, r = g) lands on 16 distinct bank quads (T[q] = q left them 2-way), and the
-  // staging stores keep their 2-way pattern
-  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((0x78 >> (2 * ((c >> 2) & 3))) & 3)); };
+  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ ((c >> 1) & 3)): each 16-lane group
+  // of a b128 fragment read ({0-3,12-15,20-27}, ... : lanes (i, g) reading c = 16 k + i, r = g)
+  // lands on 16 distinct bank quads, and so does each 8-lane group of the staging stores (8
+  // consecutive c, one r); r ^ ((c >> 2) & 3) left both 2-way
+  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((c >> 1) & 3)); };
   constexpr int XR = 512 / K;          // row blocks of 8 over X's K columns (4 or 2)
   constexpr int XJ = T / XR / 8;       // 8-row groups per thread for X (1 or 2)
   __shared__ __attribute__((aligned(16))) unsigned short zt[NB][3][H * ZP];
