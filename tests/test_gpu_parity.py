@@ -709,6 +709,37 @@ def test_fused_loss_negative_draw_equals_materialised():
         ops.edge_bce_loss(out["user"], out["post"], pos, dr, pw, neg_order="edge")
 
 
+@pytest.mark.parametrize("neg_kind", ["int32", "draw"])
+def test_loss_dp_gather_in_row_blocks_is_bitwise_one_pass(neg_kind):
+    """The sharded step's dP gather over the post table as it lands in row blocks (p_chunks: each
+    block's positives a rowptr slice with its own skew plan, _row_range) gives bitwise the loss,
+    dU and dP of the one-pass gather — blocks in any order, an empty block, heavy (chunked) rows
+    inside blocks and on their edges; int32 negatives and the in-kernel NegativeDraw."""
+    rng = np.random.default_rng(21)
+    nu, npost, E, d = 5000, 3000, 400_000, 64
+    pos = torch.from_numpy(np.stack([rng.integers(0, nu, E),
+                                     synth._zipf_sample_np(rng, npost, E, 1.0)]).astype(np.int64)
+                           ).to(DEV)
+    U = torch.from_numpy(rng.standard_normal((nu, d)).astype(np.float32) * 0.3).to(DEV)
+    P = torch.from_numpy(rng.standard_normal((npost, d)).astype(np.float32) * 0.3).to(DEV)
+    cscale = torch.tensor(1.25, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(4)
+    neg = (ops.sample_negatives(pos, npost, generator=gen) if neg_kind == "int32"
+           else ops.draw_negatives(pos, npost, generator=gen))
+    csr = ops.relation_csr_for_loss(pos, nu, npost)
+    heavy = sorted(set(csr.fwd.plan.heavy_rows.cpu().tolist()))
+    assert len(heavy) >= 3                      # the Zipf head really is chunked
+    h0 = heavy[len(heavy) // 2]
+    a, b = h0, max(h0 + 1, (h0 + npost) // 2)   # a block starting on a heavy row
+    ref = ops.edge_bce_loss_raw(U, P, pos, neg, E, cscale)
+    for chunks in ([(a, b, None), (0, a, None), (b, b, None), (b, npost, None)],
+                   [(0, npost, None)],
+                   [(q * npost // 7, (q + 1) * npost // 7, None) for q in range(7)]):
+        got = ops.edge_bce_loss_raw(U, P, pos, neg, E, cscale, p_chunks=chunks)
+        for x, y in zip(got, ref):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("nu,npost,E,d", [(3000, 1 << 20, 70_001, 128), (500, 37, 9_000, 64),
                                            (10, 5, 0, 16)])
 def test_edge_score_draw_entry_equals_materialised_draws(nu, npost, E, d):
@@ -1012,16 +1043,17 @@ def test_csr_cache_frees_structures_of_dead_edge_tensors():
 # ----------------------------------------------------------------------------- K3 on both paths
 @contextlib.contextmanager
 def _k3_split(on):
-    """The bf16x6 split (on) or the f32-input MFMA kernels (off) for H = 128, K = 128 / 256."""
+    """K3 family for H = 128, K = 128 / 256: the bf16x6 split, split once per element (1 / True,
+    the default), the round-3 per-wave split kernels (2), the f32-input MFMA kernels (0 / False)."""
     from truth_recommendation_gnn_amd import _native as N
-    prev = N.lib().hgnn_set_k3_split(1 if on else 0)
+    prev = N.lib().hgnn_set_k3_split(int(on))
     try:
         yield
     finally:
         N.lib().hgnn_set_k3_split(prev)
 
 
-@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("split", [0, 1, 2])
 @pytest.mark.parametrize("ks", [[128], [128, 128], [64, 64, 128], [64, 64]])
 def test_linear_h128_on_both_k3_paths(split, ks):
     """The H = 128 shapes the split covers (K = 128 and 256, 128-column segments and others),

@@ -11,65 +11,18 @@
 // X[row i][kc+4g .. kc+4g+3] and uses element q as the A operand of k-step q; B takes the same
 // k from W.  So k-step q sums k = kc+4g+q over g — every k of the chunk exactly once, with
 // contiguous 16-B loads (the k order inside a chunk is permuted, which only moves rounding).
-#include "hgnn_common.h"
-
-#include <hip/hip_bf16.h>
+#include "linear_common.h"
 
 #include <algorithm>
 #include <stdlib.h>
 
 namespace hgnn {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-struct Seg {
-  const float* x;
-  float* dx;
-  int32_t k;
-  int32_t off;
-};
-
-struct LinArgs {
-  Seg seg[HGNN_MAX_SEG];
-  int32_t n_seg;
-  int32_t k_total;
-  const float* w;
-  const float* bias;
-  const float* dout;
-  const float* out_act;   // ReLU output for the backward mask (nullable)
-  const uint32_t* mask_in;  // backward: the same mask as bits (hgnn_linear_fwd_mask; nullable)
-  uint32_t* mask_out;       // forward: write the ReLU mask as bits (nullable)
-  const float* add;       // forward: [n, h] rows added before the activation (nullable)
-  float* dz_out;          // backward: the masked dz written out as well (nullable; dgrad kernels)
-  uint32_t dx_acc;        // backward: bit s set = segment s's dX is added into dx, not stored
-  float* out;
-  float* slab;            // wgrad partials [gx][h][k_total+1]
-  int64_t n;
-  int32_t h;
-  int32_t relu;
-  int64_t rows_per_block; // wgrad
-};
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// ReLU mask as bits (hgnn_linear_fwd_mask), in the lane layout the persistent kernels share:
-// the lane (i, g) that holds columns 16 c + 4 g .. +3 (c = 0 .. H/16 - 1) of row i finds them in
-// word row * 4 + g, bits 4 c .. 4 c + 3 (H <= 128, a multiple of 16): one 4-B word per lane per
-// row, no cross-lane exchange in the forward, 16 B per row instead of the output's 4 H.
-__device__ __forceinline__ float4 mask4(float4 v, uint32_t word, int shift) {
-  v.x = (word >> shift) & 1u ? v.x : 0.f;
-  v.y = (word >> (shift + 1)) & 1u ? v.y : 0.f;
-  v.z = (word >> (shift + 2)) & 1u ? v.z : 0.f;
-  v.w = (word >> (shift + 3)) & 1u ? v.w : 0.f;
-  return v;
-}
-
-__device__ __forceinline__ uint32_t relu_bits(float4 v, int shift) {
-  return ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
-          (v.w > 0.f ? 8u : 0u)) << shift;
-}
 
 template <bool VEC>
 __device__ __forceinline__ void load4(const float* p, int valid_elems, float (&v)[4]) {
@@ -633,27 +586,7 @@ static int fast_grid(int64_t n_tiles) {
 //   * ds_read_b128 where lanes (i, g) read row i, columns 4g..4g+3: stride = 8 (mod 16) dwords
 //     (row i lands on 16-B slot 2i + g: even/odd by g, 8 distinct per b128 lane group);
 //   * ds_read_b32 where lanes (i, g) read row g, column i: stride = 16 (mod 32) dwords.
-constexpr int kMaxChunks = 16;   // K <= 256
-struct ChunkTab {
-  const float* x[kMaxChunks];
-  float* dx[kMaxChunks];
-  int32_t ld[kMaxChunks];
-  int32_t col[kMaxChunks];   // first column of the chunk inside its segment
-  uint32_t dx_acc;           // bit c set = chunk c's dX is added into dx (LinArgs::dx_acc)
-};
 
-// dX fragment store of the persistent kernels: stored, or added into what dx holds (the
-// gradient of a node table that another update already wrote — one pass instead of a torch add)
-__device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1, float a2,
-                                          float a3) {
-  float4* q = reinterpret_cast<float4*>(p);
-  if (add) {
-    const float4 o = *q;
-    *q = make_float4(o.x + a0, o.y + a1, o.z + a2, o.w + a3);
-  } else {
-    *q = make_float4(a0, a1, a2, a3);
-  }
-}
 
 // Address of row `row`'s float4 at columns 16 c + 4 g .. +3 of the concatenated input.  S8: every
 // 8 consecutive chunks are one segment (segments 128 columns wide, as at cfg3/cfg4), so with c
@@ -860,38 +793,6 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
 // double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
 // accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
 // 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
-typedef short bf16x8_t __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ unsigned short x6_bf16(float f) {
-  return __bfloat16_as_ushort(__float2bfloat16(f));   // round to nearest even (v_cvt_pk_bf16_f32)
-}
-__device__ __forceinline__ float x6_f32(unsigned short b) {
-  return __uint_as_float(((unsigned)b) << 16);
-}
-__device__ __forceinline__ void x6_split8(const float4& u, const float4& v, bf16x8_t& p1,
-                                          bf16x8_t& p2, bf16x8_t& p3) {
-  const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const unsigned short a1 = x6_bf16(f[j]);
-    const float r1 = f[j] - x6_f32(a1);
-    const unsigned short a2 = x6_bf16(r1);
-    p1[j] = (short)a1;
-    p2[j] = (short)a2;
-    p3[j] = (short)x6_bf16(r1 - x6_f32(a2));
-  }
-}
-// acc_hi += w1 x1; acc_lo += w2 x2 + w3 x1 + w1 x3 + w2 x1 + w1 x2 (small terms first)
-__device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x1,
-                                       const bf16x8_t& x2, const bf16x8_t& x3, f32x4& hi,
-                                       f32x4& lo) {
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x2, lo, 0, 0, 0);
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], x1, lo, 0, 0, 0);
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x3, lo, 0, 0, 0);
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x1, lo, 0, 0, 0);
-  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x2, lo, 0, 0, 0);
-  hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x1, hi, 0, 0, 0);
-}
 
 // Forward on the split: persistent, one 8-wave block per CU.  The block's HB output columns of
 // W (HB = 128, or 64 for K = 256, whose three planes for all 128 columns would not fit in LDS:
@@ -1929,6 +1830,7 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     // the fp32-exact bf16x6 split (k_linear_fwd_x6) at H = 128, K = 128 / 256: default
     // (HGNN_K3_X6=0: the f32-input MFMA kernels below)
     if (x6_enabled() && h == 128 && (a.k_total == 128 || a.k_total == 256)) {
+      if (xs_enabled()) return xs_linear_fwd(a, tab, stream);   // split once per element
       int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
                                                                a.k_total == 128 ? 256 : 128));
       if (a.k_total != 128) streams = cdiv(streams, 8) * 8;   // column-half pairs b, b + 8
@@ -2106,6 +2008,36 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     const bool split = split_env >= 0 ? split_env != 0 : (h == 128 && K == 128);
     const bool fused = !split && any_dx && (dw || db) && K <= 128 &&
                        v4_bwd_lds(h, K, true) <= 160 * 1024;
+    if (x6_enabled() && xs_enabled() && h == 128 && (K == 128 || K == 256)) {
+      // the split-once kernels (linear_xs.hip): dz split once for the dgrad and the wgrad
+      const bool wg = dw || db;
+      a.slab = nullptr;
+      if (wg) {
+        const size_t need = (size_t)xs_bwd_grid(n_rows) * h * (K + 1) * 4;
+        if (!ws || ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+        a.slab = static_cast<float*>(ws);
+      }
+      int G = 0;
+      if (any_dx && K != 128) {
+        // dgrad on the per-wave split kernel (it writes the masked dz when asked), then the
+        // wgrad from dout and the mask as before
+        const int64_t n16 = cdiv(n_rows, 16);
+        const int64_t streams = cdiv(std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 128)), 8) * 8;
+        hipLaunchKernelGGL((k_linear_dgrad_x6<256, 128>), dim3((unsigned)(2 * streams)), dim3(512),
+                           0, stream, a, tab, n16);
+        if (int rc = check_launch("k_linear_dgrad_x6")) return rc;
+        if (!wg) return HGNN_OK;
+        a.dz_out = nullptr;
+        if (int rc = xs_linear_bwd(a, tab, false, &G, stream)) return rc;
+      } else if (any_dx || wg) {
+        if (int rc = xs_linear_bwd(a, tab, any_dx, &G, stream)) return rc;
+      }
+      if (!wg) return HGNN_OK;
+      const int64_t total = (int64_t)h * (K + 1);
+      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
+                         a.slab, (int64_t)G, h, K + 1, dw, db);
+      return check_launch("k_wgrad_reduce");
+    }
     if (any_dx && !fused) {
       const int64_t n16 = cdiv(n_rows, 16);
       const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
@@ -2299,8 +2231,11 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
 }
 
 int hgnn_set_k3_split(int32_t on) {
-  const int prev = x6_enabled() ? 1 : 0;
-  if (on >= 0) g_k3_x6 = on ? 1 : 0;
+  const int prev = x6_enabled() ? (xs_enabled() ? 1 : 2) : 0;
+  if (on >= 0) {
+    g_k3_x6 = on ? 1 : 0;
+    g_k3_xs = on == 2 ? 0 : 1;
+  }
   return prev;
 }
 

@@ -1,0 +1,178 @@
+// K3 (fused multi-segment linear) types and bf16-split helpers shared by linear.hip (the f32-input
+// MFMA kernels, the general shapes and the C ABI) and linear_xs.hip (the split-once kernels).
+#pragma once
+#include "hgnn_common.h"
+
+#include <hip/hip_bf16.h>
+
+namespace hgnn {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+
+struct Seg {
+  const float* x;
+  float* dx;
+  int32_t k;
+  int32_t off;
+};
+
+struct LinArgs {
+  Seg seg[HGNN_MAX_SEG];
+  int32_t n_seg;
+  int32_t k_total;
+  const float* w;
+  const float* bias;
+  const float* dout;
+  const float* out_act;   // ReLU output for the backward mask (nullable)
+  const uint32_t* mask_in;  // backward: the same mask as bits (hgnn_linear_fwd_mask; nullable)
+  uint32_t* mask_out;       // forward: write the ReLU mask as bits (nullable)
+  const float* add;       // forward: [n, h] rows added before the activation (nullable)
+  float* dz_out;          // backward: the masked dz written out as well (nullable; dgrad kernels)
+  uint32_t dx_acc;        // backward: bit s set = segment s's dX is added into dx, not stored
+  float* out;
+  float* slab;            // wgrad partials [gx][h][k_total+1]
+  int64_t n;
+  int32_t h;
+  int32_t relu;
+  int64_t rows_per_block; // wgrad
+};
+
+// H (output width) in {64, 128}, K (sum of segments) in {64, 128, 256}, every segment a multiple
+// of 16 columns and float4-aligned.  Per 16-column chunk c of the concatenated input, a host-built
+// table gives the segment base/stride (no per-element segment search).
+constexpr int kMaxChunks = 16;   // K <= 256
+struct ChunkTab {
+  const float* x[kMaxChunks];
+  float* dx[kMaxChunks];
+  int32_t ld[kMaxChunks];
+  int32_t col[kMaxChunks];   // first column of the chunk inside its segment
+  uint32_t dx_acc;           // bit c set = chunk c's dX is added into dx (LinArgs::dx_acc)
+};
+
+// ReLU mask as bits (hgnn_linear_fwd_mask), in the lane layout the persistent kernels share:
+// the lane (i, g) that holds columns 16 c + 4 g .. +3 (c = 0 .. H/16 - 1) of row i finds them in
+// word row * 4 + g, bits 4 c .. 4 c + 3 (H <= 128, a multiple of 16): one 4-B word per lane per
+// row, no cross-lane exchange in the forward, 16 B per row instead of the output's 4 H.
+__device__ __forceinline__ float4 mask4(float4 v, uint32_t word, int shift) {
+  v.x = (word >> shift) & 1u ? v.x : 0.f;
+  v.y = (word >> (shift + 1)) & 1u ? v.y : 0.f;
+  v.z = (word >> (shift + 2)) & 1u ? v.z : 0.f;
+  v.w = (word >> (shift + 3)) & 1u ? v.w : 0.f;
+  return v;
+}
+
+// ReLU as one v_max_f32 per element (fmaxf(v, 0) compiles to a canonicalize + max pair); a NaN
+// gives 0, as fmaxf does
+__device__ __forceinline__ float relu1(float v) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ float4 relu4(float4 v) {
+  return make_float4(relu1(v.x), relu1(v.y), relu1(v.z), relu1(v.w));
+}
+
+__device__ __forceinline__ uint32_t relu_bits(float4 v, int shift) {
+  return ((v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) |
+          (v.w > 0.f ? 8u : 0u)) << shift;
+}
+
+// dX fragment store of the persistent kernels: stored, or added into what dx holds (the
+// gradient of a node table that another update already wrote — one pass instead of a torch add)
+__device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1, float a2,
+                                          float a3) {
+  float4* q = reinterpret_cast<float4*>(p);
+  if (add) {
+    const float4 o = *q;
+    *q = make_float4(o.x + a0, o.y + a1, o.z + a2, o.w + a3);
+  } else {
+    *q = make_float4(a0, a1, a2, a3);
+  }
+}
+
+// ================================================================ bf16x6: fp32-exact split
+// gfx950 runs bf16 MFMA at 16x the fp32 MFMA rate (2.5 PF vs 157 TF dense).  Every fp32 value
+// v splits exactly-enough into three bf16 pieces, v1 = bf16(v), v2 = bf16(v - v1),
+// v3 = bf16(v - v1 - v2) (|v - v1 - v2 - v3| <= ~2^-24 |v|), and a product x w becomes the six
+// piece products whose orders add to <= 4: x1w1 | x1w2 + x2w1 + x1w3 + x3w1 + x2w2 (the dropped
+// x2w3, x3w2, x3w3 are <= ~2^-24 |x w|).  Each piece product is exact in f32 and accumulates in
+// f32, so the result has fp32 accuracy: measured at most 0.68 f32 ulp of sum |x w| against
+// double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
+// accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
+// 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
+// Non-finite values: v1 = bf16(v) carries an inf (or NaN) and the residual pieces are zero, so
+// an inf input gives the inf (or NaN) the f32 product would, not inf - inf = NaN in a residual.
+__device__ __forceinline__ unsigned short x6_bf16(float f) {
+  return __bfloat16_as_ushort(__float2bfloat16(f));   // round to nearest even (v_cvt_pk_bf16_f32)
+}
+__device__ __forceinline__ float x6_f32(unsigned short b) {
+  return __uint_as_float(((unsigned)b) << 16);
+}
+// the residual after a piece, clamped to +-2^100: finite residuals (|r| <= 2^-8 |v|) pass
+// unchanged; v = +-inf gives inf - inf = NaN and a v near FLT_MAX whose piece rounded to inf
+// gives -+inf — both become a finite residual that cannot turn the inf product x1 w1 into NaN.
+// v_med3_f32 with IEEE NaN handling (a NaN operand yields the median of the other two, here
+// 2^100; scripts/probe_minmax.hip on the GPU) is one instruction where the isfinite test and its
+// select were two per element.
+__device__ __forceinline__ float x6_res(float v, unsigned short piece) {
+  const float r = v - x6_f32(piece);
+  float c;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(c) : "v"(r), "v"(-0x1p100f), "v"(0x1p100f));
+  return c;
+}
+__device__ __forceinline__ void x6_split1(float v, unsigned short& a1, unsigned short& a2,
+                                          unsigned short& a3) {
+  a1 = x6_bf16(v);
+  const float r1 = x6_res(v, a1);
+  a2 = x6_bf16(r1);
+  a3 = x6_bf16(r1 - x6_f32(a2));
+}
+__device__ __forceinline__ void x6_split8(const float4& u, const float4& v, bf16x8_t& p1,
+                                          bf16x8_t& p2, bf16x8_t& p3) {
+  const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    unsigned short a1, a2, a3;
+    x6_split1(f[j], a1, a2, a3);
+    p1[j] = (short)a1;
+    p2[j] = (short)a2;
+    p3[j] = (short)a3;
+  }
+}
+__device__ __forceinline__ void x6_split4(const float4& u, bf16x4_t& p1, bf16x4_t& p2,
+                                          bf16x4_t& p3) {
+  const float f[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    unsigned short a1, a2, a3;
+    x6_split1(f[j], a1, a2, a3);
+    p1[j] = (short)a1;
+    p2[j] = (short)a2;
+    p3[j] = (short)a3;
+  }
+}
+// acc_hi += w1 x1; acc_lo += w2 x2 + w3 x1 + w1 x3 + w2 x1 + w1 x2 (small terms first)
+__device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x1,
+                                       const bf16x8_t& x2, const bf16x8_t& x3, f32x4& hi,
+                                       f32x4& lo) {
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x2, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], x1, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x3, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], x1, lo, 0, 0, 0);
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x2, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x1, hi, 0, 0, 0);
+}
+
+// The split-once kernels (linear_xs.hip): H = 128, K = 128 / 256, every segment 16-column
+// chunked and float4-aligned.  Host launchers; the caller validated the arguments.
+bool xs_enabled();
+extern int g_k3_xs;   // -1: from HGNN_K3_XS at the first call
+int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream);
+// dW / db partials into a.slab (grid blocks x [H][K + 1]); the caller reduces them.  dx: run the
+// dgrad too (tab.dx).  Returns the block count through *grid.
+int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid, hipStream_t stream);
+int64_t xs_bwd_grid(int64_t n_rows);
+
+}  // namespace hgnn

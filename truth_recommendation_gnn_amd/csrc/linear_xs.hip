@@ -1,0 +1,481 @@
+// K3 on the fp32-exact bf16x6 split, split once per element (round 4).  Replaces SAGEConv's
+// lin_l / lin_r addmm plus WeightedRGCN's weighted sum, bias and ReLU (train_gnn.py:158-160,
+// 187-198) and their autograd at H = 128, K = 128 / 256: the cfg3 / cfg4 projections.
+//
+// The round-3 split kernels (linear.hip, k_linear_*_x6) loaded X in the MFMA fragment layout —
+// 64 B of a row per lane group per load instruction — and every wave split the values it loaded
+// (at K = 256 twice, once per column half).  They ran at 0.37-0.43 of the HBM roof, bound by
+// neither HBM nor MFMA.  Here a block stages R-row tiles with whole-row coalesced float4 loads
+// (a wave reads 1 KiB of contiguous row per instruction), splits each element ONCE into three
+// bf16 piece planes in LDS, and all 8 waves take their MFMA operands from those planes:
+//   * forward: wave w owns output columns 16 w .. 16 w + 15; its W pieces live in VGPRs for the
+//     whole launch, the tile's X pieces come from LDS (ds_read_b128 row fragments);
+//   * backward: the masked dz tile is split once and serves BOTH the dgrad (ds_read_b128 row
+//     fragments, W^T pieces in VGPRs) and the wgrad (ds_read_b64_tr_b16 transposed fragments,
+//     with the X tile's planes), so dz and X are each read from HBM once per launch.
+// Double-buffered planes, one barrier per tile; the next tile's loads are issued at the top of
+// an iteration and split into the other buffer after its MFMA sweep.
+//
+// LDS piece planes are [row][K + 16 halfwords]: rows 32 B apart mod 256 B, so the b128 row
+// fragment reads (lanes (i, g): row i, 16 B at 8 g) and the b64 transposed reads (see tr8) are
+// conflict-free, and each 16-lane group of the staging ds_write_b64 writes 128 contiguous bytes.
+#include "linear_common.h"
+
+#include <algorithm>
+#include <stdlib.h>
+
+namespace hgnn {
+
+namespace {
+
+constexpr int kH = 128;     // output width
+constexpr int kThr = 512;   // 8 waves
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// row clamp (a mixed-type min<int64_t>(int64, int32) compiled to f64 converts and v_min_f64)
+__device__ __forceinline__ uint32_t clamp_row(int64_t row, int32_t last) {
+  return min((uint32_t)row, (uint32_t)last);   // row < 2^32: n < 2^31 and at most 2 G R past it
+}
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// One [R x K] fp32 tile of the concatenated input, staged by all 512 threads: float4 j of thread
+// t is f = t + 512 j, row f / (K / 4), column 4 (f % (K / 4)) — a thread's column (and therefore
+// its 16-column chunk of the ChunkTab) is fixed, its rows step by 512 / (K / 4).  Row indices
+// are 32-bit (the host checks n < 2^31): one v_mad_u64_u32 per row address.
+template <int K, int R>
+struct XStage {
+  static constexpr int NL = R * K / 4 / kThr;
+  static constexpr int RSTEP = kThr / (K / 4);
+  struct Regs {
+    float4 v[NL];
+  };
+  const float* base;
+  uint32_t ld;
+  int row0, col;
+  __device__ __forceinline__ void init(const ChunkTab& tab) {
+    col = 4 * ((int)threadIdx.x % (K / 4));
+    row0 = (int)threadIdx.x / (K / 4);
+    const int c = col >> 4;
+    base = tab.x[c] + tab.col[c] + (col & 15);
+    ld = (uint32_t)tab.ld[c];
+  }
+  // rows past the end are clamped to the last row (loaded, never stored)
+  __device__ __forceinline__ void issue(Regs& x, int64_t r0, int32_t last) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const uint32_t row = clamp_row(r0 + row0 + j * RSTEP, last);
+      x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
+    }
+  }
+  // split into the three planes (plane stride PS halfwords, row stride LDP)
+  template <int LDP, int PS>
+  __device__ __forceinline__ void put(const Regs& x, unsigned short* pl, int64_t r0,
+                                      int64_t n) const {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      float4 v = x.v[j];
+      if (r0 + row0 + j * RSTEP >= n) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      bf16x4_t p1, p2, p3;
+      x6_split4(v, p1, p2, p3);
+      unsigned short* d = pl + (row0 + j * RSTEP) * LDP + col;
+      *reinterpret_cast<bf16x4_t*>(d) = p1;
+      *reinterpret_cast<bf16x4_t*>(d + PS) = p2;
+      *reinterpret_cast<bf16x4_t*>(d + 2 * PS) = p3;
+    }
+  }
+};
+
+// b128 row fragment of a plane: lane (i, g) reads row r0 + i, halfwords c0 + 8 g .. + 7
+template <int LDP>
+__device__ __forceinline__ bf16x8_t row8(const unsigned short* pl, int r0, int c0, int i, int g) {
+  return *reinterpret_cast<const bf16x8_t*>(pl + (r0 + i) * LDP + c0 + 8 * g);
+}
+
+// Transposed fragment of a [32 rows][LDP] plane for an MFMA operand whose reduction index runs
+// over the tile's rows: lane (i, g) receives column c0 + i at the rows of its k slots.  The
+// reduction index k = 8 g + kk maps to tile row 4 g + kk (kk < 4) and 16 + 4 g + kk - 4
+// (kk >= 4) — any bijection does, the same for both operands — so each 32-lane half of a
+// ds_read_b64_tr_b16 reads 8 consecutive rows (32 B each at 32 B apart mod 256): conflict-free.
+// Lane 4 q + p of a 16-lane group addresses row q of its 4-row block, columns 4 p .. 4 p + 3.
+template <int LDP>
+__device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int lane) {
+  const int g = lane >> 4, m = lane & 15;
+  const unsigned short* p = pl + (4 * g + (m >> 2)) * LDP + c0 + 4 * (m & 3);
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p + 16 * LDP));
+  bf16x8_t r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// ---------------------------------------------------------------- forward
+// out[n, 0:128] = act(sum_s X_s W_s^T + b (+ add)), tiles of R rows (R * K * 4 = 32 KB of X).
+// MFMA: A = W pieces (rows = output columns 16 w + i), B = X^T from the planes, so lane (i, g)
+// ends with columns 16 w + 4 g .. +3 of tile row 16 r + i: float4 stores; the ReLU mask words
+// (bit 4 c + e of word row * 4 + g) collect each wave's nibble through an LDS OR.
+// Per tile: [the previous tile's output stores] [this tile's added rows, the next tile's X]
+// [MFMA sweep] [epilogue into registers] [split of the next tile into the other buffer] [barrier].
+// Memory order matters because vmcnt is one in-order counter: a wait on an operation also waits
+// for everything issued before it.  The outputs are stored at the top of the NEXT iteration,
+// before its loads, and their registers are held until after that iteration's sweep: the
+// compiler waits for a store to read its data before it lets anything overwrite those registers,
+// and with the stores issued last (before the barrier) that wait landed at the loop head and
+// drained the prefetch with them.  The prefetch is unconditional (past the last tile the rows
+// clamp and the split goes to an unread buffer): a conditional issue made the waitcnt pass
+// assume loads in flight at the loop head and wait for everything there.  (Measured and not
+// kept: loads two tiles ahead in a second register set, the split interleaved into the sweep
+// — 3.84 vs 3.69 ms at 9M rows, K = 256; the kernel runs at a power-limited ~1.75 GHz, so
+// what counts is the instruction count, not the overlap.)
+template <int K, bool ADD, int PROBE = 0>
+__global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
+                                                        int64_t n_tiles) {
+  constexpr int R = K == 256 ? 32 : 64, KS = K / 32, RT = R / 16, LDP = K + 16, PS = R * LDP;
+  __shared__ __attribute__((aligned(16))) unsigned short pl[2][3 * PS];
+  __shared__ uint32_t mk[2][R * 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int32_t last = (int32_t)(a.n - 1);
+  const int64_t G = gridDim.x;
+  // W pieces of this wave's 16 output columns, for the whole launch
+  bf16x8_t wa[KS][3];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const float4* p = reinterpret_cast<const float4*>(a.w + (int64_t)(16 * w + i) * K + 32 * s +
+                                                      8 * g);
+    x6_split8(p[0], p[1], wa[s][0], wa[s][1], wa[s][2]);
+  }
+  const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + 16 * w + 4 * g)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool mask_out = a.mask_out != nullptr;
+  for (int e = threadIdx.x; e < 2 * R * 4; e += kThr) (&mk[0][0])[e] = 0u;
+  XStage<K, R> xs;
+  xs.init(tab);
+  typename XStage<K, R>::Regs xr;
+  float4 ad[ADD ? RT : 1];
+  float4 po[RT];   // the previous tile's output rows
+#pragma unroll
+  for (int r = 0; r < RT; ++r) po[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto store_prev = [&](int64_t tp, int bp) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const int64_t row = tp * R + 16 * r + i;
+      if (row < a.n) *reinterpret_cast<float4*>(a.out + row * kH + 16 * w + 4 * g) = po[r];
+    }
+    if (mask_out && threadIdx.x < R * 4) {   // its mask words are complete (last barrier)
+      const int64_t row = tp * R + (threadIdx.x >> 2);
+      if (row < a.n) a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
+      mk[bp][threadIdx.x] = 0u;
+    }
+  };
+  int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
+  xs.issue(xr, t * R, last);
+  xs.template put<LDP, PS>(xr, pl[0], t * R, a.n);
+  __syncthreads();
+  int it = 0;
+  for (; t < n_tiles; t += G, ++it) {
+    const int b = it & 1;
+    if (it > 0) store_prev(t - G, b ^ 1);
+    if constexpr (ADD) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        const uint32_t row = clamp_row(t * R + 16 * r + i, last);
+        ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
+    }
+    if constexpr (PROBE != 2) xs.issue(xr, (t + G) * R, last);
+    __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
+    const unsigned short* p = pl[b];
+    f32x4 hi[RT], lo[RT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
+        const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
+        const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
+        if constexpr (PROBE != 1) x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
+        else { hi[r][0] += (float)x1[0]; lo[r][1] += (float)x2[1] + (float)x3[2]; }
+      }
+    }
+    // the stored rows' registers are reserved until here (see above)
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+      asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      float4 v = make_float4((hi[r][0] + lo[r][0]) + bb.x, (hi[r][1] + lo[r][1]) + bb.y,
+                             (hi[r][2] + lo[r][2]) + bb.z, (hi[r][3] + lo[r][3]) + bb.w);
+      if constexpr (ADD) {
+        v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
+      }
+      if (a.relu) v = relu4(v);
+      po[r] = v;
+      if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
+    }
+    xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R, a.n);
+    __syncthreads();
+  }
+  store_prev(t - G, (it - 1) & 1);
+}
+
+// ---------------------------------------------------------------- backward
+// Per 32-row tile: dz = dout masked by the ReLU bits (or by out > 0, or none), written to dz_out
+// when asked, summed for db, split into planes; X split into planes.  Then
+//   DX: dX^T = W^T dz^T (wave w owns dX columns 16 w .. +15 = chunk w; K = 128): A = W^T pieces
+//       in VGPRs, B = dz row fragments;
+//   WG: dW += dz^T X over the tile's 32 rows (one MFMA k-step): wave w owns dW columns
+//       [KW w, KW w + KW), KW = K / 8, every h; A = transposed dz fragments, B = transposed X.
+// The block's dW / db partials go to its slab [H][K + 1] (k_wgrad_reduce sums them in order).
+template <int K, bool DX, bool WG, bool ACC>
+__global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const ChunkTab tab,
+                                                        int64_t n_tiles) {
+  static_assert(!DX || K == 128, "dgrad: one 16-column chunk per wave");
+  constexpr int R = 32, LDZ = kH + 16, LDX = K + 16, ZS = R * LDZ, XS = R * LDX;
+  constexpr int KT = K / 128;      // 16-column k tiles of dW per wave
+  constexpr int HS = kH / 32;      // dgrad MFMA k-steps (reduction over h)
+  __shared__ __attribute__((aligned(16))) unsigned short zp[2][3 * ZS];
+  __shared__ __attribute__((aligned(16))) unsigned short xp[WG ? 2 : 1][WG ? 3 * XS : 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const int32_t last32 = (int32_t)(a.n - 1);
+  const int64_t G = gridDim.x;
+  const bool bits = a.mask_in != nullptr;
+  const bool masked = !bits && a.out_act != nullptr;
+  // dgrad: W^T pieces of dX columns 16 w + i, h = 32 s + 8 g .. +7
+  bf16x8_t wt[DX ? HS : 1][3];
+  if constexpr (DX) {
+#pragma unroll
+    for (int s = 0; s < HS; ++s) {
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = a.w[(int64_t)(32 * s + 8 * g + e) * K + 16 * w + i];
+      x6_split8(make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]),
+                wt[s][0], wt[s][1], wt[s][2]);
+    }
+  }
+  // dz staging: float4 j of thread t at row (t >> 5) + 16 j, columns 4 (t & 31) .. +3
+  constexpr int ZL = 2;
+  const int zc = 4 * (threadIdx.x & 31), zr = threadIdx.x >> 5;
+  const int msh = 4 * (zc >> 4);      // bits of column tile zc / 16 in word row * 4 + (zc / 4) % 4
+  float4 zv[ZL], mv[ZL];
+  uint32_t mw[ZL];
+  XStage<K, R> xs;
+  typename XStage<K, R>::Regs xr;
+  if constexpr (WG) xs.init(tab);
+  auto issue = [&](int64_t tt) {
+#pragma unroll
+    for (int j = 0; j < ZL; ++j) {
+      const uint64_t row = clamp_row(tt * R + zr + 16 * j, last32);
+      zv[j] = *reinterpret_cast<const float4*>(a.dout + row * kH + zc);
+      if (bits) mw[j] = a.mask_in[row * 4 + ((zc >> 2) & 3)];
+      if (masked) mv[j] = *reinterpret_cast<const float4*>(a.out_act + row * kH + zc);
+    }
+    if constexpr (WG) xs.issue(xr, tt * R, last32);
+  };
+  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto put = [&](int64_t tt, int b) {
+#pragma unroll
+    for (int j = 0; j < ZL; ++j) {
+      const int64_t row = tt * R + zr + 16 * j;
+      float4 z = zv[j];
+      if (bits) z = mask4(z, mw[j], msh);
+      if (masked) {
+        const float4 m = mv[j];
+        z.x = m.x > 0.f ? z.x : 0.f; z.y = m.y > 0.f ? z.y : 0.f;
+        z.z = m.z > 0.f ? z.z : 0.f; z.w = m.w > 0.f ? z.w : 0.f;
+      }
+      if (row >= a.n) z = make_float4(0.f, 0.f, 0.f, 0.f);
+      else if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + row * kH + zc) = z;
+      dbacc.x += z.x; dbacc.y += z.y; dbacc.z += z.z; dbacc.w += z.w;
+      bf16x4_t p1, p2, p3;
+      x6_split4(z, p1, p2, p3);
+      unsigned short* d = zp[b] + (zr + 16 * j) * LDZ + zc;
+      *reinterpret_cast<bf16x4_t*>(d) = p1;
+      *reinterpret_cast<bf16x4_t*>(d + ZS) = p2;
+      *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
+    }
+    if constexpr (WG) xs.template put<LDX, XS>(xr, xp[b], tt * R, a.n);
+  };
+  f32x4 hw[WG ? 8 : 1][KT], lw[WG ? 8 : 1][KT];
+#pragma unroll
+  for (int h = 0; h < (WG ? 8 : 1); ++h)
+#pragma unroll
+    for (int u = 0; u < KT; ++u) hw[h][u] = lw[h][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // dgrad: this wave's dX columns are chunk w (K = 128), loop-invariant
+  float* dxp = nullptr;
+  int64_t dxld = 0;
+  bool acc_dx = false;
+  if constexpr (DX) {
+    dxp = tab.dx[w] ? tab.dx[w] + tab.col[w] : nullptr;
+    dxld = tab.ld[w];
+    acc_dx = (tab.dx_acc >> w) & 1u;
+  }
+  int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
+  issue(t);
+  put(t, 0);
+  __syncthreads();
+  for (int it = 0; t < n_tiles; t += G, ++it) {
+    const int b = it & 1;
+    // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
+    // wait leaves the prefetch in flight
+    float4 dxo[ACC ? R / 16 : 1];
+    if constexpr (ACC) {
+      if (dxp) {
+#pragma unroll
+        for (int r = 0; r < R / 16; ++r)
+          dxo[r] = *reinterpret_cast<const float4*>(
+              dxp + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld + 4 * g);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    issue(t + G);   // consumed by put() at the end of this iteration, unconditionally (see forward)
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
+    const unsigned short* z = zp[b];
+    f32x4 dh[DX ? R / 16 : 1], dl[DX ? R / 16 : 1];
+    if constexpr (DX) {
+#pragma unroll
+      for (int r = 0; r < R / 16; ++r) {
+        dh[r] = dl[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < HS; ++s) {
+          const bf16x8_t x1 = row8<LDZ>(z, 16 * r, 32 * s, i, g);
+          const bf16x8_t x2 = row8<LDZ>(z + ZS, 16 * r, 32 * s, i, g);
+          const bf16x8_t x3 = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s, i, g);
+          x6_mma(wt[s], x1, x2, x3, dh[r], dl[r]);
+        }
+      }
+    }
+    if constexpr (WG) {
+      const unsigned short* x = xp[b];
+      bf16x8_t xb[KT][3];
+#pragma unroll
+      for (int u = 0; u < KT; ++u)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) xb[u][q] = tr8<LDX>(x + q * XS, 16 * (KT * w + u), lane);
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        bf16x8_t za[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) za[q] = tr8<LDZ>(z + q * ZS, 16 * h, lane);
+#pragma unroll
+        for (int u = 0; u < KT; ++u) x6_mma(za, xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
+      }
+    }
+    if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
+#pragma unroll
+      for (int r = 0; r < R / 16; ++r) {
+        const int64_t row = t * R + 16 * r + i;
+        if (dxp && row < a.n) {
+          float4 v = make_float4(dh[r][0] + dl[r][0], dh[r][1] + dl[r][1], dh[r][2] + dl[r][2],
+                                 dh[r][3] + dl[r][3]);
+          if constexpr (ACC) {
+            if (acc_dx) {
+              v.x = dxo[r].x + v.x; v.y = dxo[r].y + v.y; v.z = dxo[r].z + v.z;
+              v.w = dxo[r].w + v.w;
+            }
+          }
+          *reinterpret_cast<float4*>(dxp + row * dxld + 4 * g) = v;
+        }
+      }
+    }
+    put(t + G, b ^ 1);
+    __syncthreads();
+  }
+  if constexpr (WG) {
+    constexpr int KEXT = K + 1;
+    float* slab = a.slab + (int64_t)blockIdx.x * kH * KEXT;
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+#pragma unroll
+      for (int u = 0; u < KT; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          slab[(int64_t)(16 * h + 4 * g + j) * KEXT + 16 * (KT * w + u) + i] =
+              hw[h][u][j] + lw[h][u][j];
+    // db: the 16 row groups' column partials, summed in a fixed order (the loop's last barrier
+    // retired every plane read, so the planes hold the reduction)
+    float4* red = reinterpret_cast<float4*>(&zp[0][0]);
+    red[threadIdx.x] = dbacc;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      float4 s = red[threadIdx.x];
+#pragma unroll
+      for (int q = 1; q < 16; ++q) {
+        const float4 v = red[q * 32 + threadIdx.x];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+      const int c = 4 * threadIdx.x;
+      slab[(int64_t)(c + 0) * KEXT + K] = s.x;
+      slab[(int64_t)(c + 1) * KEXT + K] = s.y;
+      slab[(int64_t)(c + 2) * KEXT + K] = s.z;
+      slab[(int64_t)(c + 3) * KEXT + K] = s.w;
+    }
+  }
+}
+
+}  // namespace
+
+// On unless HGNN_K3_XS=0 (then the round-3 split kernels), and only while the split itself is on
+// (hgnn_set_k3_split / HGNN_K3_X6, linear.hip).
+int g_k3_xs = -1;
+bool xs_enabled() {
+  if (g_k3_xs < 0) g_k3_xs = (!getenv("HGNN_K3_XS") || atoi(getenv("HGNN_K3_XS")) != 0) ? 1 : 0;
+  return g_k3_xs != 0;
+}
+
+int64_t xs_bwd_grid(int64_t n_rows) {
+  return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_rows, 32), 256));
+}
+
+int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
+  if (a.n >= (int64_t(1) << 31)) return fail(HGNN_E_UNSUPPORTED, "k_lin_fwd_xs: n >= 2^31 rows");
+  const int K = a.k_total;
+  const int64_t R = K == 256 ? 32 : 64;
+  const int64_t n_tiles = cdiv(a.n, R);
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 256))), block(kThr);
+  static const int probe = getenv("HGNN_XS_PROBE") ? atoi(getenv("HGNN_XS_PROBE")) : 0;
+  if (probe == 1 && K == 256 && !a.add) {
+    hipLaunchKernelGGL((k_lin_fwd_xs<256, false, 1>), grid, block, 0, stream, a, tab, n_tiles);
+  } else if (probe == 2 && K == 256 && !a.add) {
+    hipLaunchKernelGGL((k_lin_fwd_xs<256, false, 2>), grid, block, 0, stream, a, tab, n_tiles);
+  } else if (K == 128) {
+    if (a.add) hipLaunchKernelGGL((k_lin_fwd_xs<128, true>), grid, block, 0, stream, a, tab, n_tiles);
+    else hipLaunchKernelGGL((k_lin_fwd_xs<128, false>), grid, block, 0, stream, a, tab, n_tiles);
+  } else {
+    if (a.add) hipLaunchKernelGGL((k_lin_fwd_xs<256, true>), grid, block, 0, stream, a, tab, n_tiles);
+    else hipLaunchKernelGGL((k_lin_fwd_xs<256, false>), grid, block, 0, stream, a, tab, n_tiles);
+  }
+  return check_launch("k_lin_fwd_xs");
+}
+
+int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid_out,
+                  hipStream_t stream) {
+  if (a.n >= (int64_t(1) << 31)) return fail(HGNN_E_UNSUPPORTED, "k_lin_bwd_xs: n >= 2^31 rows");
+  const int K = a.k_total;
+  const int64_t n_tiles = cdiv(a.n, 32);
+  const int64_t G = xs_bwd_grid(a.n);
+  *grid_out = (int)G;
+  const bool wg = a.slab != nullptr;
+  const dim3 grid((unsigned)G), block(kThr);
+  if (dx && K != 128) return fail(HGNN_E_UNSUPPORTED, "k_lin_bwd_xs: dgrad needs K = 128");
+  bool acc = false;
+  for (int c = 0; c < K / 16; ++c) acc |= tab.dx[c] && ((tab.dx_acc >> c) & 1u);
+#define HGNN_BXS(KV, DXV, WGV, ACCV) \
+  hipLaunchKernelGGL((k_lin_bwd_xs<KV, DXV, WGV, ACCV>), grid, block, 0, stream, a, tab, n_tiles)
+  if (K == 128 && dx) {
+    if (wg) { if (acc) HGNN_BXS(128, true, true, true); else HGNN_BXS(128, true, true, false); }
+    else { if (acc) HGNN_BXS(128, true, false, true); else HGNN_BXS(128, true, false, false); }
+  } else if (K == 128) {
+    HGNN_BXS(128, false, true, false);
+  } else {
+    HGNN_BXS(256, false, true, false);
+  }
+#undef HGNN_BXS
+  return check_launch("k_lin_bwd_xs");
+}
+
+}  // namespace hgnn

@@ -945,10 +945,13 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     st["p_chunks"] = [(q * S, (q + 1) * S, None if q == r else works[q].wait)
                                       for q in order]
                 else:                             # own block, blocks below it, blocks above it
+                    # each range waits on every broadcast it reads (stream waits, free): no
+                    # reliance on the backend finishing them in issue order
+                    def wait_all(qs):
+                        return (lambda: [works[q].wait() for q in qs]) if qs else None
                     st["p_chunks"] = [(r * S, (r + 1) * S, None),
-                                      (0, r * S, works[r - 1].wait if r > 0 else None),
-                                      ((r + 1) * S, W * S, works[W - 1].wait if r + 1 < W
-                                       else None)]
+                                      (0, r * S, wait_all(range(0, r))),
+                                      ((r + 1) * S, W * S, wait_all(range(r + 1, W)))]
                 ag = _AllOf(works)
             else:
                 st["y_p"], ag = env.all_gather_async(table) if multi else (table, None)
