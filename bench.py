@@ -90,7 +90,8 @@ def parse(argv=None):
     p.add_argument("--full-batch", action="store_true",
                    help="cfg5: the full-graph 4-relation step instead of the sampled mini-batches")
     p.add_argument("--batch-seeds", type=int, default=1024,
-                   help="cfg5 mini-batch: seed users and seed posts per batch per rank")
+                   help="cfg5 mini-batch: positive engages edges per batch per rank (one uniform "
+                        "negative post each; the seeds are their distinct endpoints)")
     p.add_argument("--torch-loss", action="store_true",
                    help="cfg5 mini-batch: the link loss as torch ops instead of the fused kernels")
     p.add_argument("--no-graph", action="store_true",
@@ -107,8 +108,9 @@ def parse(argv=None):
                    help="default: the box's allotted CPUs (OMP_NUM_THREADS / affinity)")
     p.add_argument("--cpu-sample-scale", type=float, default=None,
                    help="cfg5: the CPU baseline's down-scaled sample")
-    p.add_argument("--cpu-steps", type=int, default=3,
-                   help="timed CPU-baseline steps (median; after one warm-up)")
+    p.add_argument("--cpu-steps", type=int, default=None,
+                   help="timed CPU-baseline steps (median; after one warm-up; default 1 for "
+                        "cfg4's 1/8 shard, ~62 s each on 16 cores, else 3)")
     p.add_argument("--cpu-shard", type=int, default=None,
                    help="full-batch configs: time rank 0's 1/S destination shard on the CPU oracle "
                         "(default: cfg4 64, cfg2/cfg3 1 = the whole graph)")
@@ -214,7 +216,7 @@ def cpu_baseline(cfg, threads=None, scale=None):
 # >100 GB per materialised [E, d] relation on the oracle) as a destination shard.  The default
 # cfg4 shard keeps the bench's CPU leg to ~30 s; `--cpu-shard 8` is the verdict's 1/8 shard
 # (about 2 minutes, recorded separately under profiles/).
-CPU_SHARD = {"cfg4": 64}
+CPU_SHARD = {"cfg4": 8}
 
 
 def cpu_baseline_shard(cfg, g, rels, threads=None, shard=None, steps=3, warmup=1):
@@ -575,12 +577,14 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     if rank != 0:
         return None
     roof = _roofline(kern, cfg, world)
+    if roof is not None and not on_cpu and not sharded:
+        roof["one_pass"] = _one_pass_k1(g, cfg, roof)
     proj = _projection(kern)
     cpu = None
     if not args.no_cpu_baseline and world == 1 and not on_cpu and not sharded:
         if set(et for et, _ in rels) == {synth.ENGAGES, synth.REV_ENGAGES}:
             cpu = cpu_baseline_shard(cfg, g, rels, args.cpu_threads, args.cpu_shard,
-                                     steps=args.cpu_steps)
+                                     steps=args.cpu_steps or (1 if cfg.name == "cfg4" else 3))
         else:
             cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
     strong = world == 1 or not args.weak
@@ -656,9 +660,43 @@ def _roofline(kern, cfg, world, pooled=False):
             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
             "traffic_source": tsrc, "avg_launch_us": round(per_launch_ms * 1e3, 1),
+            "frac_note": ("frac = ALGORITHMIC bytes (SURVEY §8d: one source row per edge) per "
+                          "launch over its time, cache-assisted: a launch is the source-block "
+                          "passes (DESIGN §5) whose ~600 MB slices and the Zipf-hot rows reuse "
+                          "L2 / the Infinity Cache, and PMC FETCH_SIZE counts Infinity-Cache "
+                          "hits too; `traffic` is that PMC count (the passes' output round trips "
+                          "included); `one_pass` is the unblocked gather"),
             "algorithmic_bytes_per_launch": int(per_launch_bytes),
             "bytes_formula": ("4*E*(2+d) + 4*(N_dst+1) + 4*N_dst*d" if weighted
                               else "4*E*(1+d) + 4*(N_dst+1) + 4*N_dst*d")}
+
+
+def _one_pass_k1(g, cfg, roof):
+    """The roofline kernel as ONE pass (no source blocking), timed with HIP events
+    outside the timed region: the same algorithmic bytes over its own time."""
+    from truth_recommendation_gnn_amd import graph as G
+    if not roof["kernel"].startswith("k_gather K1 mean fwd"):
+        return None
+    e = g.edge_index_dict[synth.ENGAGES]
+    csr = G.relation_csr(e, cfg.num_users, cfg.num_posts)
+    x = g.x_dict["user"]
+    keep = ops.GATHER_BLOCK_BYTES
+    ops.GATHER_BLOCK_BYTES = 0
+    try:
+        ops.gather_mean(x, csr)
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        for _ in range(3):
+            ops.gather_mean(x, csr)
+        s1.record()
+        torch.cuda.synchronize()
+        ms = s0.elapsed_time(s1) / 3
+    finally:
+        ops.GATHER_BLOCK_BYTES = keep
+    ach = roof["algorithmic_bytes_per_launch"] / (ms * 1e-3) / 1e9
+    return {"avg_launch_us": round(ms * 1e3, 1), "achieved": round(ach, 1),
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "note": "the same gather in one pass over the 4.6 GB user table (HGNN_GATHER_BLOCK_GB=0)"}
 
 
 def _projection(kern):
@@ -679,7 +717,9 @@ def _projection(kern):
            "hbm_GB/s": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1),
            "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 1),
            "flops_per_launch": int(r["flops"] / r["launches"]),
-           "flops_formula": "2*N*K*H (K = sum of the input segments)"}
+           "flops_formula": "2*N*K*H (K = sum of the input segments)",
+           "hbm_frac": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "bytes_formula": "4*N*(K+H) (inputs read once, output written once)"}
     if x6:
         # H = 128, K = 128/256 run on bf16 MFMA as an fp32-exact three-piece split:
         # six bf16 products per fp32 product, so its own MFMA ceiling is 1/6 of the dense bf16
@@ -687,18 +727,30 @@ def _projection(kern):
         out["method"] = ("bf16x6: fp32-exact 3-piece bf16 split, 6 v_mfma_f32_16x16x32_bf16 "
                          "products per fp32 product, f32 accumulate")
         out["split_mfma_ceiling_TFLOPs"] = round(BF16_MFMA_PEAK_TFS / 6, 1)
+        out["note"] = ("on the split the kernel's roof is HBM (hbm_frac; the split's MFMA "
+                       "ceiling is 2.5 PF / 6 at the nominal clock); `frac` keeps the fp32-MFMA "
+                       "view of earlier rounds")
     return out
 
 
 # ----------------------------------------------------------------------------- cfg5 mini-batch
+def _pad_rows(v, n):
+    """The eager step's seed rows padded to the captured capacity (the link loss's shape)."""
+    if int(v.shape[0]) == n:
+        return v
+    return torch.cat([v, v.new_zeros((n - int(v.shape[0]),) + tuple(v.shape[1:]))])
+
+
 def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     """BASELINE cfg5: the 4-relation graph (cfg4 + 90M user->user follows + 10M post->post),
     neighbour-sampled (fanout [15, 10], PyG NeighborLoader semantics, ``sampler.py``), one
-    mini-batch of ``--batch-seeds`` seed users + seed posts per rank per step: sample -> 2-layer
-    hetero SAGE on the blocks (K1/K2/K3) -> link loss on the seed pairs -> backward -> Adam.
-    N ranks are data-parallel (each holds the graph, samples its own slice of the epoch's seed
-    order; one RCCL all-reduce of the weight gradients per step).  Edges = the sampled message
-    edges of every block and relation (what the gathers aggregate), summed over ranks."""
+    link-prediction mini-batch of ``--batch-seeds`` positive engages edges per rank per step
+    (one uniform negative post each; seeds = their distinct endpoints): sample -> 2-layer hetero
+    SAGE on the blocks (K1/K2/K3) -> the reference's link loss over the batch's pairs ->
+    backward -> Adam.  N ranks are data-parallel (each holds the graph, takes its own slice of
+    the epoch's edge order; one RCCL all-reduce of the weight gradients per step, between the
+    two graph replays).  Edges = the sampled message edges of every block and relation (what the
+    gathers aggregate), summed over ranks."""
     from truth_recommendation_gnn_amd import minibatch, ops, sampler
     if dev.type == "cpu":
         raise SystemExit("the cfg5 mini-batch bench runs the HIP sampler: no CPU rehearsal")
@@ -717,14 +769,21 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
             dist.broadcast(p.data, 0)
     # one rank: the step (forward, loss, backward, Adam) replayed as a HIP graph over
     # static-capacity blocks (minibatch.py); the sampler stays eager (two syncs per hop)
-    use_graph = not args.no_graph and world == 1
+    # the step (forward, loss, backward, Adam) replayed as a HIP graph over static-capacity
+    # blocks (minibatch.py); the sampler stays eager (two syncs per hop).  N > 1: the forward +
+    # loss + backward graph, the eager all-reduce of the gradients, then the Adam graph.
+    use_graph = not args.no_graph
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
     gen = torch.Generator(device=dev).manual_seed(0)
-    # one shuffle per epoch, as a loader over the seed nodes does; batches are slices of it
-    order = {"user": torch.randperm(cfg.num_users, device=dev, generator=gen),
-             "post": torch.randperm(cfg.num_posts, device=dev, generator=gen)}
+    gen_neg = torch.Generator(device=dev).manual_seed(1)
+    # link prediction as a link loader does it: one shuffle of the positive (engages) edges per
+    # epoch, each batch a slice of B of them; their endpoints and one uniform negative post per
+    # positive (train_gnn.py:259-273) are the seeds
+    pos_ei = g.edge_index_dict[synth.ENGAGES]
+    n_pos = int(pos_ei.shape[1])
+    order = torch.randperm(n_pos, device=dev, generator=gen, dtype=torch.int32)
     nb = args.batch_seeds
-    per_epoch = min(cfg.num_users, cfg.num_posts) // (nb * world)
+    per_epoch = n_pos // (nb * world)
     state = {"b": 0, "edges": 0}
     # the next batch is sampled on a side stream while this one's forward / backward runs: the
     # sampler's two host syncs per hop then wait for the sampling kernels only, not for the
@@ -737,60 +796,74 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
     def sample(b):
         gb = (b % max(per_epoch, 1)) * world + rank            # this rank's slice of the order
-        seeds = {t: o[gb * nb:(gb + 1) * nb] for t, o in order.items()}
+        ids = order[gb * nb:(gb + 1) * nb].long()
+
+        def make():
+            lb = minibatch.link_batch(pos_ei, ids, cfg.num_posts, generator=gen_neg)
+            lb.mb = s.sample(lb.seeds, seed=gb)
+            return lb
         if side is None:
-            return s.sample(seeds, seed=gb), None
+            return make(), None
         with torch.cuda.stream(side):
-            mb = s.sample(seeds, seed=gb)
+            lb = make()
         ev = torch.cuda.Event()
         ev.record(side)
-        return mb, ev
+        return lb, ev
 
     nxt = [None]
-
-    # link loss on the (seed user i, seed post i) pairs with seed post i - 1 as the negative:
-    # the reference's loss (train_gnn.py:259-281, BCE-with-logits means, unit edge weights) through
-    # the library's fused loss kernels (a dozen launches where the torch expression took ~25)
-    pairs = torch.arange(nb, device=dev)
-    pos_pairs = torch.stack([pairs, pairs])
-    neg_pairs = ((pairs - 1) % nb).to(torch.int32)
-    one = torch.ones((), device=dev)
+    # capacities: B user seeds, 2B post seeds (positives + negatives); a batch's distinct
+    # endpoints fill a prefix, the rest are padded rows the loss never reads
+    n_seeds = {"user": nb, "post": 2 * nb}
+    link_loss = minibatch.LinkLoss(nb, n_seeds["user"], n_seeds["post"], dev, n_total=nb * world)
 
     def loss_of(out):
         if args.torch_loss:
             u, p = out["user"], out["post"]
-            pos = (u * p).sum(1)
-            neg = (u * p.roll(1, 0)).sum(1)
-            return (torch.nn.functional.softplus(-pos).mean()
-                    + torch.nn.functional.softplus(neg).mean())
-        return ops.edge_bce_loss(out["user"], out["post"], pos_pairs, neg_pairs, None,
-                                 neg_order="user", check=False, cscale=one)
+            pu, pp, pn = link_loss.uop.long(), link_loss.col.long(), link_loss.neg.long()
+            pos = (u[pu] * p[pp]).sum(1)
+            neg = (u[pu] * p[pn]).sum(1)
+            return (torch.nn.functional.softplus(-pos).sum()
+                    + torch.nn.functional.softplus(neg).sum()) / (nb * world)
+        return link_loss(out)
+
+    loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
+
+    def sync():
+        parallel.sync_grads(model, env)          # no-op at world size 1
 
     captured = None
     if use_graph:
         # the capture's two warm-up passes are training steps on batch 0 (then recorded once)
-        captured = minibatch.CapturedStep(model, g.x_dict, s, {"user": nb, "post": nb}, loss_of,
-                                          opt)
-        captured.capture(sample(0)[0], warmup=2)
+        captured = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_of, opt,
+                                          between=sync if world > 1 else None)
+        lb0 = sample(0)[0]
+        link_loss.load(lb0.pu, lb0.pp, lb0.pn)
+        captured.capture(lb0.mb, warmup=2)
 
-    def eager(mb):
-        out = sampler.forward_blocks(model, mb, g.x_dict)
-        loss = loss_of(out)
+    def eager(lb):
+        link_loss.make_csr()
+        out = sampler.forward_blocks(model, lb.mb, g.x_dict)
+        loss = loss_of({t: v if t not in n_seeds else _pad_rows(v, n_seeds[t])
+                        for t, v in out.items()})
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        parallel.sync_grads(model, env)          # no-op at world size 1
+        sync()
         opt.step()
         return loss
 
     def step(graph=True):
-        mb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
+        lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
         state["b"] += 1
         if ev is not None:
             main = torch.cuda.current_stream(dev)
             main.wait_event(ev)
-            mb.record_stream(main)
+            lb.mb.record_stream(main)
+            for t in (lb.pu, lb.pp, lb.pn):
+                t.record_stream(main)
+        mb = lb.mb
         state["edges"] += sum(blk.csr[et].num_edges for blk in mb.blocks for et in blk.csr)
-        loss = captured.step(mb) if (graph and captured is not None) else eager(mb)
+        link_loss.load(lb.pu, lb.pp, lb.pn)     # on this stream: the running step reads them
+        loss = captured.step(mb) if (graph and captured is not None) else eager(lb)
         if side is not None:
             nxt[0] = sample(state["b"])          # under this step's GPU work
         return loss
@@ -832,14 +905,19 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         "config": {"workload": f"{cfg.name} neighbour-sampled: U={cfg.num_users} "
                                f"P={cfg.num_posts} E_engage={cfg.num_engages} (+reverse) "
                                f"social={cfg.num_social} post_post={cfg.num_post_post}, "
-                               f"d=h={cfg.dim}, fanout {fanouts}, {nb}+{nb} seeds per rank per "
-                               "step, sample + 2-layer fwd + loss + bwd + Adam",
+                               f"d=h={cfg.dim}, fanout {fanouts}, link prediction: {nb} "
+                               "positive engages edges + 1 uniform negative post each per rank "
+                               "per step, seeds = their distinct endpoints; sample + 2-layer fwd "
+                               "+ loss + bwd + Adam",
                    "edges_per_step": round(edges / args.steps),
-                   "global_batch": 2 * nb * world,
+                   "global_batch": nb * world,
                    "batches_per_s": round(world * args.steps / elapsed, 1),
                    "parallelism": f"data-parallel x{world}" if world > 1 else "single",
-                   "execution": ("one HIP graph replay per step over static-capacity blocks "
-                                 "(sampler eager)" if captured is not None else "eager")
+                   "execution": (("one HIP graph replay per step over static-capacity blocks "
+                                  if world == 1 else "HIP graph replays per step (forward + loss "
+                                  "+ backward; eager gradient all-reduce; Adam) over "
+                                  "static-capacity blocks ") + "(sampler eager)"
+                                 if captured is not None else "eager")
                    + (", next batch sampled on a side stream" if side is not None else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),
         "cpu_baseline": cpu,

@@ -644,9 +644,9 @@ def test_sample_negatives_uniform_and_seeded():
                                       (16384 * 5, 1000), (12_345, 2**17),
                                       (70_000_001, 1_000_000)])   # > 2^26 draws, ragged last tile
 def test_draw_sort_negatives_is_draw_then_sort(E, n_keys):
-    """hgnn_draw_sort_negatives (draws computed inside the sort's first pass; for keys up to 2^20
-    the two-level grouping of csrc/negatives.hip) is bit for bit hgnn_uniform_i32 followed by
-    hgnn_sort_pairs_i32 (the LSD radix sort), and a stable sort (numpy) of the draws."""
+    """hgnn_draw_sort_negatives (draws computed inside the sort's first pass) is bit for bit
+    hgnn_uniform_i32 followed by hgnn_sort_pairs_i32 (the LSD radix sort), and a stable sort
+    (numpy) of the draws."""
     from truth_recommendation_gnn_amd import _native as Nn
     lib, s = Nn.lib(), Nn.stream_ptr(torch.device(DEV))
     seed = torch.tensor([0x1234_5678_9ABC_DEF], dtype=torch.int64, device=DEV)

@@ -186,6 +186,115 @@ def test_captured_step_layouts(case):
     for k, p in model.named_parameters():
         if p.grad is not None:
             _close(got[k], p.grad, k)
-    with pytest.raises(ValueError, match="seeds"):
-        step.step(s.sample({"user": torch.arange(n - 1, device=DEV),
+    with pytest.raises(ValueError, match="exceed"):
+        step.step(s.sample({"user": torch.arange(n + 1, device=DEV),
                             "post": torch.arange(n, device=DEV)}))
+
+
+# ----------------------------------------------------------------------------- link batches (cfg5)
+def _link_setup(B=48, fanouts=(5, 3)):
+    from truth_recommendation_gnn_amd import minibatch, synth
+    g, s, _, make_model, _ = _setup(fanouts=fanouts)
+    ei = g.edge_index_dict[synth.ENGAGES]
+    P = g.x_dict["post"].shape[0]
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    order = torch.randperm(int(ei.shape[1]), device=DEV, generator=gen)
+
+    def batch(b):
+        lb = minibatch.link_batch(ei, order[b * B:(b + 1) * B], int(P), generator=gen)
+        lb.mb = s.sample(lb.seeds, seed=b)
+        return lb
+    return g, s, batch, make_model, ei, int(P), {"user": B, "post": 2 * B}
+
+
+def test_link_batch_positives_are_graph_edges():
+    """cfg5's batches are link prediction on real edges: every positive pair is an
+    engages edge of the graph, the negatives are posts, the seeds are the distinct endpoints
+    (sorted), and the local ids index the seeds (= the sampled outputs' rows)."""
+    g, s, batch, _, ei, P, _ = _link_setup()
+    U = int(g.x_dict["user"].shape[0])
+    keys = ei[0].long() * P + ei[1].long()
+    for b in (0, 1, 7):
+        lb = batch(b)
+        assert bool(torch.isin(lb.pos_u.long() * P + lb.pos_p.long(), keys).all())
+        assert int(lb.neg_p.min()) >= 0 and int(lb.neg_p.max()) < P
+        for t, n_max in (("user", U), ("post", P)):
+            sd = lb.seeds[t]
+            assert bool((sd[1:] > sd[:-1]).all()) and int(sd.max()) < n_max
+        assert torch.equal(lb.seeds["user"][lb.pu], lb.pos_u)
+        assert torch.equal(lb.seeds["post"][lb.pp], lb.pos_p)
+        assert torch.equal(lb.seeds["post"][lb.pn], lb.neg_p)
+        assert torch.equal(lb.mb.nodes[-1]["user"].long(), lb.seeds["user"])
+
+
+def _ref_link_loss(out, lb):
+    """The reference's loss on the batch's pairs (train_gnn.py:259-281, unit edge weights)."""
+    u, p = out["user"], out["post"]
+    pos = (u[lb.pu] * p[lb.pp]).sum(1)
+    neg = (u[lb.pu] * p[lb.pn]).sum(1)
+    return (torch.nn.functional.softplus(-pos).mean()
+            + torch.nn.functional.softplus(neg).mean())
+
+
+def test_captured_link_step_matches_reference_loss():
+    """The captured link-prediction step (static capacities: B users, 2B posts; the fused loss
+    over the pairs, its post grouping built inside the graph) against the eager block forward
+    with the reference loss as torch ops, on new batches: loss and every gradient."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, batch, make_model, _, _, n_seeds = _link_setup()
+    B = n_seeds["user"]
+    model = make_model()
+    ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, None, slack=16)
+    lb0 = batch(0)
+    ll.load(lb0.pu, lb0.pp, lb0.pn)
+    step.capture(lb0.mb)
+    for b in (1, 2, 6):
+        lb = batch(b)
+        ll.load(lb.pu, lb.pp, lb.pn)
+        got_loss = float(step.step(lb.mb))
+        got = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+        ref_model = make_model()
+        ref_model.load_state_dict(model.state_dict())
+        ref = _ref_link_loss(sampler.forward_blocks(ref_model, lb.mb, g.x_dict), lb)
+        ref.backward()
+        assert abs(got_loss - float(ref)) <= 2e-6 * abs(float(ref)), (got_loss, float(ref))
+        for n, p in ref_model.named_parameters():
+            _close(got[n], p.grad, n)
+
+
+def test_captured_link_step_with_gradient_hook_trains_like_eager():
+    """The data-parallel form of the captured step: forward + loss + backward replayed, an eager
+    hook on the gradients (parallel.sync_grads' all-reduce at N > 1; here a stand-in that scales
+    them), then the replayed Adam step — against the same training steps run eagerly."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, batch, make_model, _, _, n_seeds = _link_setup()
+    B = n_seeds["user"]
+    model, ref = make_model(), make_model()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=True)
+    ref_opt = torch.optim.Adam(ref.parameters(), lr=1e-3, fused=True)
+
+    def hook(m):
+        for p in m.parameters():
+            if p.grad is not None:
+                p.grad.mul_(0.5)
+    ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, opt, slack=16,
+                                  between=lambda: hook(model))
+    lb0 = batch(0)
+    ll.load(lb0.pu, lb0.pp, lb0.pn)
+    step.capture(lb0.mb, warmup=2)
+    assert step.graph_opt is not None
+    losses = []
+    for lb in [lb0, lb0] + [batch(b) for b in (1, 2, 3)]:
+        if lb is not lb0:
+            ll.load(lb.pu, lb.pp, lb.pn)
+            losses.append(float(step.step(lb.mb)))
+        ref_opt.zero_grad(set_to_none=True)
+        _ref_link_loss(sampler.forward_blocks(ref, lb.mb, g.x_dict), lb).backward()
+        hook(ref)
+        ref_opt.step()
+    torch.cuda.synchronize()
+    for (n, p), (_, r) in zip(model.named_parameters(), ref.named_parameters()):
+        _close(p.detach(), r.detach(), n)
+    assert all(np.isfinite(losses))

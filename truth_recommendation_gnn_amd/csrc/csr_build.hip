@@ -9,7 +9,6 @@
 #include "hgnn_common.h"
 
 #include <stdlib.h>
-#include <string.h>
 
 namespace hgnn {
 
@@ -567,10 +566,8 @@ int hgnn_coo_to_csr(const int64_t* key, const int64_t* other, int64_t E, int64_t
 }
 
 size_t hgnn_sort_pairs_ws_bytes(int64_t E, int64_t n_keys) {
-  const size_t lsd = sort_ws_bytes(E < 1 ? 1 : E);
-  if (!negatives_two_level_applies(E, n_keys)) return lsd;
-  const size_t two = negatives_two_level_ws_bytes(E, n_keys);   // hgnn_draw_sort_negatives
-  return lsd > two ? lsd : two;
+  (void)n_keys;
+  return sort_ws_bytes(E < 1 ? 1 : E);
 }
 
 int hgnn_sort_pairs_i32(const int32_t* keys, const int32_t* a, const int32_t* b, int64_t E,
@@ -801,14 +798,6 @@ int hgnn_draw_sort_negatives(const uint64_t* d_seed, const int32_t* a, int64_t E
                        n_keys + 1, 0);
     return check_launch("draw_sort_negatives(empty)");
   }
-  // the two-level grouping of negatives.hip (keys <= 2^20) only under HGNN_NEG_SORT=2level: as
-  // measured so far it loses to the 3-pass LSD sort below (cfg4: 5.5-5.9 vs 3.1 ms)
-  static const bool two_level =
-      getenv("HGNN_NEG_SORT") && strcmp(getenv("HGNN_NEG_SORT"), "2level") == 0;
-  if (two_level && negatives_two_level_applies(E, n_keys) &&
-      ws_bytes >= negatives_two_level_ws_bytes(E, n_keys))
-    return negatives_two_level(d_seed, a, E, n_keys, neg_out, rowptr, a_sorted, ws, ws_bytes,
-                               stream);
   if (ws_bytes < sort_ws_bytes(E))
     return fail(HGNN_E_WS, "draw_sort_negatives: workspace too small");
   Workspace w(ws, ws_bytes);

@@ -148,11 +148,5 @@ __device__ __forceinline__ int32_t uniform_draw(uint64_t seed, int64_t i, uint32
 int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, size_t* ws_bytes,
                        hipStream_t stream);
 
-// negatives.hip: the two-level draw + grouping behind hgnn_draw_sort_negatives (keys <= 2^20)
-bool negatives_two_level_applies(int64_t E, int64_t n_keys);
-size_t negatives_two_level_ws_bytes(int64_t E, int64_t n_keys);
-int negatives_two_level(const uint64_t* d_seed, const int32_t* a, int64_t E, int64_t n_keys,
-                        int32_t* neg_out, int32_t* rowptr, int32_t* a_sorted, void* ws,
-                        size_t ws_bytes, hipStream_t stream);
 
 }  // namespace hgnn

@@ -2018,18 +2018,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
         a.slab = static_cast<float*>(ws);
       }
       int G = 0;
-      if (any_dx && K != 128) {
-        // dgrad on the per-wave split kernel (it writes the masked dz when asked), then the
-        // wgrad from dout and the mask as before
-        const int64_t n16 = cdiv(n_rows, 16);
-        const int64_t streams = cdiv(std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 128)), 8) * 8;
-        hipLaunchKernelGGL((k_linear_dgrad_x6<256, 128>), dim3((unsigned)(2 * streams)), dim3(512),
-                           0, stream, a, tab, n16);
-        if (int rc = check_launch("k_linear_dgrad_x6")) return rc;
-        if (!wg) return HGNN_OK;
-        a.dz_out = nullptr;
-        if (int rc = xs_linear_bwd(a, tab, false, &G, stream)) return rc;
-      } else if (any_dx || wg) {
+      if (any_dx || wg) {
         if (int rc = xs_linear_bwd(a, tab, any_dx, &G, stream)) return rc;
       }
       if (!wg) return HGNN_OK;

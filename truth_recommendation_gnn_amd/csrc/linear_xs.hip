@@ -185,10 +185,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
       }
       __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
     }
-    if constexpr (PROBE != 2) xs.issue(xr, (t + G) * R, last);
+    if constexpr ((PROBE & 2) == 0) xs.issue(xr, (t + G) * R, last);
     __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
     const unsigned short* p = pl[b];
     f32x4 hi[RT], lo[RT];
+    if constexpr ((PROBE & 4) == 0) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -197,8 +198,28 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
         const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
         const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
-        if constexpr (PROBE != 1) x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
+        if constexpr ((PROBE & 1) == 0) x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
         else { hi[r][0] += (float)x1[0]; lo[r][1] += (float)x2[1] + (float)x3[2]; }
+      }
+    }
+    } else {   // fragments read one k-step ahead
+      bf16x8_t f[2][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) f[0][q] = row8<LDP>(p + q * PS, 0, 0, i, g);
+#pragma unroll
+      for (int r = 0; r < RT; ++r) {
+        hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int c = (r * KS + s) & 1;
+          const int rn = s + 1 < KS ? r : r + 1, sn = s + 1 < KS ? s + 1 : 0;
+          if (rn < RT) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) f[c ^ 1][q] = row8<LDP>(p + q * PS, 16 * rn, 32 * sn, i, g);
+          }
+          if constexpr ((PROBE & 1) == 0) x6_mma(wa[s], f[c][0], f[c][1], f[c][2], hi[r], lo[r]);
+          else { hi[r][0] += (float)f[c][0][0]; lo[r][1] += (float)f[c][1][1] + (float)f[c][2][2]; }
+        }
       }
     }
     // the stored rows' registers are reserved until here (see above)
@@ -225,15 +246,16 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
 // ---------------------------------------------------------------- backward
 // Per 32-row tile: dz = dout masked by the ReLU bits (or by out > 0, or none), written to dz_out
 // when asked, summed for db, split into planes; X split into planes.  Then
-//   DX: dX^T = W^T dz^T (wave w owns dX columns 16 w .. +15 = chunk w; K = 128): A = W^T pieces
-//       in VGPRs, B = dz row fragments;
+//   DX: dX^T = W^T dz^T (wave w owns the dX column tiles w + 8 u, u < K / 128 — 16-column
+//       chunks of the ChunkTab); A = W^T pieces in VGPRs, B = dz row fragments (K = 256 with
+//       the wgrad too would not fit the registers: the host runs that as two launches);
 //   WG: dW += dz^T X over the tile's 32 rows (one MFMA k-step): wave w owns dW columns
 //       [KW w, KW w + KW), KW = K / 8, every h; A = transposed dz fragments, B = transposed X.
 // The block's dW / db partials go to its slab [H][K + 1] (k_wgrad_reduce sums them in order).
 template <int K, bool DX, bool WG, bool ACC>
 __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const ChunkTab tab,
                                                         int64_t n_tiles) {
-  static_assert(!DX || K == 128, "dgrad: one 16-column chunk per wave");
+  static_assert(!(DX && WG) || K == 128, "dgrad + wgrad in one pass: K = 128");
   constexpr int R = 32, LDZ = kH + 16, LDX = K + 16, ZS = R * LDZ, XS = R * LDX;
   constexpr int KT = K / 128;      // 16-column k tiles of dW per wave
   constexpr int HS = kH / 32;      // dgrad MFMA k-steps (reduction over h)
@@ -245,17 +267,21 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   const int64_t G = gridDim.x;
   const bool bits = a.mask_in != nullptr;
   const bool masked = !bits && a.out_act != nullptr;
-  // dgrad: W^T pieces of dX columns 16 w + i, h = 32 s + 8 g .. +7
-  bf16x8_t wt[DX ? HS : 1][3];
+  // dgrad: W^T pieces of dX columns 16 (w + 8 u) + i, h = 32 s + 8 g .. +7
+  constexpr int DT = DX ? KT : 1;
+  bf16x8_t wt[DT][DX ? HS : 1][3];
   if constexpr (DX) {
 #pragma unroll
-    for (int s = 0; s < HS; ++s) {
-      float f[8];
+    for (int u = 0; u < DT; ++u)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) f[e] = a.w[(int64_t)(32 * s + 8 * g + e) * K + 16 * w + i];
-      x6_split8(make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]),
-                wt[s][0], wt[s][1], wt[s][2]);
-    }
+      for (int s = 0; s < HS; ++s) {
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          f[e] = a.w[(int64_t)(32 * s + 8 * g + e) * K + 16 * (w + 8 * u) + i];
+        x6_split8(make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]),
+                  wt[u][s][0], wt[u][s][1], wt[u][s][2]);
+      }
   }
   // dz staging: float4 j of thread t at row (t >> 5) + 16 j, columns 4 (t & 31) .. +3
   constexpr int ZL = 2;
@@ -305,14 +331,16 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   for (int h = 0; h < (WG ? 8 : 1); ++h)
 #pragma unroll
     for (int u = 0; u < KT; ++u) hw[h][u] = lw[h][u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // dgrad: this wave's dX columns are chunk w (K = 128), loop-invariant
-  float* dxp = nullptr;
-  int64_t dxld = 0;
-  bool acc_dx = false;
-  if constexpr (DX) {
-    dxp = tab.dx[w] ? tab.dx[w] + tab.col[w] : nullptr;
-    dxld = tab.ld[w];
-    acc_dx = (tab.dx_acc >> w) & 1u;
+  // dgrad: this wave's dX column tiles are chunks w + 8 u, loop-invariant
+  float* dxp[DT];
+  int64_t dxld[DT];
+  bool acc_dx[DT];
+#pragma unroll
+  for (int u = 0; u < DT; ++u) {
+    const int c = w + 8 * u;
+    dxp[u] = DX && tab.dx[c] ? tab.dx[c] + tab.col[c] : nullptr;
+    dxld[u] = DX ? tab.ld[c] : 0;
+    acc_dx[u] = DX && ((tab.dx_acc >> c) & 1u);
   }
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   issue(t);
@@ -322,30 +350,35 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     const int b = it & 1;
     // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
     // wait leaves the prefetch in flight
-    float4 dxo[ACC ? R / 16 : 1];
+    float4 dxo[DT][ACC ? R / 16 : 1];
     if constexpr (ACC) {
-      if (dxp) {
 #pragma unroll
-        for (int r = 0; r < R / 16; ++r)
-          dxo[r] = *reinterpret_cast<const float4*>(
-              dxp + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld + 4 * g);
+      for (int u = 0; u < DT; ++u) {
+        if (dxp[u]) {
+#pragma unroll
+          for (int r = 0; r < R / 16; ++r)
+            dxo[u][r] = *reinterpret_cast<const float4*>(
+                dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     issue(t + G);   // consumed by put() at the end of this iteration, unconditionally (see forward)
     __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
     const unsigned short* z = zp[b];
-    f32x4 dh[DX ? R / 16 : 1], dl[DX ? R / 16 : 1];
+    f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
     if constexpr (DX) {
 #pragma unroll
       for (int r = 0; r < R / 16; ++r) {
-        dh[r] = dl[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < DT; ++u) dh[u][r] = dl[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < HS; ++s) {
           const bf16x8_t x1 = row8<LDZ>(z, 16 * r, 32 * s, i, g);
           const bf16x8_t x2 = row8<LDZ>(z + ZS, 16 * r, 32 * s, i, g);
           const bf16x8_t x3 = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s, i, g);
-          x6_mma(wt[s], x1, x2, x3, dh[r], dl[r]);
+#pragma unroll
+          for (int u = 0; u < DT; ++u) x6_mma(wt[u][s], x1, x2, x3, dh[u][r], dl[u][r]);
         }
       }
     }
@@ -367,20 +400,22 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     }
     if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
 #pragma unroll
-      for (int r = 0; r < R / 16; ++r) {
-        const int64_t row = t * R + 16 * r + i;
-        if (dxp && row < a.n) {
-          float4 v = make_float4(dh[r][0] + dl[r][0], dh[r][1] + dl[r][1], dh[r][2] + dl[r][2],
-                                 dh[r][3] + dl[r][3]);
-          if constexpr (ACC) {
-            if (acc_dx) {
-              v.x = dxo[r].x + v.x; v.y = dxo[r].y + v.y; v.z = dxo[r].z + v.z;
-              v.w = dxo[r].w + v.w;
+      for (int u = 0; u < DT; ++u)
+#pragma unroll
+        for (int r = 0; r < R / 16; ++r) {
+          const int64_t row = t * R + 16 * r + i;
+          if (dxp[u] && row < a.n) {
+            float4 v = make_float4(dh[u][r][0] + dl[u][r][0], dh[u][r][1] + dl[u][r][1],
+                                   dh[u][r][2] + dl[u][r][2], dh[u][r][3] + dl[u][r][3]);
+            if constexpr (ACC) {
+              if (acc_dx[u]) {
+                v.x = dxo[u][r].x + v.x; v.y = dxo[u][r].y + v.y; v.z = dxo[u][r].z + v.z;
+                v.w = dxo[u][r].w + v.w;
+              }
             }
+            *reinterpret_cast<float4*>(dxp[u] + row * dxld[u] + 4 * g) = v;
           }
-          *reinterpret_cast<float4*>(dxp + row * dxld + 4 * g) = v;
         }
-      }
     }
     put(t + G, b ^ 1);
     __syncthreads();
@@ -438,10 +473,12 @@ int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
   const int64_t n_tiles = cdiv(a.n, R);
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 256))), block(kThr);
   static const int probe = getenv("HGNN_XS_PROBE") ? atoi(getenv("HGNN_XS_PROBE")) : 0;
-  if (probe == 1 && K == 256 && !a.add) {
-    hipLaunchKernelGGL((k_lin_fwd_xs<256, false, 1>), grid, block, 0, stream, a, tab, n_tiles);
-  } else if (probe == 2 && K == 256 && !a.add) {
-    hipLaunchKernelGGL((k_lin_fwd_xs<256, false, 2>), grid, block, 0, stream, a, tab, n_tiles);
+  if (probe && K == 256 && !a.add) {
+    switch (probe) {
+#define P(v) case v: hipLaunchKernelGGL((k_lin_fwd_xs<256, false, v>), grid, block, 0, stream, a, tab, n_tiles); break;
+      P(1) P(2) P(4) P(5) P(6)
+#undef P
+    }
   } else if (K == 128) {
     if (a.add) hipLaunchKernelGGL((k_lin_fwd_xs<128, true>), grid, block, 0, stream, a, tab, n_tiles);
     else hipLaunchKernelGGL((k_lin_fwd_xs<128, false>), grid, block, 0, stream, a, tab, n_tiles);
@@ -461,7 +498,6 @@ int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid_out,
   *grid_out = (int)G;
   const bool wg = a.slab != nullptr;
   const dim3 grid((unsigned)G), block(kThr);
-  if (dx && K != 128) return fail(HGNN_E_UNSUPPORTED, "k_lin_bwd_xs: dgrad needs K = 128");
   bool acc = false;
   for (int c = 0; c < K / 16; ++c) acc |= tab.dx[c] && ((tab.dx_acc >> c) & 1u);
 #define HGNN_BXS(KV, DXV, WGV, ACCV) \
@@ -472,7 +508,17 @@ int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid_out,
   } else if (K == 128) {
     HGNN_BXS(128, false, true, false);
   } else {
-    HGNN_BXS(256, false, true, false);
+    // K = 256: the dgrad and the wgrad as two passes (their registers do not fit one wave)
+    if (dx) {
+      if (acc) HGNN_BXS(256, true, false, true); else HGNN_BXS(256, true, false, false);
+      if (int rc = check_launch("k_lin_bwd_xs")) return rc;
+    }
+    if (wg) {
+      LinArgs b = a;
+      b.dz_out = nullptr;   // the dgrad pass wrote it
+      hipLaunchKernelGGL((k_lin_bwd_xs<256, false, true, false>), grid, block, 0, stream, b, tab,
+                         n_tiles);
+    }
   }
 #undef HGNN_BXS
   return check_launch("k_lin_bwd_xs");

@@ -28,6 +28,7 @@ parameter gradient).
 """
 from __future__ import annotations
 
+import dataclasses
 import weakref
 from typing import Callable, Dict, List, Mapping, Optional, Tuple
 
@@ -93,10 +94,11 @@ class StaticBlocks:
         if len(mb.blocks) != self.L:
             raise ValueError(f"{len(mb.blocks)} blocks for {self.L} static levels")
         seeds = mb.nodes[-1]
-        if {t: int(v.numel()) for t, v in seeds.items()} != self.n_seeds:
-            # the loss reads the first n_seeds rows per type: a short batch would feed it padding
-            raise ValueError(f"batch seeds {({t: int(v.numel()) for t, v in seeds.items()})} "
-                             f"!= the captured {self.n_seeds}")
+        got = {t: int(v.numel()) for t, v in seeds.items()}
+        if set(got) != set(self.n_seeds) or any(got[t] > self.n_seeds[t] for t in got):
+            # fewer seeds than the capacity leave padded level-0 rows (a link batch's unique
+            # endpoints vary in number; its loss reads the seed rows by their local ids)
+            raise ValueError(f"batch seeds {got} exceed the captured capacity {self.n_seeds}")
         L = self.L
         rp, col, mp, nd, e, rpo, colo, dcap, ecap, dummy, spread = ([] for _ in range(11))
         for h in range(L):
@@ -201,23 +203,37 @@ class CapturedStep:
     """Forward + ``loss_fn(out)`` + backward (+ ``optimizer.step()``) of a sampled mini-batch,
     captured once on static blocks and replayed per batch.  The optimizer must be capturable
     (``torch.optim.Adam(..., capturable=True)``); gradients live in the graph's memory pool and
-    are rewritten by every replay (zeroed once before capture)."""
+    are rewritten by every replay (zeroed once before capture).
+
+    ``between`` (data-parallel ranks): an eager call between the backward and the optimizer step
+    — ``parallel.sync_grads``'s all-reduce of the gradients — so the step is two replays, the
+    forward + loss + backward graph and the optimizer graph, around it.  A ``loss_fn`` with a
+    ``make_csr()`` method (``LinkLoss``) gets fresh structures before each recorded pass."""
 
     def __init__(self, model: HeteroSAGE, x_dict: Mapping[str, torch.Tensor],
                  smp: NeighborSampler, n_seeds: Mapping[str, int],
                  loss_fn: Callable[[Dict[str, torch.Tensor]], torch.Tensor],
-                 optimizer: Optional[torch.optim.Optimizer] = None, slack: int = SLACK):
+                 optimizer: Optional[torch.optim.Optimizer] = None, slack: int = SLACK,
+                 between: Optional[Callable[[], None]] = None):
         self.model, self.x_dict, self.loss_fn, self.opt = model, x_dict, loss_fn, optimizer
+        self.between = between
         self.blocks = StaticBlocks(smp, n_seeds, slack)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
         self.out: Optional[Dict[str, torch.Tensor]] = None
 
-    def _body(self):
+    def _fresh(self):
+        self.blocks.make_csrs()
+        mk = getattr(self.loss_fn, "make_csr", None)
+        if mk is not None:
+            mk()
+
+    def _body(self, with_opt: bool = True):
         out = self.blocks.forward(self.model, self.x_dict)
         loss = self.loss_fn(out)
         loss.backward()
-        if self.opt is not None:
+        if self.opt is not None and with_opt:
             self.opt.step()
         return out, loss
 
@@ -226,25 +242,34 @@ class CapturedStep:
         these are training steps), then record the step."""
         dev = self.blocks.smp.device
         self.blocks.load(first)
+        split = self.between is not None and self.opt is not None
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(warmup):
-                self.blocks.make_csrs()
+                self._fresh()
                 self._zero_grad()
-                self._body()
+                self._body(with_opt=not split)
+                if split:
+                    self.between()
+                    self.opt.step()
         torch.cuda.current_stream(dev).wait_stream(side)
-        self.blocks.make_csrs()            # fresh: their CSC and 1/deg builds are recorded
+        self._fresh()                      # fresh: their CSC and 1/deg builds are recorded
         self._zero_grad()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            out, loss = self._body()
+            out, loss = self._body(with_opt=not split)
         # the static outputs without the recorded autograd graph (kept alive, its AccumulateGrad
         # nodes would tie later eager backwards of the same parameters to the capture stream)
         self.out = {t: v.detach() for t, v in out.items()}
         self.loss = loss.detach()
         del out, loss
         self.graph = g
+        if split:
+            go = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(go):
+                self.opt.step()
+            self.graph_opt = go
 
     def _zero_grad(self):
         if self.opt is not None:
@@ -258,4 +283,105 @@ class CapturedStep:
             raise RuntimeError("CapturedStep.step before capture()")
         self.blocks.load(mb)
         self.graph.replay()
+        if self.graph_opt is not None:
+            self.between()
+            self.graph_opt.replay()
         return self.loss
+
+
+# ----------------------------------------------------------------------------- link batches
+class _LossCSR:
+    """The grouping ``ops._edge_bce`` reads for a link batch: ``bwd`` = the positive pairs by
+    user (built outside the step), ``fwd`` = the same pairs by post (the transposed grouping of
+    a ``from_csr`` relation: one ``hgnn_csr_transpose`` on first use, no host sync)."""
+
+    def __init__(self, rowptr_u, col_p, uop, n_users: int, n_posts: int):
+        self._rel = RelationCSR.from_csr(rowptr_u, col_p, n_posts, n_users,
+                                         may_have_heavy_rows=False)
+        self.n_src, self.n_dst = int(n_users), int(n_posts)
+        self.num_edges = int(col_p.numel())
+        self._uop = uop
+
+    @property
+    def fwd(self):
+        return self._rel.bwd
+
+    @property
+    def bwd(self):
+        return self._rel.fwd
+
+
+class LinkLoss:
+    """The reference's loss (train_gnn.py:259-281: BCE-with-logits means over the positive
+    edges and over one uniform negative post per positive, unit edge weights) on a link
+    mini-batch, through the library's fused loss kernels (``ops._EdgeBCELoss``) over fixed-size
+    buffers: ``load(pu, pp, pn)`` (local user / post ids of the positives, local post ids of the
+    negatives; no sync) groups the pairs by user into them, ``make_csr()`` makes fresh
+    structures over them (their post grouping is built on first use: inside a capture, per
+    replay).  ``n_total`` = the positives of ALL ranks, so per-rank losses add up to the global
+    batch's mean (data-parallel gradients are summed)."""
+
+    def __init__(self, n_edges: int, n_users: int, n_posts: int, device, n_total: int = 0):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.E, self.n_users, self.n_posts = int(n_edges), int(n_users), int(n_posts)
+        self.n_total = int(n_total) if n_total else self.E
+        self.rowptr = torch.zeros(self.n_users + 1, **i32)
+        self.col = torch.zeros(self.E, **i32)
+        self.neg = torch.zeros(self.E, **i32)
+        self.uop = torch.zeros(self.E, **i32)
+        self.cscale = torch.ones((), dtype=torch.float32, device=device)
+        self.csr: Optional[_LossCSR] = None
+
+    def load(self, pu: torch.Tensor, pp: torch.Tensor, pn: torch.Tensor) -> None:
+        if int(pu.numel()) != self.E:
+            raise ValueError(f"{int(pu.numel())} positives for a {self.E}-edge link loss")
+        order = torch.argsort(pu, stable=True)
+        cnt = torch.zeros(self.n_users + 1, dtype=torch.int64, device=pu.device)
+        cnt.scatter_add_(0, pu.to(torch.int64) + 1, torch.ones_like(pu, dtype=torch.int64))
+        self.rowptr.copy_(torch.cumsum(cnt, 0))
+        self.col.copy_(pp[order])
+        self.neg.copy_(pn[order])
+        self.uop.copy_(pu[order])
+
+    def make_csr(self) -> None:
+        self.csr = _LossCSR(self.rowptr, self.col, self.uop, self.n_users, self.n_posts)
+
+    def __call__(self, out: Mapping[str, torch.Tensor]) -> torch.Tensor:
+        U, P = out["user"], out["post"]
+        if int(U.shape[0]) != self.n_users or int(P.shape[0]) != self.n_posts:
+            raise ValueError(f"link loss over {self.n_users} users / {self.n_posts} posts, got "
+                             f"{tuple(U.shape)} / {tuple(P.shape)}")
+        if self.csr is None:
+            self.make_csr()
+        return ops._EdgeBCELoss.apply(U, P, self.csr, self.neg, self.cscale, False, self.n_total)
+
+
+@dataclasses.dataclass
+class LinkBatch:
+    """A link-prediction mini-batch (PyG LinkNeighborLoader semantics, binary negatives): B
+    positive ``engages`` edges, one uniform negative post per positive (train_gnn.py:272), the
+    seeds = the distinct endpoints (users; posts of the positives and negatives, each sorted),
+    and the pairs as local ids into the seeds (= the sampled outputs' rows)."""
+    pos_u: torch.Tensor      # global ids [B]
+    pos_p: torch.Tensor
+    neg_p: torch.Tensor
+    seeds: Dict[str, torch.Tensor]
+    pu: torch.Tensor         # local ids [B]
+    pp: torch.Tensor
+    pn: torch.Tensor
+    mb: Optional[MiniBatch] = None
+
+
+def link_batch(edge_index: torch.Tensor, edge_ids: torch.Tensor, num_posts: int,
+               generator: Optional[torch.Generator] = None) -> LinkBatch:
+    """The positives ``edge_index[:, edge_ids]`` ((user, post) rows), their negatives drawn
+    uniformly over the posts, the distinct endpoints as seeds (two host syncs: the unique
+    counts)."""
+    pos_u, pos_p = edge_index[0, edge_ids], edge_index[1, edge_ids]
+    neg_p = torch.randint(0, int(num_posts), (int(edge_ids.numel()),), device=pos_u.device,
+                          generator=generator, dtype=pos_u.dtype)
+    su = torch.unique(pos_u)
+    sp = torch.unique(torch.cat([pos_p, neg_p]))
+    return LinkBatch(pos_u, pos_p, neg_p, {"user": su, "post": sp},
+                     torch.searchsorted(su, pos_u), torch.searchsorted(sp, pos_p),
+                     torch.searchsorted(sp, neg_p))
