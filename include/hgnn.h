@@ -273,10 +273,10 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
 
 /* K3 at H = 128 and K = 128 / 256 runs on bf16 MFMA as an fp32-exact three-piece split (each
  * fp32 operand = three bf16 pieces, six piece products per fp32 product, f32 accumulation:
- * fp32-class error) unless HGNN_K3_X6=0.  on = 1 selects the split (the
- * split-once kernels, each operand element split once per block), 2 the round-3 per-wave split
- * kernels (HGNN_K3_XS=0), 0 the f32-input MFMA kernels, for the calls that follow (process-wide,
- * not thread-safe against calls in flight); on < 0 only queries.  Returns the previous setting. */
+ * fp32-class error; each operand element split once per block) unless
+ * HGNN_K3_X6=0.  on = 1 / 0 selects the split or the f32-input MFMA kernels for the calls that
+ * follow (process-wide, not thread-safe against calls in flight); on < 0 only queries.  Returns
+ * the previous setting. */
 int hgnn_set_k3_split(int32_t on);
 
 /* Single-input forms, one PyG Linear at a time (SURVEY §8b names; same kernels as above):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """K3 at the cfg4 step's shapes (HIP events), each result checked against float64 torch: the
-kernel family comes from the environment (HGNN_K3_XS=0: the round-3 per-wave split kernels;
-HGNN_K3_X6=0: the f32-input kernels), read once per process, so run one process per family.
+kernel family comes from the environment (HGNN_K3_X6=0: the f32-input kernels instead of the
+bf16x6 split), read once per process, so run one process per family.
 
   python scripts/k3_xs_bench.py [--rows 9000000] [--post-rows 1000000] [--reps 10]
 
@@ -96,8 +96,7 @@ def case(name, n, ks, relu, add_on, mask_on, bwd_dx, bwd_w, dz_on, reps, dev, g,
         rec.update({"bwd_ms": round(ms_b, 3), "bwd_GBs": round(nbb / ms_b / 1e6, 1),
                     "bwd_frac": round(nbb / ms_b / 1e6 / 8000, 3),
                     "bwd_rel_err": {k: float(f"{v:.2e}") for k, v in e.items()}})
-    rec["family"] = ("f32" if os.environ.get("HGNN_K3_X6") == "0" else
-                     "x6" if os.environ.get("HGNN_K3_XS") == "0" else "xs")
+    rec["family"] = "f32" if os.environ.get("HGNN_K3_X6") == "0" else "bf16x6 split-once"
     out.append(rec)
     print(json.dumps(rec), flush=True)
 

@@ -1043,8 +1043,8 @@ def test_csr_cache_frees_structures_of_dead_edge_tensors():
 # ----------------------------------------------------------------------------- K3 on both paths
 @contextlib.contextmanager
 def _k3_split(on):
-    """K3 family for H = 128, K = 128 / 256: the bf16x6 split, split once per element (1 / True,
-    the default), the round-3 per-wave split kernels (2), the f32-input MFMA kernels (0 / False)."""
+    """K3 at H = 128, K = 128 / 256: the bf16x6 split (True, the default) or the f32-input MFMA
+    kernels (False)."""
     from truth_recommendation_gnn_amd import _native as N
     prev = N.lib().hgnn_set_k3_split(int(on))
     try:
@@ -1053,7 +1053,7 @@ def _k3_split(on):
         N.lib().hgnn_set_k3_split(prev)
 
 
-@pytest.mark.parametrize("split", [0, 1, 2])
+@pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("ks", [[128], [128, 128], [64, 64, 128], [64, 64]])
 def test_linear_h128_on_both_k3_paths(split, ks):
     """The H = 128 shapes the split covers (K = 128 and 256, 128-column segments and others),
@@ -1068,6 +1068,42 @@ def test_linear_h128_on_both_k3_paths(split, ks):
             test_linear_bwd_dx_accumulate_bitwise(ks, 128, masked)
         for mode in ("all", "wgrad_only", "dz_out"):
             test_linear_relu_bits_equal_float_mask(ks, 128, mode)
+
+
+@pytest.mark.parametrize("ks", [[128], [128, 128]])
+@pytest.mark.parametrize("relu", [False, True])
+def test_linear_split_passes_inf_and_nan_like_f32_kernels(ks, relu):
+    """Non-finite inputs: an inf or NaN in X gives the split the +-inf / NaN pattern
+    of the f32-input kernels in the forward, and an inf in dout the same dX, rather than NaN
+    from inf - bf16(inf) in a residual piece or from inf times W's mixed-sign residual pieces."""
+    gen = torch.Generator().manual_seed(7)
+    n, K = 300, sum(ks)
+    segs = [torch.randn(n, k, generator=gen) for k in ks]
+    segs[0][5, 3] = float("inf")
+    segs[-1][9, 17] = float("-inf")
+    segs[0][11, 40] = float("nan")
+    w = torch.randn(128, K, generator=gen) * 0.1
+    b = torch.randn(128, generator=gen)
+    dout = torch.randn(n, 128, generator=gen)
+    dout[20, 7] = float("inf")
+    dout[21, 9] = float("-inf")
+    res = {}
+    for split in (False, True):
+        with _k3_split(split):
+            sd = [s_.to(DEV) for s_ in segs]
+            out = ops.linear_fwd(sd, w.to(DEV), b.to(DEV), relu)
+            dxs = [torch.empty_like(s_) for s_ in sd]
+            finite = [s_.nan_to_num(0.0, 0.0, 0.0) for s_ in sd]
+            ops.linear_bwd(finite, w.to(DEV), dout.to(DEV), None, dxs, False, False)
+            res[split] = (out.cpu(), torch.cat([d.cpu() for d in dxs], 1))
+    for a, c in zip(res[False], res[True]):
+        assert torch.equal(torch.isnan(a), torch.isnan(c))
+        assert torch.equal(torch.isposinf(a), torch.isposinf(c))
+        assert torch.equal(torch.isneginf(a), torch.isneginf(c))
+        fin = torch.isfinite(a)
+        assert bool(torch.isinf(a).any()) or relu
+        scale = float(a[fin].abs().max())
+        assert float((a[fin] - c[fin]).abs().max()) <= 2e-5 * scale
 
 
 def test_k3_split_matches_f32_kernels_closely():

@@ -783,131 +783,6 @@ __global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const
   }
 }
 
-// ================================================================ bf16x6: fp32-exact split
-// gfx950 runs bf16 MFMA at 16x the fp32 MFMA rate (2.5 PF vs 157 TF dense).  Every fp32 value
-// v splits exactly-enough into three bf16 pieces, v1 = bf16(v), v2 = bf16(v - v1),
-// v3 = bf16(v - v1 - v2) (|v - v1 - v2 - v3| <= ~2^-24 |v|), and a product x w becomes the six
-// piece products whose orders add to <= 4: x1w1 | x1w2 + x2w1 + x1w3 + x3w1 + x2w2 (the dropped
-// x2w3, x3w2, x3w3 are <= ~2^-24 |x w|).  Each piece product is exact in f32 and accumulates in
-// f32, so the result has fp32 accuracy: measured at most 0.68 f32 ulp of sum |x w| against
-// double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
-// accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
-// 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
-
-// Forward on the split: persistent, one 8-wave block per CU.  The block's HB output columns of
-// W (HB = 128, or 64 for K = 256, whose three planes for all 128 columns would not fit in LDS:
-// then two blocks take the two column halves of the same tiles, in step, so the second read of
-// a tile's rows mostly hits the caches) are split once into three bf16 planes in LDS; each wave
-// streams 16-row tiles.  Lane (i, g) loads row i's columns 32 s + 8 g .. +7 for k-step s, splits
-// them in registers and re-loads the slot with the next tile's as soon as it is split.  MFMA
-// operands: A = the W planes (rows = output columns), B = X^T, so the lane ends with columns
-// 16 c + 4 g .. +3 of row i: the v4/v5 layout (float4 stores, the same ReLU mask words).
-template <int K, int HB, bool ADD, bool S8>
-__global__ void __launch_bounds__(512, 1) k_linear_fwd_x6(const LinArgs a, const ChunkTab tab,
-                                                          int64_t n_tiles) {
-  // LDB = K + 16 halfwords: rows 32 B apart mod 256, so each 16-lane group of a ds_read_b128
-  // fragment read ({0-3,12-15,20-27}, ...) hits 16 distinct bank quads (K + 8 was 2-way: 4 extra
-  // LDS cycles per read, SQ_LDS_BANK_CONFLICT = 4.0 x SQ_INSTS_LDS in profiles/pmc_k3_cfg4_r3.json)
-  constexpr int NT = HB / 16, KS = K / 32, LDB = K + 16, NH = 128 / HB;
-  __shared__ __attribute__((aligned(16))) unsigned short wp[3][HB * LDB];
-  // NH = 2: blocks b and b + 8 (the same XCD: hardware block b runs on XCD b % 8) take the two
-  // column halves of one tile stream, so the second read of a tile's rows can hit that L2
-  const int hb = NH == 1 ? 0 : (int)((blockIdx.x >> 3) & 1), col0 = hb * HB;
-  const int64_t stream_id = NH == 1 ? blockIdx.x : (blockIdx.x & 7) + 8 * (blockIdx.x >> 4);
-  for (int idx = threadIdx.x; idx < HB * K; idx += 512) {
-    const int j = idx / K, k = idx % K;
-    const float v = a.w[(int64_t)(col0 + j) * K + k];
-    const unsigned short a1 = x6_bf16(v);
-    const float r1 = v - x6_f32(a1);
-    const unsigned short a2 = x6_bf16(r1);
-    wp[0][j * LDB + k] = a1;
-    wp[1][j * LDB + k] = a2;
-    wp[2][j * LDB + k] = x6_bf16(r1 - x6_f32(a2));
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t nw = (int64_t)(gridDim.x / NH) * 8;
-  const int64_t last = a.n - 1;
-  int64_t t = stream_id * 8 + wave;
-  float4 xv[KS][2];
-  auto load_s = [&](int64_t tt, int s) {
-    const float4* p = x_chunk<S8>(tab, min<int64_t>(tt * 16 + i, last), 2 * s + (g >> 1), 0) +
-                      2 * (g & 1);
-    xv[s][0] = p[0];
-    xv[s][1] = p[1];
-  };
-  if (t < n_tiles) {
-#pragma unroll
-    for (int s = 0; s < KS; ++s) load_s(t, s);
-  }
-  __syncthreads();
-  for (; t < n_tiles; t += nw) {
-    const int64_t tn = t + nw < n_tiles ? t + nw : t;
-    const int64_t row = t * 16 + i;
-    int wo = i * LDB + 8 * g;
-    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
-    float4 ad[ADD ? NT : 1];       // the added rows, in flight during the sweep (see Epi)
-    if constexpr (ADD) {
-#pragma unroll
-      for (int c = 0; c < NT; ++c)
-        ad[c] = row < a.n ? *reinterpret_cast<const float4*>(a.add + row * 128 + col0 + 16 * c +
-                                                             4 * g)
-                          : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    f32x4 hi[NT], lo[NT];
-#pragma unroll
-    for (int c = 0; c < NT; ++c) hi[c] = lo[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8_t cw[3], nx[3];
-    auto rd = [&](int s, int c, bf16x8_t (&f)[3]) {
-      const int off = wo + 16 * c * LDB + 32 * s;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8_t*>(&wp[q][off]);
-    };
-    rd(0, 0, cw);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      bf16x8_t x1, x2, x3;
-      x6_split8(xv[s][0], xv[s][1], x1, x2, x3);
-      load_s(tn, s);   // the next tile's k-step s, a whole tile of MFMAs ahead of its use
-#pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        if (c + 1 < NT) rd(s, c + 1, nx);
-        else if (s + 1 < KS) rd(s + 1, 0, nx);
-        x6_mma(cw, x1, x2, x3, hi[c], lo[c]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cw[q] = nx[q];
-      }
-    }
-    if (row < a.n) {
-      uint32_t mbits = 0;
-#pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        const float4 bb = a.bias ? *reinterpret_cast<const float4*>(a.bias + col0 + 16 * c + 4 * g)
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 v = make_float4((hi[c][0] + lo[c][0]) + bb.x, (hi[c][1] + lo[c][1]) + bb.y,
-                               (hi[c][2] + lo[c][2]) + bb.z, (hi[c][3] + lo[c][3]) + bb.w);
-        if constexpr (ADD) {
-          v.x += ad[c].x; v.y += ad[c].y; v.z += ad[c].z; v.w += ad[c].w;
-        }
-        if (a.relu) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        mbits |= relu_bits(v, 4 * c);
-        *reinterpret_cast<float4*>(a.out + row * 128 + col0 + 16 * c + 4 * g) = v;
-      }
-      if (a.mask_out) {
-        // word row * 4 + g holds bit 4 c + e of column tile c (0..7); a column half owns its
-        // 16-bit half of it (no two blocks write the same bytes)
-        if constexpr (NH == 1)
-          a.mask_out[row * 4 + g] = mbits;
-        else
-          reinterpret_cast<unsigned short*>(a.mask_out)[(row * 4 + g) * 2 + hb] =
-              (unsigned short)mbits;
-      }
-    }
-  }
-}
-
 // Backward v4: two roles per SIMD.  512 threads; waves 0-3 ("dz waves") load the masked dz
 // fragments of 16 rows each, run dgrad (dX^T = W^T dz^T, straight from registers) and the bias
 // sums, and publish dz to LDS; waves 4-7 ("X waves") stage the X tile and run wgrad.  dz / X
@@ -1237,122 +1112,6 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
   }
 }
 
-// wgrad on the bf16x6 split (H = 128, K = 128 / 256): dW = dz^T X, db = colsum(dz), 32-row tiles
-// (one k-step of v_mfma_f32_16x16x32_bf16 runs over 32 rows).  Staging: thread (column c, row
-// block rb) loads 8 rows of one column of dz (masked) and of X with dword loads (a wave covers 64
-// consecutive columns of a row: coalesced), splits them and writes each piece plane as one 16-B
-// run of the TRANSPOSED image zt[q][h][row] / xt[q][k][row] (64-B rows, the 16-B chunks XOR-
-// swizzled by (c >> 2) & 3 so the b128 fragment reads of 16 lanes hit 16 distinct bank groups).  Wave w owns output rows
-// h in [16 w, 16 w + 16) and every k tile: per tile 3 + 3 KT fragment reads feed 6 KT MFMAs.
-// NB = 2: double-buffered image, one barrier per tile (144 KB at K = 256); NB = 1: two.  The block's partial dW / db goes to its slab (k_wgrad_reduce).
-template <int K, int NB>
-__global__ void __launch_bounds__(512, 1) k_linear_wgrad_x6(const LinArgs a, const ChunkTab tab,
-                                                            int64_t n_tiles) {
-  constexpr int H = 128, T = 32, KT = K / 16, ZP = T;
-  // element (c, 8-row block r) of a plane at c * ZP + 8 (r ^ ((c >> 1) & 3)): each 16-lane group
-  // of a b128 fragment read ({0-3,12-15,20-27}, ... : lanes (i, g) reading c = 16 k + i, r = g)
-  // lands on 16 distinct bank quads, and so does each 8-lane group of the staging stores (8
-  // consecutive c, one r); r ^ ((c >> 2) & 3) left both 2-way
-  auto sw = [](int c, int r) { return c * ZP + 8 * (r ^ ((c >> 1) & 3)); };
-  constexpr int XR = 512 / K;          // row blocks of 8 over X's K columns (4 or 2)
-  constexpr int XJ = T / XR / 8;       // 8-row groups per thread for X (1 or 2)
-  __shared__ __attribute__((aligned(16))) unsigned short zt[NB][3][H * ZP];
-  __shared__ __attribute__((aligned(16))) unsigned short xt[NB][3][K * ZP];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int zc = threadIdx.x & 127, zrb = threadIdx.x >> 7;     // dz: column, 8-row block
-  const int xc = threadIdx.x % K, xrb = threadIdx.x / K;        // X: column, first 8-row block
-  const float* xseg = tab.x[xc >> 4] + tab.col[xc >> 4] + (xc & 15);
-  const int64_t xld = tab.ld[xc >> 4];
-  const bool bits = a.mask_in != nullptr;
-  const bool masked = !bits && a.out_act != nullptr;
-  const int64_t n_my = (n_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x;
-  const int64_t last = a.n - 1;
-  float zr[8], mr[8], xr[XJ][8];
-  uint32_t br[8];
-  auto issue = [&](int64_t it) {
-    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t row = min<int64_t>(r0 + zrb * 8 + j, last);
-      zr[j] = a.dout[row * H + zc];
-      if (bits) br[j] = a.mask_in[row * 4 + ((zc & 15) >> 2)];
-      if (masked) mr[j] = a.out_act[row * H + zc];
-    }
-#pragma unroll
-    for (int q = 0; q < XJ; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t row = min<int64_t>(r0 + (xrb + q * XR) * 8 + j, last);
-        xr[q][j] = xseg[row * xld];
-      }
-  };
-  f32x4 hi[KT], lo[KT];
-#pragma unroll
-  for (int k = 0; k < KT; ++k) hi[k] = lo[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbacc = 0.f;
-  const int bsh = 4 * (zc >> 4) + (zc & 3);
-  auto put8 = [&](unsigned short* plane0, int pstride, const float (&v)[8]) {
-    bf16x8_t p1, p2, p3;
-    x6_split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p1, p2,
-              p3);
-    *reinterpret_cast<bf16x8_t*>(plane0) = p1;
-    *reinterpret_cast<bf16x8_t*>(plane0 + pstride) = p2;
-    *reinterpret_cast<bf16x8_t*>(plane0 + 2 * pstride) = p3;
-  };
-  if (n_my > 0) issue(0);
-  for (int64_t it = 0; it < n_my; ++it) {
-    const int b = NB == 2 ? (int)(it & 1) : 0;
-    const int64_t r0 = (blockIdx.x + it * gridDim.x) * T;
-    if (NB == 1 && it > 0) __syncthreads();   // the previous tile's MFMA reads are done
-    {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float z = zr[j];
-        if (bits) z = (br[j] >> bsh) & 1u ? z : 0.f;
-        if (masked) z = mr[j] > 0.f ? z : 0.f;
-        if (r0 + zrb * 8 + j >= a.n) z = 0.f;   // clamped rows contribute 0
-        dbacc += z;
-        v[j] = z;
-      }
-      put8(&zt[b][0][sw(zc, zrb)], H * ZP, v);
-#pragma unroll
-      for (int q = 0; q < XJ; ++q) put8(&xt[b][0][sw(xc, xrb + q * XR)], K * ZP, xr[q]);
-    }
-    if (it + 1 < n_my) issue(it + 1);
-    __syncthreads();
-    bf16x8_t af[3];
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      af[q] = *reinterpret_cast<const bf16x8_t*>(&zt[b][q][sw(16 * wave + i, g)]);
-#pragma unroll
-    for (int k = 0; k < KT; ++k) {
-      const int off = sw(16 * k + i, g);
-      const bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(&xt[b][0][off]);
-      const bf16x8_t b2 = *reinterpret_cast<const bf16x8_t*>(&xt[b][1][off]);
-      const bf16x8_t b3 = *reinterpret_cast<const bf16x8_t*>(&xt[b][2][off]);
-      x6_mma(af, b1, b2, b3, hi[k], lo[k]);
-    }
-  }
-  constexpr int KEXT = K + 1;
-  float* slab = a.slab + (int64_t)blockIdx.x * H * KEXT;
-#pragma unroll
-  for (int k = 0; k < KT; ++k)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      slab[(int64_t)(16 * wave + 4 * g + r) * KEXT + 16 * k + i] = hi[k][r] + lo[k][r];
-  // db: the four row blocks' column partials, summed in a fixed order
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(&zt[0][0][0]);
-  red[threadIdx.x] = dbacc;
-  __syncthreads();
-  if (threadIdx.x < H)
-    slab[(int64_t)threadIdx.x * KEXT + K] =
-        ((red[threadIdx.x] + red[H + threadIdx.x]) + red[2 * H + threadIdx.x]) +
-        red[3 * H + threadIdx.x];
-}
-
 // T-row tiles need every one of the 512 threads to stage at least one float4 of dz and of X
 template <int H, int K, int T>
 constexpr bool wgrad5_valid() { return T * H / 4 >= 512 && T * K / 4 >= 512; }
@@ -1463,118 +1222,6 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
     }
 #pragma unroll
     for (int c = 0; c < HC; ++c) zc[c] = zn[c];
-  }
-}
-
-// dgrad on the bf16x6 split (H = 128): dX = dz W, out^T = W^T dz^T.  The block's KB output
-// columns of W^T (KB = 128, or 64 for K = 256: two blocks b, b + 8 take the two halves of one tile
-// stream, as the forward) are split once into three bf16 planes in LDS; lane (i, g) loads row i's
-// dout at h = 32 s + 8 g .. +7, masks it (ReLU bits: words row * 4 + 2 (g & 1) and + 1, or the
-// forward output), writes the masked dz once when asked (column half 0), splits it and re-loads
-// the slot with the next tile's.  The lane ends with dX[row i][16 c + 4 g .. +3]: store_dx4
-// through the segment table (stored, or added where dx_acc says).
-template <int K, int KB>
-__global__ void __launch_bounds__(512, 1) k_linear_dgrad_x6(const LinArgs a, const ChunkTab tab,
-                                                            int64_t n_tiles) {
-  constexpr int H = 128, NT = KB / 16, HS = H / 32, LDB = H + 16, NH = K / KB;   // see fwd
-  __shared__ __attribute__((aligned(16))) unsigned short wp[3][KB * LDB];
-  const int hb = NH == 1 ? 0 : (int)((blockIdx.x >> 3) & 1), col0 = hb * KB;
-  const int64_t stream_id = NH == 1 ? blockIdx.x : (blockIdx.x & 7) + 8 * (blockIdx.x >> 4);
-  for (int idx = threadIdx.x; idx < H * KB; idx += 512) {
-    const int j = idx / KB, kk = idx % KB;      // W[j][col0 + kk] -> W^T row kk, column j
-    const float v = a.w[(int64_t)j * K + col0 + kk];
-    const unsigned short a1 = x6_bf16(v);
-    const float r1 = v - x6_f32(a1);
-    const unsigned short a2 = x6_bf16(r1);
-    wp[0][kk * LDB + j] = a1;
-    wp[1][kk * LDB + j] = a2;
-    wp[2][kk * LDB + j] = x6_bf16(r1 - x6_f32(a2));
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t nw = (int64_t)(gridDim.x / NH) * 8;
-  const int64_t last = a.n - 1;
-  const bool bits = a.mask_in != nullptr;
-  const bool masked = !bits && a.out_act != nullptr;
-  int64_t t = stream_id * 8 + wave;
-  float4 zv[HS][2], mv[HS][2];
-  uint2 mw = make_uint2(0u, 0u);
-  auto load_s = [&](int64_t tt, int s) {
-    const int64_t row = min<int64_t>(tt * 16 + i, last);
-    const float4* p = reinterpret_cast<const float4*>(a.dout + row * H + 32 * s + 8 * g);
-    zv[s][0] = p[0];
-    zv[s][1] = p[1];
-    if (masked) {
-      const float4* q = reinterpret_cast<const float4*>(a.out_act + row * H + 32 * s + 8 * g);
-      mv[s][0] = q[0];
-      mv[s][1] = q[1];
-    }
-    if (bits && s == 0) mw = *reinterpret_cast<const uint2*>(a.mask_in + row * 4 + 2 * (g & 1));
-  };
-  if (t < n_tiles) {
-#pragma unroll
-    for (int s = 0; s < HS; ++s) load_s(t, s);
-  }
-  __syncthreads();
-  for (; t < n_tiles; t += nw) {
-    const int64_t tn = t + nw < n_tiles ? t + nw : t;
-    const int64_t row = t * 16 + i;
-    int wo = i * LDB + 8 * g;
-    asm volatile("" : "+v"(wo));   // W^T fragments stay per-tile LDS reads (see fwd v4)
-    f32x4 hi[NT], lo[NT];
-#pragma unroll
-    for (int c = 0; c < NT; ++c) hi[c] = lo[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8_t cw[3], nx[3];
-    auto rd = [&](int s, int c, bf16x8_t (&f)[3]) {
-      const int off = wo + 16 * c * LDB + 32 * s;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) f[q] = *reinterpret_cast<const bf16x8_t*>(&wp[q][off]);
-    };
-    rd(0, 0, cw);
-    const uint2 mcur = mw;
-#pragma unroll
-    for (int s = 0; s < HS; ++s) {
-      float4 z0 = zv[s][0], z1 = zv[s][1];
-      if (bits) {   // element j of k-step s: column tile 2 s + (g >> 1), word j / 4, bit j % 4
-        const int sh = 4 * (2 * s + (g >> 1));
-        z0 = mask4(z0, mcur.x, sh);
-        z1 = mask4(z1, mcur.y, sh);
-      }
-      if (masked) {
-        const float4 m0 = mv[s][0], m1 = mv[s][1];
-        z0.x = m0.x > 0.f ? z0.x : 0.f; z0.y = m0.y > 0.f ? z0.y : 0.f;
-        z0.z = m0.z > 0.f ? z0.z : 0.f; z0.w = m0.w > 0.f ? z0.w : 0.f;
-        z1.x = m1.x > 0.f ? z1.x : 0.f; z1.y = m1.y > 0.f ? z1.y : 0.f;
-        z1.z = m1.z > 0.f ? z1.z : 0.f; z1.w = m1.w > 0.f ? z1.w : 0.f;
-      }
-      if (a.dz_out && hb == 0 && row < a.n) {
-        float4* q = reinterpret_cast<float4*>(a.dz_out + row * H + 32 * s + 8 * g);
-        q[0] = z0;
-        q[1] = z1;
-      }
-      bf16x8_t x1, x2, x3;
-      x6_split8(z0, z1, x1, x2, x3);
-      load_s(tn, s);   // the next tile's k-step s (and at s = 0 its mask words)
-#pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        if (c + 1 < NT) rd(s, c + 1, nx);
-        else if (s + 1 < HS) rd(s + 1, 0, nx);
-        x6_mma(cw, x1, x2, x3, hi[c], lo[c]);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) cw[q] = nx[q];
-      }
-    }
-    if (row < a.n) {
-#pragma unroll
-      for (int c = 0; c < NT; ++c) {
-        const int ct = hb * NT + c;
-        float* dx = tab.dx[ct];
-        if (dx)
-          store_dx4(dx + row * tab.ld[ct] + tab.col[ct] + 4 * g, (tab.dx_acc >> ct) & 1u,
-                    hi[c][0] + lo[c][0], hi[c][1] + lo[c][1], hi[c][2] + lo[c][2],
-                    hi[c][3] + lo[c][3]);
-      }
-    }
   }
 }
 
@@ -1827,29 +1474,10 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
     static const bool s8_env = !getenv("HGNN_K3_S8") || atoi(getenv("HGNN_K3_S8")) != 0;
     const bool s8 = s8_env && h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
-    // the fp32-exact bf16x6 split (k_linear_fwd_x6) at H = 128, K = 128 / 256: default
+    // the fp32-exact bf16x6 split at H = 128, K = 128 / 256 (linear_xs.hip), the default
     // (HGNN_K3_X6=0: the f32-input MFMA kernels below)
-    if (x6_enabled() && h == 128 && (a.k_total == 128 || a.k_total == 256)) {
-      if (xs_enabled()) return xs_linear_fwd(a, tab, stream);   // split once per element
-      int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
-                                                               a.k_total == 128 ? 256 : 128));
-      if (a.k_total != 128) streams = cdiv(streams, 8) * 8;   // column-half pairs b, b + 8
-#define HGNN_FWDX6(KV, HBV, AV)                                                                  \
-  {                                                                                              \
-    const dim3 gx6((unsigned)(streams * (128 / HBV)));                                           \
-    if (s8) hipLaunchKernelGGL((k_linear_fwd_x6<KV, HBV, AV, true>), gx6, block, 0, stream, a,   \
-                               tab, n_tiles);                                                    \
-    else hipLaunchKernelGGL((k_linear_fwd_x6<KV, HBV, AV, false>), gx6, block, 0, stream, a,     \
-                            tab, n_tiles);                                                       \
-  }
-      if (a.k_total == 128) {
-        if (add) HGNN_FWDX6(128, 128, true) else HGNN_FWDX6(128, 128, false)
-      } else {
-        if (add) HGNN_FWDX6(256, 64, true) else HGNN_FWDX6(256, 64, false)
-      }
-#undef HGNN_FWDX6
-      return check_launch("k_linear_fwd_x6");
-    }
+    if (x6_enabled() && h == 128 && (a.k_total == 128 || a.k_total == 256))
+      return xs_linear_fwd(a, tab, stream);
     const int fwd_ver = fwd_env ? fwd_env : (!s8 && h == 128 && a.k_total == 128 ? 5 : 4);
 #define HGNN_FWD4S(HV, KV, AV, SV)                                                               \
   if (fwd_ver == 4)                                                                              \
@@ -2008,7 +1636,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     const bool split = split_env >= 0 ? split_env != 0 : (h == 128 && K == 128);
     const bool fused = !split && any_dx && (dw || db) && K <= 128 &&
                        v4_bwd_lds(h, K, true) <= 160 * 1024;
-    if (x6_enabled() && xs_enabled() && h == 128 && (K == 128 || K == 256)) {
+    if (x6_enabled() && h == 128 && (K == 128 || K == 256)) {
       // the split-once kernels (linear_xs.hip): dz split once for the dgrad and the wgrad
       const bool wg = dw || db;
       a.slab = nullptr;
@@ -2032,19 +1660,6 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8), 256))),
           block(512);
       const size_t lds = dgrad4_lds(h, K);
-      if (x6_enabled() && h == 128 && (K == 128 || K == 256)) {   // bf16x6 split (see forward)
-        int64_t streams = std::max<int64_t>(1, std::min<int64_t>(cdiv(n16, 8),
-                                                                 K == 128 ? 256 : 128));
-        if (K != 128) streams = cdiv(streams, 8) * 8;
-        if (K == 128)
-          hipLaunchKernelGGL((k_linear_dgrad_x6<128, 128>), dim3((unsigned)streams), block, 0,
-                             stream, a, tab, n16);
-        else
-          hipLaunchKernelGGL((k_linear_dgrad_x6<256, 128>), dim3((unsigned)(2 * streams)), block,
-                             0, stream, a, tab, n16);
-        if (int rc = check_launch("k_linear_dgrad_x6")) return rc;
-        goto dgrad_done;
-      }
       {
       // v5 at H = 128 (K = 256: 5.06 vs 5.70 ms; K = 128: 3.22 vs 3.25 ms at N = 9M)
       static const int dg_env = getenv("HGNN_K3_DGRAD") ? atoi(getenv("HGNN_K3_DGRAD")) : 0;
@@ -2066,7 +1681,6 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       if (int rc = check_launch("k_linear_dgrad_v4")) return rc;
       }
     }
-  dgrad_done:
     if (!(dw || db)) return HGNN_OK;
     if (!ws) return fail(HGNN_E_WS, "linear_bwd: weight gradients need the workspace");
     if (a.dz_out && !fused) {   // the dgrad kernel wrote the masked dz: wgrad streams it alone
@@ -2078,27 +1692,6 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;
     // v4 kept elsewhere (K = 256: v5 6.44 / 9.51 ms at T = 16 / 32 vs 5.65; H = 64 needs T >= 32,
     // which measured slower than v4: 2.44 vs 1.94 ms)
-    if (!fused && x6_enabled() && h == 128 && (K == 128 || K == 256)) {   // bf16x6 (see fwd)
-      const int64_t n_tiles = cdiv(n_rows, 32);
-      const int G = (int)std::min<int64_t>(n_tiles, 256);
-      const size_t need = (size_t)G * h * (K + 1) * 4;
-      if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
-      a.slab = static_cast<float*>(ws);
-      // (a variant staging float4 columns on 2-4 of the 8 waves measured slower: 6.34 vs 4.81 ms
-      // and 11.36 vs 8.59 ms for the 9M-row K = 128 / 256 backward — the split work then sits on
-      // fewer waves while the others wait at the barrier)
-      if (K == 128)
-        hipLaunchKernelGGL((k_linear_wgrad_x6<128, 2>), dim3(G), dim3(512), 0, stream, a, tab,
-                           n_tiles);
-      else
-        hipLaunchKernelGGL((k_linear_wgrad_x6<256, 2>), dim3(G), dim3(512), 0, stream, a, tab,
-                           n_tiles);
-      if (int rc = check_launch("k_linear_wgrad_x6")) return rc;
-      const int64_t total = (int64_t)h * (K + 1);
-      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                         a.slab, (int64_t)G, h, K + 1, dw, db);
-      return check_launch("k_wgrad_reduce");
-    }
     static const int wg_env = getenv("HGNN_K3_WGRAD") ? atoi(getenv("HGNN_K3_WGRAD")) : 0;
     const int wg_ver = wg_env ? wg_env : (h == 128 && K == 128 ? 5 : 4);
     static const int wg_t = getenv("HGNN_K3_WGRAD_T") ? atoi(getenv("HGNN_K3_WGRAD_T")) : 16;
@@ -2220,11 +1813,8 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
 }
 
 int hgnn_set_k3_split(int32_t on) {
-  const int prev = x6_enabled() ? (xs_enabled() ? 1 : 2) : 0;
-  if (on >= 0) {
-    g_k3_x6 = on ? 1 : 0;
-    g_k3_xs = on == 2 ? 0 : 1;
-  }
+  const int prev = x6_enabled() ? 1 : 0;
+  if (on >= 0) g_k3_x6 = on ? 1 : 0;
   return prev;
 }
 

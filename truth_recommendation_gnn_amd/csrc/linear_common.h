@@ -102,8 +102,11 @@ __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1
 // double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
 // accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
 // 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
-// Non-finite values: v1 = bf16(v) carries an inf (or NaN) and the residual pieces are zero, so
-// an inf input gives the inf (or NaN) the f32 product would, not inf - inf = NaN in a residual.
+// Non-finite values: v1 = bf16(v) carries an inf (or NaN) and the residual pieces are finite
+// (x6_res), and a result whose large product sum is +-inf is that inf (x6_out): the small
+// products of an inf with W's residual pieces, whose signs differ, would otherwise turn it into
+// NaN.  So an inf input gives the +-inf (or NaN) the f32 kernels give; a finite |v| above the
+// largest bf16 (3.39e38, which rounds to inf) is the one case that differs.
 __device__ __forceinline__ unsigned short x6_bf16(float f) {
   return __bfloat16_as_ushort(__float2bfloat16(f));   // round to nearest even (v_cvt_pk_bf16_f32)
 }
@@ -153,6 +156,11 @@ __device__ __forceinline__ void x6_split4(const float4& u, bf16x4_t& p1, bf16x4_
     p3[j] = (short)a3;
   }
 }
+// hi + lo of the split's two accumulators, hi alone when it is +-inf (see above)
+__device__ __forceinline__ float x6_out(float hi, float lo) {
+  return __builtin_isinf(hi) ? hi : hi + lo;
+}
+
 // acc_hi += w1 x1; acc_lo += w2 x2 + w3 x1 + w1 x3 + w2 x1 + w1 x2 (small terms first)
 __device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x1,
                                        const bf16x8_t& x2, const bf16x8_t& x3, f32x4& hi,
@@ -167,8 +175,6 @@ __device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x
 
 // The split-once kernels (linear_xs.hip): H = 128, K = 128 / 256, every segment 16-column
 // chunked and float4-aligned.  Host launchers; the caller validated the arguments.
-bool xs_enabled();
-extern int g_k3_xs;   // -1: from HGNN_K3_XS at the first call
 int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream);
 // dW / db partials into a.slab (grid blocks x [H][K + 1]); the caller reduces them.  dx: run the
 // dgrad too (tab.dx).  Returns the block count through *grid.

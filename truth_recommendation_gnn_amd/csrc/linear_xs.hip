@@ -128,7 +128,7 @@ __device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int la
 // kept: loads two tiles ahead in a second register set, the split interleaved into the sweep
 // — 3.84 vs 3.69 ms at 9M rows, K = 256; the kernel runs at a power-limited ~1.75 GHz, so
 // what counts is the instruction count, not the overlap.)
-template <int K, bool ADD, int PROBE = 0>
+template <int K, bool ADD>
 __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
                                                         int64_t n_tiles) {
   constexpr int R = K == 256 ? 32 : 64, KS = K / 32, RT = R / 16, LDP = K + 16, PS = R * LDP;
@@ -185,11 +185,10 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
       }
       __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
     }
-    if constexpr ((PROBE & 2) == 0) xs.issue(xr, (t + G) * R, last);
+    xs.issue(xr, (t + G) * R, last);
     __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
     const unsigned short* p = pl[b];
     f32x4 hi[RT], lo[RT];
-    if constexpr ((PROBE & 4) == 0) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -198,28 +197,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
         const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
         const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
-        if constexpr ((PROBE & 1) == 0) x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
-        else { hi[r][0] += (float)x1[0]; lo[r][1] += (float)x2[1] + (float)x3[2]; }
-      }
-    }
-    } else {   // fragments read one k-step ahead
-      bf16x8_t f[2][3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) f[0][q] = row8<LDP>(p + q * PS, 0, 0, i, g);
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const int c = (r * KS + s) & 1;
-          const int rn = s + 1 < KS ? r : r + 1, sn = s + 1 < KS ? s + 1 : 0;
-          if (rn < RT) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) f[c ^ 1][q] = row8<LDP>(p + q * PS, 16 * rn, 32 * sn, i, g);
-          }
-          if constexpr ((PROBE & 1) == 0) x6_mma(wa[s], f[c][0], f[c][1], f[c][2], hi[r], lo[r]);
-          else { hi[r][0] += (float)f[c][0][0]; lo[r][1] += (float)f[c][1][1] + (float)f[c][2][2]; }
-        }
+        x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
       }
     }
     // the stored rows' registers are reserved until here (see above)
@@ -228,8 +206,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
       asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
-      float4 v = make_float4((hi[r][0] + lo[r][0]) + bb.x, (hi[r][1] + lo[r][1]) + bb.y,
-                             (hi[r][2] + lo[r][2]) + bb.z, (hi[r][3] + lo[r][3]) + bb.w);
+      float4 v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
+                             x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
       if constexpr (ADD) {
         v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
       }
@@ -405,8 +383,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         for (int r = 0; r < R / 16; ++r) {
           const int64_t row = t * R + 16 * r + i;
           if (dxp[u] && row < a.n) {
-            float4 v = make_float4(dh[u][r][0] + dl[u][r][0], dh[u][r][1] + dl[u][r][1],
-                                   dh[u][r][2] + dl[u][r][2], dh[u][r][3] + dl[u][r][3]);
+            float4 v = make_float4(x6_out(dh[u][r][0], dl[u][r][0]), x6_out(dh[u][r][1], dl[u][r][1]),
+                                   x6_out(dh[u][r][2], dl[u][r][2]), x6_out(dh[u][r][3], dl[u][r][3]));
             if constexpr (ACC) {
               if (acc_dx[u]) {
                 v.x = dxo[u][r].x + v.x; v.y = dxo[u][r].y + v.y; v.z = dxo[u][r].z + v.z;
@@ -454,14 +432,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
 
 }  // namespace
 
-// On unless HGNN_K3_XS=0 (then the round-3 split kernels), and only while the split itself is on
-// (hgnn_set_k3_split / HGNN_K3_X6, linear.hip).
-int g_k3_xs = -1;
-bool xs_enabled() {
-  if (g_k3_xs < 0) g_k3_xs = (!getenv("HGNN_K3_XS") || atoi(getenv("HGNN_K3_XS")) != 0) ? 1 : 0;
-  return g_k3_xs != 0;
-}
-
 int64_t xs_bwd_grid(int64_t n_rows) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_rows, 32), 256));
 }
@@ -472,14 +442,7 @@ int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
   const int64_t R = K == 256 ? 32 : 64;
   const int64_t n_tiles = cdiv(a.n, R);
   const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 256))), block(kThr);
-  static const int probe = getenv("HGNN_XS_PROBE") ? atoi(getenv("HGNN_XS_PROBE")) : 0;
-  if (probe && K == 256 && !a.add) {
-    switch (probe) {
-#define P(v) case v: hipLaunchKernelGGL((k_lin_fwd_xs<256, false, v>), grid, block, 0, stream, a, tab, n_tiles); break;
-      P(1) P(2) P(4) P(5) P(6)
-#undef P
-    }
-  } else if (K == 128) {
+  if (K == 128) {
     if (a.add) hipLaunchKernelGGL((k_lin_fwd_xs<128, true>), grid, block, 0, stream, a, tab, n_tiles);
     else hipLaunchKernelGGL((k_lin_fwd_xs<128, false>), grid, block, 0, stream, a, tab, n_tiles);
   } else {

@@ -874,8 +874,74 @@ def _row_range(grouped, lo: int, hi: int):
     return g
 
 
+def _sort_negatives(csr, neg_u_order, draw, neg, neg32: bool, uop, E: int, np_: int, err,
+                    dev):
+    """The negatives (user-grouped order) grouped by post: (rowptr over posts, users in that
+    order), stable — the order the dP gather sums them in."""
+    lib = N.lib()
+    rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
+    nu_s = torch.empty(E, dtype=torch.int32, device=dev)
+    ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
+    if draw is not None:
+        # draws computed in the sort's first pass (and again in the scoring pass: no
+        # position-order copy is written)
+        with _timed("sort_negatives", 4 * E * (2 * 4)):
+            N.check(lib.hgnn_draw_sort_negatives(
+                N.ptr(draw.seed), N.ptr(uop), E, np_, None, N.ptr(rowptr_n),
+                N.ptr(nu_s), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                "hgnn_draw_sort_negatives")
+    elif neg32:
+        # int32 keys: no validation pass (the scoring pass below counts out-of-range
+        # negatives; the sort only misplaces such a key, never dereferences it)
+        with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
+            N.check(lib.hgnn_sort_pairs_i32(
+                N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                None, None, N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                "hgnn_sort_pairs_i32")
+    else:
+        with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
+            N.check(lib.hgnn_sort_pairs_i64(
+                N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
+                None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
+                "hgnn_sort_pairs_i64")
+    return rowptr_n, nu_s
+
+
+class PresortedNegatives:
+    """The loss's negatives already grouped by post (``presort_negatives``): the sharded step
+    sorts them under a collective, ahead of the loss that consumes them."""
+
+    def __init__(self, key, rowptr, users):
+        self.key, self.rowptr, self.users = key, rowptr, users
+
+
+def _neg_inputs(neg_u_order):
+    draw = neg_u_order if isinstance(neg_u_order, NegativeDraw) else None
+    neg32 = neg_u_order.dtype == torch.int32
+    if draw is not None:
+        neg = None
+    else:
+        neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
+    return draw, neg32, neg
+
+
+def presort_negatives(n_users: int, n_posts: int, pos_edges: torch.Tensor, neg_p,
+                      neg_order: str = "user") -> PresortedNegatives:
+    """The grouping ``edge_bce_loss_raw`` would sort its negatives into, done now (it needs
+    only the edges and the draws, not the embeddings); pass it back as ``presorted=``."""
+    csr = relation_csr_for_loss(pos_edges, n_users, n_posts)
+    neg_u = _negatives_user_order(csr, neg_p, neg_order)
+    draw, neg32, neg = _neg_inputs(neg_u)
+    dev = csr.fwd.rowptr.device
+    err = torch.zeros(2, dtype=torch.int32, device=dev)
+    E = csr.num_edges
+    rp, us = _sort_negatives(csr, neg_u, draw, neg, neg32, _user_of_pos(csr), E, n_posts, err,
+                             dev)
+    return PresortedNegatives((id(csr), E, n_posts, id(neg_p), neg_order), rp, us)
+
+
 def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
-              ready=None, on_dP=None, p_chunks=None):
+              ready=None, on_dP=None, p_chunks=None, presorted=None):
     """Loss value and its gradients for a unit upstream gradient: (loss, dU, dP).  ``on_dP(dP)``,
     if given, is called once dP's kernels are enqueued and before the scoring pass (dU, the loss)
     is: the sharded step starts dP's reduce-scatter there, under the scoring pass.
@@ -914,37 +980,19 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
         neg = None   # drawn again where read (the sort's first pass, the scoring pass)
     else:
         neg = neg_u_order.contiguous() if neg32 else neg_u_order.to(torch.int64).contiguous()
-    rowptr_n = torch.empty(np_ + 1, dtype=torch.int32, device=dev)
-    nu_s = torch.empty(E, dtype=torch.int32, device=dev)
     dP = torch.empty_like(P)
     # dP chain (side stream under HGNN_STREAMS=1): sort the negatives (post, user) by post,
     # then the two dP gathers, each edge's weight recomputed from <U[u], P[post]>
     # (hgnn_score_gather); pass A (loss + dU) needs none of it.
     lanes = _Lanes(dev, 2)
     with lanes.ctx(1):
-        ws = N.workspace(lib.hgnn_sort_pairs_ws_bytes(E, np_), dev)
-        if draw is not None:
-            # draws computed in the sort's first pass (and again in the scoring pass: no
-            # position-order copy is written)
-            with _timed("sort_negatives", 4 * E * (2 * 4)):
-                N.check(lib.hgnn_draw_sort_negatives(
-                    N.ptr(draw.seed), N.ptr(uop), E, np_, None, N.ptr(rowptr_n),
-                    N.ptr(nu_s), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                    "hgnn_draw_sort_negatives")
-        elif neg32:
-            # int32 keys: no validation pass (the scoring pass below counts out-of-range
-            # negatives; the sort only misplaces such a key, never dereferences it)
-            with _timed("sort_negatives", 4 * E * (2 * 4) + 4 * E):
-                N.check(lib.hgnn_sort_pairs_i32(
-                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
-                    None, None, N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                    "hgnn_sort_pairs_i32")
+        if presorted is not None:
+            if presorted.key[:3] != (id(csr), E, np_):
+                raise ValueError("edge_bce_loss: the presorted negatives are for other edges")
+            rowptr_n, nu_s = presorted.rowptr, presorted.users
         else:
-            with _timed("sort_negatives", 4 * E * (2 + 1 + 4) + 4 * E):
-                N.check(lib.hgnn_sort_pairs_i64(
-                    N.ptr(neg), N.ptr(uop), None, E, np_, N.ptr(rowptr_n), N.ptr(nu_s),
-                    None, N.ptr(err[1:]), N.ptr(ws), ws.numel(), N.stream_ptr(dev)),
-                    "hgnn_sort_pairs_i64")
+            rowptr_n, nu_s = _sort_negatives(csr, neg_u_order, draw, neg, neg32, uop, E, np_,
+                                             err, dev)
     if ready is not None and p_chunks is None:
         # P is still arriving (parallel.py's all-gather of the post table): the sort above
         # needs only the edges, so it ran ahead; every kernel below reads P
@@ -1053,14 +1101,18 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
 
 def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
                       neg_p: torch.Tensor, n_edges_total: int, cscale: torch.Tensor,
-                      neg_order: str = "user", ready=None, on_dP=None, p_chunks=None):
+                      neg_order: str = "user", ready=None, on_dP=None, p_chunks=None,
+                      presorted: Optional[PresortedNegatives] = None):
     """:func:`edge_bce_loss` outside autograd: (loss, dL/dU, dL/dP) from the same kernels, for
     callers that run their own backward schedule (``parallel.UserShard.step``; ``on_dP``,
-    ``p_chunks``: see ``_edge_bce``)."""
+    ``p_chunks``: see ``_edge_bce``; ``presorted``: from :func:`presort_negatives` on the same
+    edges and draws)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     neg_u = _negatives_user_order(csr, neg_p, neg_order)
+    if presorted is not None and presorted.key[3:] != (id(neg_p), neg_order):
+        raise ValueError("edge_bce_loss_raw: presorted negatives of other draws")
     return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready,
-                     on_dP, p_chunks)
+                     on_dP, p_chunks, presorted)
 
 
 def _negatives_user_order(csr, neg_p, neg_order):
