@@ -88,6 +88,30 @@ class EmulEnv(parallel.DistEnv):
                             // self.world)
 
 
+def link_timeline(log, t0, step_ms, gbs):
+    """The recorded step replayed against one serial link of ``gbs`` GB/s: the collectives run
+    in issue order, one at a time (one communicator), each recv_bytes / rate long, starting when
+    issued and the link is free; a consumer that waits before its collective has ended stalls
+    the compute (and every later issue) by the difference.  Returns the stall in total and per
+    collective: the step at that link rate is the compute plus the stall."""
+    ev = []
+    for i, r in enumerate(log):
+        ev.append((t0.elapsed_time(r["issue"]), 0, i))
+        ev.append((t0.elapsed_time(r["wait"]) if "wait" in r else step_ms, 1, i))
+    ev.sort()
+    shift, free, end, stall = 0.0, 0.0, {}, [0.0] * len(log)
+    for t, kind, i in ev:
+        if kind == 0:
+            start = max(t + shift, free)
+            end[i] = free = start + log[i]["recv_bytes"] / (gbs * 1e9) * 1e3
+        elif end[i] > t + shift:
+            stall[i] = end[i] - (t + shift)
+            shift += stall[i]
+    return {"link_GBs": gbs, "step_ms_compute": round(step_ms, 3),
+            "stall_ms": round(shift, 3), "step_ms_with_link": round(step_ms + shift, 3),
+            "stall_ms_by_collective": [round(x, 3) for x in stall]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
@@ -121,6 +145,9 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(3)
 
     def step():
+        if env.log is not None:                   # the step's start, for the link timeline
+            env.t0 = torch.cuda.Event(enable_timing=True)
+            env.t0.record()
         opt.zero_grad(set_to_none=True)
         neg = ops.draw_negatives(shard.pos_local, gcfg.num_posts, generator=gen)
         shard.step(model, x_user, x_post, neg, neg_order="user", x_user_full=x_full)
@@ -145,7 +172,12 @@ def main():
     step()
     flat = torch.cat([p.grad.reshape(-1) for p in model.parameters()])   # sync_grads' all-reduce
     env.all_reduce_async(flat).wait()
+    t_end = torch.cuda.Event(enable_timing=True)
+    t_end.record()
     torch.cuda.synchronize()
+    step_ms = env.t0.elapsed_time(t_end)
+    timeline = {f"{n}": link_timeline(env.log, env.t0, step_ms, XGMI_LINK_GBS * k)
+                for n, k in (("1link_ring", 1), ("7links", XGMI_LINKS))}
     colls = []
     for r in env.log:
         cover = r["issue"].elapsed_time(r["wait"]) if "wait" in r else None
@@ -160,6 +192,7 @@ def main():
     print(json.dumps({"world": args.world, "rank": args.rank, "config": gcfg.name,
                       "chunked_last_gather": parallel.CHUNKED_LAST_GATHER,
                       "collectives": colls,
+                      "link_timeline": timeline,
                       "scaling": "strong" if args.strong else "weak",
                       "users_own": shard.n_own, "posts_padded": shard.n_posts_pad,
                       "local_edges_per_step": edges_local,

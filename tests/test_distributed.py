@@ -93,6 +93,19 @@ def _worker(rank, world, port, q, kind="engage2", slice_inputs=False):
     (3, "engage2", True), (3, "rel4", True), (8, "tiny4", True), (2, "engage3", True),
     (3, "soc2", True), (1, "engage2", True)])
 def test_user_sharded_step_matches_single_process_oracle(world, kind, slice_inputs):
+    _run_and_check(world, kind, slice_inputs)
+
+
+@pytest.mark.parametrize("split", ["1", "3"])
+@pytest.mark.parametrize("world,kind", [(3, "engage2"), (2, "rel4")])
+def test_sharded_step_with_other_partial_sum_splits(world, kind, split, monkeypatch):
+    """The user->post partial sums as one reduce-scatter (round 3) or three row ranges per slice
+    (parallel.SPLIT_PARTIALS; the default, two, is every other case): the same oracle step."""
+    monkeypatch.setenv("HGNN_SPLIT_PARTIALS", split)     # read at import by the spawned ranks
+    _run_and_check(world, kind, False)
+
+
+def _run_and_check(world, kind, slice_inputs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -1046,7 +1046,11 @@ class _EdgeBCELoss(torch.autograd.Function):
     keeps them; the first backward scales them in place by the upstream gradient and hands them
     on (no copy: 2 x 4.6 GB at cfg4).  A second backward through a retained graph
     (``retain_graph=True``) recomputes them from the saved embeddings and the same negatives —
-    the kernels are deterministic, so it returns what the first did, as torch's loss would."""
+    the kernels are deterministic, so it returns what the first did, as torch's loss would.
+    For that recompute U and P stay saved until the graph is freed (as torch's own loss saves
+    its inputs): at cfg4 4.6 + 0.5 GB of the 288 GB, held from the forward to the end of the
+    backward, which the split K3 backward (mask bits, not the outputs) would otherwise release
+    after this loss's backward."""
 
     @staticmethod
     def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,

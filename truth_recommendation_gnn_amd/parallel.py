@@ -82,16 +82,19 @@ class DistEnv:
         on device tensors (a one-GPU rehearsal) goes through all-reduce / all_gather lists."""
         return dist.get_backend(self.group) == "nccl" or not t.is_cuda
 
-    def reduce_scatter_async(self, full: torch.Tensor):
-        """Sum over ranks of ``full`` [world*S, ...]; returns (this rank's slice [S, ...], work)."""
+    def reduce_scatter_async(self, full: torch.Tensor, out: Optional[torch.Tensor] = None):
+        """Sum over ranks of ``full`` [world*S, ...]; returns (this rank's slice [S, ...], work).
+        ``out``: a contiguous [S, ...] buffer (e.g. a row range of a larger table) to land in."""
         S = full.shape[0] // self.world
-        if self._direct(full):
+        if out is None:
             out = torch.empty((S,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+        if self._direct(full):
             work = dist.reduce_scatter_tensor(out, full, group=self.group, async_op=True)
             return out, _Held(work, full, out)
         t = full.clone()
         dist.all_reduce(t, group=self.group)
-        return t[self.rank * S:(self.rank + 1) * S].clone(), _Done()
+        out.copy_(t[self.rank * S:(self.rank + 1) * S])
+        return out, _Done()
 
     def all_gather_async(self, own: torch.Tensor):
         """Concatenation over ranks of ``own`` [S, ...]; returns (full [world*S, ...], work)."""
@@ -184,6 +187,13 @@ class _AllOf:
 # HGNN_CHUNKED_GATHER=1 one dP launch per block, 2 three launches (own block, the blocks below,
 # the blocks above), 0 one all-gather and one dP launch.
 CHUNKED_LAST_GATHER = int(os.environ.get("HGNN_CHUNKED_GATHER", "2"))
+
+# user->post partial sums at world > 1 in this many row ranges of every slice (1 = one
+# reduce-scatter of the whole padded table, round 3).  With 2, the first range's reduce-scatter
+# is issued after half the gather and the second after the rest, so the link starts while the
+# gather runs; the backward's all-gather of the slice gradients is split the same way and its K2
+# starts on the first range while the second lands.  HGNN_SPLIT_PARTIALS=1|2.
+SPLIT_PARTIALS = int(os.environ.get("HGNN_SPLIT_PARTIALS", "2"))
 
 
 class Pending:
@@ -478,6 +488,28 @@ class _Rel:
     # (global user ids).  Layer 1 reads the static input user table, which each rank can hold
     # whole: the slice's mean is then computed locally, with no partial sums to reduce-scatter.
     slice_csr: object = None
+    # world > 1: the same edges split by the row range of every post slice their post lies in
+    # (_PartialHalf).  user->post: the partial sums travel as one reduce-scatter per range, the
+    # first issued while the second range's gather still runs; post->user: the K2 of a
+    # pre-projected relation's dz into the post table, one reduce-scatter per range likewise
+    # (see SPLIT_PARTIALS)
+    halves: Optional[List["_PartialHalf"]] = None
+
+
+@dataclasses.dataclass
+class _PartialHalf:
+    """A relation's edges whose post lies in rows [lo, hi) of its owner's slice, the post ids
+    renumbered into a table of world * (hi - lo) rows in which owner q's rows come q-th: a
+    reduce-scatter of such a table hands every rank rows [lo, hi) of its own slice, and an
+    all-gather of those rows builds it.  user->post: w_fwd / row_w the partial sums' 1/deg(post)
+    and w_bwd its adjoint; post->user: w_bwd = 1/deg(user) per edge, the mean's K2 over the
+    whole relation's degrees."""
+    csr: object
+    w_fwd: Optional[torch.Tensor]
+    w_bwd: torch.Tensor
+    row_w: Optional[torch.Tensor]
+    lo: int
+    hi: int
 
 
 @dataclasses.dataclass
@@ -572,7 +604,8 @@ class UserShard:
         if kind == ("post", "user"):
             m = self._owned_users(dst)
             local = torch.stack([src[m], dst[m] - self.lo]).contiguous()
-            return _Rel(kind, impl.relation(local, self.n_posts_pad, self.n_own))
+            return _Rel(kind, impl.relation(local, self.n_posts_pad, self.n_own),
+                        halves=self._k2_halves(local))
         if kind == ("user", "user"):
             m = self._owned_users(dst)
             s = src[m]
@@ -600,11 +633,60 @@ class UserShard:
                 sl = torch.stack([src[ms], dst[ms] - self.p_lo]).contiguous()
                 slice_rel = impl.relation(sl, self.n_users, self.post_rows)
             return _Rel(kind, rel, impl.edge_weights_fwd(rel, inv), impl.edge_weights_bwd(rel, inv),
-                        inv, slice_rel)
+                        inv, slice_rel, self._partial_halves(local, inv))
         # post -> post: edges into the owned slice of the post table
         m = (dst >= self.p_lo) & (dst < self.p_hi)
         local = torch.stack([src[m], dst[m] - self.p_lo]).contiguous()
         return _Rel(kind, impl.relation(local, self.n_posts_pad, self.post_rows))
+
+    def _ranges(self):
+        """The SPLIT_PARTIALS row ranges of a post slice, or None (world 1, slices too short)."""
+        W, S = self.env.world, self.post_rows
+        n = min(max(SPLIT_PARTIALS, 1), S)
+        if W == 1 or n < 2:
+            return None
+        return [(S * i // n, S * (i + 1) // n) for i in range(n)]
+
+    def _renumber(self, post: torch.Tensor, lo: int, hi: int):
+        """Mask of the padded post ids in rows [lo, hi) of their slice, and their ids in the
+        range table (owner q's rows q-th)."""
+        S = self.post_rows
+        q, j = torch.div(post, S, rounding_mode="floor"), post % S
+        m = (j >= lo) & (j < hi)
+        return m, q[m] * (hi - lo) + (j[m] - lo)
+
+    def _partial_halves(self, local: torch.Tensor, inv: torch.Tensor):
+        """The user->post edges (local user, padded post) per row range (_PartialHalf)."""
+        ranges = self._ranges()
+        if ranges is None:
+            return None
+        W, inv_q = self.env.world, inv.view(self.env.world, self.post_rows)
+        out = []
+        for lo, hi in ranges:
+            m, ids = self._renumber(local[1], lo, hi)
+            rel = self.impl.relation(torch.stack([local[0][m], ids]).contiguous(), self.n_own,
+                                     W * (hi - lo))
+            inv_h = inv_q[:, lo:hi].reshape(-1).contiguous()
+            out.append(_PartialHalf(rel, self.impl.edge_weights_fwd(rel, inv_h),
+                                    self.impl.edge_weights_bwd(rel, inv_h), inv_h, lo, hi))
+        return out
+
+    def _k2_halves(self, local: torch.Tensor):
+        """The post->user edges (padded post, local user) per row range, each edge weighted by
+        1/deg(user) over the whole relation (_PartialHalf)."""
+        ranges = self._ranges()
+        if ranges is None:
+            return None
+        deg = torch.bincount(local[1], minlength=self.n_own).to(torch.float32)
+        inv_u = 1.0 / deg.clamp(min=1.0)
+        out = []
+        for lo, hi in ranges:
+            m, ids = self._renumber(local[0], lo, hi)
+            rel = self.impl.relation(torch.stack([ids, local[1][m]]).contiguous(),
+                                     self.env.world * (hi - lo), self.n_own)
+            out.append(_PartialHalf(rel, None, self.impl.edge_weights_bwd(rel, inv_u), None,
+                                    lo, hi))
+        return out
 
     def _setup_halo(self, remote: torch.Tensor) -> _Halo:
         """Tell every owner which of its rows this rank needs (two all-to-alls, once)."""
@@ -754,6 +836,23 @@ class UserShard:
                                        ready=pend.wait)
 
 
+def _issue_slice_gathers(shard, env, pm, dxp, multi):
+    """B4: all-gathers of the slice gradients of every user->post relation's partial sums —
+    per row range in the forward's layout (_PartialHalf) — as {relation: [(range, (table,
+    work))]} (range None: the whole padded table)."""
+    gath = {}
+    for j, (_, et, _) in enumerate(pm):
+        r = shard.rels[et]
+        if r.kind[0] == "user":
+            if multi and r.halves:
+                gath[et] = [(hf, env.all_gather_async(dxp[j][hf.lo:hf.hi].contiguous()))
+                            for hf in r.halves]
+            else:
+                gath[et] = [(None, env.all_gather_async(dxp[j]) if multi
+                             else (dxp[j], _Done()))]
+    return gath
+
+
 def _k2_into(impl, buf, g, csr):
     """K2 of ``g`` over ``csr`` added into ``buf``; the first contribution writes a fresh buffer
     (every row, zero where no edge), so no zero fill of the whole table precedes it."""
@@ -879,8 +978,18 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     # static inputs held whole: the owned slice's mean, no partial sums to reduce
                     rs[et] = (impl.gather_mean_raw(x_user_full, r.slice_csr), _Done())
                     continue
-                part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd, r.row_w)
-                rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
+                if multi and r.halves:
+                    # one reduce-scatter per row range of the slices, each issued as soon as
+                    # its range's partial sums are enqueued
+                    a = h_u.new_empty(shard.post_rows, h_u.shape[1])
+                    works = []
+                    for hf in r.halves:
+                        part = impl.weighted_gather_raw(h_u, hf.csr, hf.w_fwd, hf.row_w)
+                        works.append(env.reduce_scatter_async(part, out=a[hf.lo:hf.hi])[1])
+                    rs[et] = (a, _AllOf(works))
+                else:
+                    part = impl.weighted_gather_raw(h_u, r.csr, r.w_fwd, r.row_w)
+                    rs[et] = env.reduce_scatter_async(part) if multi else (part, _Done())
                 rs_issued = True
         if (multi and rs_issued and li == L - 1 and presorted is None
                 and hasattr(impl, "presort_negatives")):
@@ -1019,64 +1128,91 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
         if pm and R is None:                    # B1 adjoint of the post-table all-gather
             g = G_full if G_full is not None else ypo.new_zeros(shard.n_posts_pad, ypo.shape[1])
             R = env.reduce_scatter_async(g) if multi else (g, _Done())
-        # B2a user-side projection backward (a pre-projected relation: dz as a side output)
-        dxu, dz = [], None
-        pending_w = None
-        if um:
-            dxu = [torch.empty_like(a) if need_x else None for a in a_u]
-            dxu.append(torch.empty_like(hu) if need_x else None)
-            if jp is not None:
-                dz = torch.empty_like(G_u)
-                dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu, m_u,
-                                  dz_out=dz)
-                pending_w = (convs, um, dW, db, col_pre)  # the block's gradient comes with dP
+        def b2a():
+            # B2a user-side projection backward (a pre-projected relation: dz as a side output)
+            dxu, dz, pending_w = [], None, None
+            if um:
+                dxu = [torch.empty_like(a) if need_x else None for a in a_u]
+                dxu.append(torch.empty_like(hu) if need_x else None)
+                if jp is not None:
+                    dz = torch.empty_like(G_u)
+                    dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu,
+                                      m_u, dz_out=dz)
+                    pending_w = (convs, um, dW, db, col_pre)  # the block's gradient comes with dP
+                else:
+                    dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu,
+                                      m_u)
+                    impl.grads_to_params(convs, um, dW, db)
+                d_hu = dxu[-1]
             else:
-                dW, db = _lin_bwd(impl, a_u + [hu], Wu, G_u.contiguous(), yu, dxu, has_bu, m_u)
-                impl.grads_to_params(convs, um, dW, db)
-            d_hu = dxu[-1]
+                d_hu = G_u if need_x else None
+            return dxu, dz, pending_w, d_hu
+
+        def b3():
+            # B3 post-side projection backward (waits for the reduce-scatter)
+            nonlocal R, R_proj
+            dxp, d_hpo = [], G_own
+            if pm:
+                r_slice, r_w = R
+                r_w.wait()
+                R = None
+                if R_proj is not None:
+                    # the reduce-scatter brought the next layer's dP slice: the projection's
+                    # backward (S rows) gives this layer's output-slice gradient and the block's
+                    block, (o, k), (n_convs, n_um, n_dW, n_db, _) = R_proj
+                    R_proj = None
+                    g_y = torch.empty_like(ypo)
+                    dblock, _ = impl.linear_bwd_raw([ypo], block, r_slice.contiguous(), None,
+                                                    [g_y], True, False)
+                    dW_full = torch.cat([n_dW[:, :o], dblock, n_dW[:, o:]], dim=1)
+                    impl.grads_to_params(n_convs, n_um, dW_full, n_db)
+                    r_slice = g_y
+                g_slice = r_slice if G_own is None else r_slice + G_own
+                dxp = [torch.empty_like(a) if need_x else None for a in a_p]
+                dxp.append(torch.empty_like(hpo) if need_x else None)
+                dW, db = _lin_bwd(impl, a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, has_bp,
+                                  m_p)
+                impl.grads_to_params(convs, pm, dW, db)
+                d_hpo = dxp[-1]
+            return dxp, d_hpo
+
+        # The loss's layer: its reduce-scatter (dP) has had the rest of the loss under it, so the
+        # post side goes first and its slice gradients' all-gather then runs under the user-side
+        # backward as well; lower layers keep the user side first, under their reduce-scatter.
+        if li == L - 1 and multi:
+            dxp, d_hpo = b3()
+            ag_early = _issue_slice_gathers(shard, env, pm, dxp, multi) if need_x else {}
+            dxu, dz, pending_w, d_hu = b2a()
         else:
-            d_hu = G_u if need_x else None
-        # B3 post-side projection backward (waits for the reduce-scatter)
-        dxp = []
-        d_hpo = G_own
-        if pm:
-            r_slice, r_w = R
-            r_w.wait()
-            R = None
-            if R_proj is not None:
-                # the reduce-scatter brought the next layer's dP slice: the projection's backward
-                # (S rows) gives this layer's output-slice gradient and the block's gradient
-                block, (o, k), (n_convs, n_um, n_dW, n_db, _) = R_proj
-                R_proj = None
-                g_y = torch.empty_like(ypo)
-                dblock, _ = impl.linear_bwd_raw([ypo], block, r_slice.contiguous(), None, [g_y],
-                                                True, False)
-                dW_full = torch.cat([n_dW[:, :o], dblock, n_dW[:, o:]], dim=1)
-                impl.grads_to_params(n_convs, n_um, dW_full, n_db)
-                r_slice = g_y
-            g_slice = r_slice if G_own is None else r_slice + G_own
-            dxp = [torch.empty_like(a) if need_x else None for a in a_p]
-            dxp.append(torch.empty_like(hpo) if need_x else None)
-            dW, db = _lin_bwd(impl, a_p + [hpo], Wp, g_slice.contiguous(), ypo, dxp, has_bp, m_p)
-            impl.grads_to_params(convs, pm, dW, db)
-            d_hpo = dxp[-1]
+            dxu, dz, pending_w, d_hu = b2a()
+            dxp, d_hpo = b3()
+            ag_early = None
         if not need_x:
             break
         # B4 slice gradients of the post partial sums: all-gather (in flight over B2b)
-        gath = {}
-        for j, (_, et, _) in enumerate(pm):
-            if shard.rels[et].kind[0] == "user":
-                gath[et] = env.all_gather_async(dxp[j]) if multi else (dxp[j], _Done())
+        gath = ag_early if ag_early is not None else _issue_slice_gathers(shard, env, pm, dxp,
+                                                                          multi)
         # B2b gradients into the previous layer's post table (of its projected rows when this
         # layer pre-projects: the K2 of dz) and the halo (a layer without a post side passes the
         # table through: its gradient flows on unchanged)
         G_prev = None if pm else G_full
         d_xext = None
         ai = 0
+        prev_pm = saved[li - 1][2]
+        R_split = None                          # the K2 of dz per row range, each reduce-scattered
         for j, (_, et, _) in enumerate(um):
             r = shard.rels[et]
             if j == jp:
-                G_prev = _k2_into(impl, G_prev, dz, r.csr)
+                if multi and r.halves and prev_pm and G_prev is None:
+                    # (the only contribution to this table: _pre_rel admits no other relation
+                    # into it) one reduce-scatter per range, the first under the second's K2
+                    g_sl = dz.new_empty(shard.post_rows, dz.shape[1])
+                    works = [env.reduce_scatter_async(
+                        impl.weighted_scatter_bwd_raw(dz, hf.csr, hf.w_bwd),
+                        out=g_sl[hf.lo:hf.hi])[1] for hf in r.halves]
+                    R_split = (g_sl, _AllOf(works))
+                else:
+                    G_prev = _k2_into(impl, G_prev, dz, r.csr)
                 continue
             if r.kind[0] == "post":
                 G_prev = _k2_into(impl, G_prev, dxu[ai], r.csr)
@@ -1098,17 +1234,24 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                 back, back_w = env.all_to_all_async(d_xext[n_own:].contiguous(), hl.recv_splits,
                                                     hl.send_splits)
         # the previous layer's post-table gradient is complete: its reduce-scatter starts now
-        prev_pm = saved[li - 1][2]
         if prev_pm:
-            g = G_prev if G_prev is not None else hpo.new_zeros(shard.n_posts_pad, hpo.shape[1])
-            R = env.reduce_scatter_async(g) if multi else (g, _Done())
+            if R_split is not None:
+                R = R_split
+            else:
+                g = G_prev if G_prev is not None else hpo.new_zeros(shard.n_posts_pad,
+                                                                     hpo.shape[1])
+                R = env.reduce_scatter_async(g) if multi else (g, _Done())
             if jp is not None:
                 R_proj = (proj[li][0], col_pre, pending_w)
         # B5 user rows' share of the post partial sums, then the halo rows' gradients
-        for et, (full, w) in gath.items():
-            w.wait()
+        for et, parts in gath.items():
             r = shard.rels[et]
-            impl.weighted_scatter_bwd_raw(full, r.csr, r.w_bwd, out=d_hu)
+            for hf, (full, w) in parts:       # the first range's K2 while the next one lands
+                w.wait()
+                if hf is None:
+                    impl.weighted_scatter_bwd_raw(full, r.csr, r.w_bwd, out=d_hu)
+                else:
+                    impl.weighted_scatter_bwd_raw(full, hf.csr, hf.w_bwd, out=d_hu)
         if back is not None:
             back_w.wait()
             impl.scatter_mean_bwd_raw(back, shard.halo.rel_send, out=d_hu)
