@@ -674,7 +674,7 @@ def _roofline(kern, cfg, world, pooled=False):
 def _one_pass_k1(g, cfg, roof):
     """The roofline kernel as ONE pass (no source blocking), timed with HIP events
     outside the timed region: the same algorithmic bytes over its own time."""
-    from truth_recommendation_gnn_amd import graph as G
+    from truth_recommendation_gnn_amd import graph as G, ops
     if not roof["kernel"].startswith("k_gather K1 mean fwd"):
         return None
     e = g.edge_index_dict[synth.ENGAGES]
