@@ -63,9 +63,10 @@ class EmulEnv(parallel.DistEnv):
         self.log.append(rec)
         return _Issued(self.log, rec)
 
-    def reduce_scatter_async(self, full):
+    def reduce_scatter_async(self, full, out=None):
         S = full.shape[0] // self.world
-        out = full[self.rank * S:(self.rank + 1) * S].clone()
+        mine = full[self.rank * S:(self.rank + 1) * S]
+        out = mine.clone() if out is None else out.copy_(mine)
         nbytes = full.numel() * full.element_size() * (self.world - 1) // self.world
         return out, self._issued("reduce_scatter", nbytes)
 

@@ -23,6 +23,11 @@
 
 #include <algorithm>
 #include <stdlib.h>
+#include <type_traits>
+
+#ifndef HGNN_XS_STAGGER
+#define HGNN_XS_STAGGER 1
+#endif
 
 namespace hgnn {
 
@@ -68,14 +73,16 @@ struct XStage {
       x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
     }
   }
-  // split into the three planes (plane stride PS halfwords, row stride LDP)
-  template <int LDP, int PS>
+  // split into the three planes (plane stride PS halfwords, row stride LDP).  ZERO: rows past n
+  // (clamped copies of the last row) become zeros — the backward's reductions over rows need
+  // that (0 x inf would be NaN); a forward row only reaches its own output, never stored
+  template <int LDP, int PS, bool ZERO = false>
   __device__ __forceinline__ void put(const Regs& x, unsigned short* pl, int64_t r0,
-                                      int64_t n) const {
+                                      int64_t n = 0) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       float4 v = x.v[j];
-      if (r0 + row0 + j * RSTEP >= n) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ZERO && r0 + row0 + j * RSTEP >= n) v = make_float4(0.f, 0.f, 0.f, 0.f);
       bf16x4_t p1, p2, p3;
       x6_split4(v, p1, p2, p3);
       unsigned short* d = pl + (row0 + j * RSTEP) * LDP + col;
@@ -171,54 +178,77 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   };
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   xs.issue(xr, t * R, last);
-  xs.template put<LDP, PS>(xr, pl[0], t * R, a.n);
-  __syncthreads();
-  int it = 0;
-  for (; t < n_tiles; t += G, ++it) {
-    const int b = it & 1;
-    if (it > 0) store_prev(t - G, b ^ 1);
-    if constexpr (ADD) {
+  xs.template put<LDP, PS>(xr, pl[0], t * R);
+  // Staggered halves (HGNN_XS_STAGGER): the two waves sharing a SIMD (w and w + 4) run the same
+  // program in lockstep, so both sweep (matrix pipe busy, VALU idle) and then both split (VALU
+  // busy, matrix pipe idle).  Waves 4-7 instead split the next tile FIRST — from loads issued an
+  // iteration earlier — and sweep after, so each SIMD pairs one wave's MFMAs with its partner's
+  // split.  Both orders write the other buffer and read this one between the same two barriers.
+  // A/B at the cfg4 9M-row shapes: K = 256 3.75 -> 3.59 ms, K = 128 + add 2.74 -> 2.67 ms, the
+  // backward unchanged (within noise); `s_setprio 1` for waves 4-7 on top was slower.
+  // (Measured and not kept: a prefetch two tiles deep in a second register set, with the added
+  // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256.)
+  auto loop = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    if constexpr (LATE) xs.issue(xr, (t + G) * R, last);
+    __syncthreads();
+    int it = 0;
+    for (; t < n_tiles; t += G, ++it) {
+      const int b = it & 1;
+      if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
+      if (it > 0) store_prev(t - G, b ^ 1);
+      if constexpr (ADD) {
+#pragma unroll
+        for (int r = 0; r < RT; ++r) {
+          const uint32_t row = clamp_row(t * R + 16 * r + i, last);
+          ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
+      }
+      xs.issue(xr, (t + (LATE ? 2 : 1) * G) * R, last);
+      __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
+      const unsigned short* p = pl[b];
+      f32x4 hi[RT], lo[RT];
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        const uint32_t row = clamp_row(t * R + 16 * r + i, last);
-        ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+        hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
+          const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
+          const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
+          x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
+        }
       }
-      __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
-    }
-    xs.issue(xr, (t + G) * R, last);
-    __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
-    const unsigned short* p = pl[b];
-    f32x4 hi[RT], lo[RT];
+      // the stored rows' registers are reserved until here (see above)
 #pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int r = 0; r < RT; ++r)
+        asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
-        const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
-        const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
-        x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
+      for (int r = 0; r < RT; ++r) {
+        float4 v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
+                               x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
+        if constexpr (ADD) {
+          v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
+        }
+        if (a.relu) v = relu4(v);
+        po[r] = v;
+        if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
       }
+      if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
+      __syncthreads();
     }
-    // the stored rows' registers are reserved until here (see above)
-#pragma unroll
-    for (int r = 0; r < RT; ++r)
-      asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      float4 v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
-                             x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
-      if constexpr (ADD) {
-        v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
-      }
-      if (a.relu) v = relu4(v);
-      po[r] = v;
-      if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
-    }
-    xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R, a.n);
-    __syncthreads();
+    store_prev(t - G, (it - 1) & 1);
+  };
+#if HGNN_XS_STAGGER
+  if (w >= 4) {
+    loop(std::true_type{});
+  } else {
+    loop(std::false_type{});
   }
-  store_prev(t - G, (it - 1) & 1);
+#else
+  loop(std::false_type{});
+#endif
 }
 
 // ---------------------------------------------------------------- backward
@@ -302,7 +332,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       *reinterpret_cast<bf16x4_t*>(d + ZS) = p2;
       *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
     }
-    if constexpr (WG) xs.template put<LDX, XS>(xr, xp[b], tt * R, a.n);
+    if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
   };
   f32x4 hw[WG ? 8 : 1][KT], lw[WG ? 8 : 1][KT];
 #pragma unroll
@@ -323,81 +353,96 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   issue(t);
   put(t, 0);
-  __syncthreads();
-  for (int it = 0; t < n_tiles; t += G, ++it) {
-    const int b = it & 1;
-    // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
-    // wait leaves the prefetch in flight
-    float4 dxo[DT][ACC ? R / 16 : 1];
-    if constexpr (ACC) {
+  // staggered halves as in the forward: waves 4-7 put the next tile first, then sweep
+  auto loop = [&](auto late_c) {
+    constexpr bool LATE = decltype(late_c)::value;
+    if constexpr (LATE) issue(t + G);
+    __syncthreads();
+    for (int it = 0; t < n_tiles; t += G, ++it) {
+      const int b = it & 1;
+      if constexpr (LATE) put(t + G, b ^ 1);
+      // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
+      // wait leaves the prefetch in flight
+      float4 dxo[DT][ACC ? R / 16 : 1];
+      if constexpr (ACC) {
 #pragma unroll
-      for (int u = 0; u < DT; ++u) {
-        if (dxp[u]) {
+        for (int u = 0; u < DT; ++u) {
+          if (dxp[u]) {
 #pragma unroll
-          for (int r = 0; r < R / 16; ++r)
-            dxo[u][r] = *reinterpret_cast<const float4*>(
-                dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    issue(t + G);   // consumed by put() at the end of this iteration, unconditionally (see forward)
-    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
-    const unsigned short* z = zp[b];
-    f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
-    if constexpr (DX) {
-#pragma unroll
-      for (int r = 0; r < R / 16; ++r) {
-#pragma unroll
-        for (int u = 0; u < DT; ++u) dh[u][r] = dl[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < HS; ++s) {
-          const bf16x8_t x1 = row8<LDZ>(z, 16 * r, 32 * s, i, g);
-          const bf16x8_t x2 = row8<LDZ>(z + ZS, 16 * r, 32 * s, i, g);
-          const bf16x8_t x3 = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s, i, g);
-#pragma unroll
-          for (int u = 0; u < DT; ++u) x6_mma(wt[u][s], x1, x2, x3, dh[u][r], dl[u][r]);
-        }
-      }
-    }
-    if constexpr (WG) {
-      const unsigned short* x = xp[b];
-      bf16x8_t xb[KT][3];
-#pragma unroll
-      for (int u = 0; u < KT; ++u)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) xb[u][q] = tr8<LDX>(x + q * XS, 16 * (KT * w + u), lane);
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        bf16x8_t za[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) za[q] = tr8<LDZ>(z + q * ZS, 16 * h, lane);
-#pragma unroll
-        for (int u = 0; u < KT; ++u) x6_mma(za, xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
-      }
-    }
-    if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
-#pragma unroll
-      for (int u = 0; u < DT; ++u)
-#pragma unroll
-        for (int r = 0; r < R / 16; ++r) {
-          const int64_t row = t * R + 16 * r + i;
-          if (dxp[u] && row < a.n) {
-            float4 v = make_float4(x6_out(dh[u][r][0], dl[u][r][0]), x6_out(dh[u][r][1], dl[u][r][1]),
-                                   x6_out(dh[u][r][2], dl[u][r][2]), x6_out(dh[u][r][3], dl[u][r][3]));
-            if constexpr (ACC) {
-              if (acc_dx[u]) {
-                v.x = dxo[u][r].x + v.x; v.y = dxo[u][r].y + v.y; v.z = dxo[u][r].z + v.z;
-                v.w = dxo[u][r].w + v.w;
-              }
-            }
-            *reinterpret_cast<float4*>(dxp[u] + row * dxld[u] + 4 * g) = v;
+            for (int r = 0; r < R / 16; ++r)
+              dxo[u][r] = *reinterpret_cast<const float4*>(
+                  dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
           }
         }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      issue(t + (LATE ? 2 : 1) * G);   // consumed by the next put(), unconditionally (see forward)
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
+      const unsigned short* z = zp[b];
+      f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
+      if constexpr (DX) {
+#pragma unroll
+        for (int r = 0; r < R / 16; ++r) {
+#pragma unroll
+          for (int u = 0; u < DT; ++u) dh[u][r] = dl[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s = 0; s < HS; ++s) {
+            const bf16x8_t x1 = row8<LDZ>(z, 16 * r, 32 * s, i, g);
+            const bf16x8_t x2 = row8<LDZ>(z + ZS, 16 * r, 32 * s, i, g);
+            const bf16x8_t x3 = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s, i, g);
+#pragma unroll
+            for (int u = 0; u < DT; ++u) x6_mma(wt[u][s], x1, x2, x3, dh[u][r], dl[u][r]);
+          }
+        }
+      }
+      if constexpr (WG) {
+        const unsigned short* x = xp[b];
+        bf16x8_t xb[KT][3];
+#pragma unroll
+        for (int u = 0; u < KT; ++u)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) xb[u][q] = tr8<LDX>(x + q * XS, 16 * (KT * w + u), lane);
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          bf16x8_t za[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q) za[q] = tr8<LDZ>(z + q * ZS, 16 * h, lane);
+#pragma unroll
+          for (int u = 0; u < KT; ++u) x6_mma(za, xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
+        }
+      }
+      if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
+#pragma unroll
+        for (int u = 0; u < DT; ++u)
+#pragma unroll
+          for (int r = 0; r < R / 16; ++r) {
+            const int64_t row = t * R + 16 * r + i;
+            if (dxp[u] && row < a.n) {
+              float4 v = make_float4(x6_out(dh[u][r][0], dl[u][r][0]), x6_out(dh[u][r][1], dl[u][r][1]),
+                                     x6_out(dh[u][r][2], dl[u][r][2]), x6_out(dh[u][r][3], dl[u][r][3]));
+              if constexpr (ACC) {
+                if (acc_dx[u]) {
+                  v.x = dxo[u][r].x + v.x; v.y = dxo[u][r].y + v.y; v.z = dxo[u][r].z + v.z;
+                  v.w = dxo[u][r].w + v.w;
+                }
+              }
+              *reinterpret_cast<float4*>(dxp[u] + row * dxld[u] + 4 * g) = v;
+            }
+          }
+      }
+      if constexpr (!LATE) put(t + G, b ^ 1);
+      __syncthreads();
     }
-    put(t + G, b ^ 1);
-    __syncthreads();
+  };
+#if HGNN_XS_STAGGER
+  if (w >= 4) {
+    loop(std::true_type{});
+  } else {
+    loop(std::false_type{});
   }
+#else
+  loop(std::false_type{});
+#endif
   if constexpr (WG) {
     constexpr int KEXT = K + 1;
     float* slab = a.slab + (int64_t)blockIdx.x * kH * KEXT;
