@@ -30,7 +30,7 @@ def main():
             objs.append(objdir / (src.stem + ".o"))
             continue
         obj = vdir / (src.stem + ".o")
-        r = subprocess.run([B.HIPCC, *B.FLAGS, *rest, "-c", str(src), "-o", str(obj)],
+        r = subprocess.run([B.HIPCC, *B.FLAGS, *B.FILE_FLAGS.get(src.stem, []), *rest, "-c", str(src), "-o", str(obj)],
                            capture_output=True, text=True)
         if r.returncode:
             raise SystemExit(r.stderr)

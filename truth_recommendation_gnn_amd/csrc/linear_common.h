@@ -102,28 +102,22 @@ __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1
 // double (scripts/k3_x6_probe.hip; the large product and the five small ones kept in separate
 // accumulators), with v_mfma_f32_16x16x32_bf16 (16 cycles per 16x16x32) doing 24 MFMAs per
 // 16 x 16 x 128 tile where the f32 form needs 32 of v_mfma_f32_16x16x4_f32 at 32 cycles.
-// Non-finite values: v1 = bf16(v) carries an inf (or NaN) and the residual pieces are finite
-// (x6_res), and a result whose large product sum is +-inf is that inf (x6_out): the small
-// products of an inf with W's residual pieces, whose signs differ, would otherwise turn it into
-// NaN.  So an inf input gives the +-inf (or NaN) the f32 kernels give; a finite |v| above the
-// largest bf16 (3.39e38, which rounds to inf) is the one case that differs.
+// Non-finite values: v1 = bf16(v) carries an inf (or NaN) into the large product, whose
+// accumulator holds nothing else; the residual pieces of an inf are NaN (inf - inf), so the small
+// products' accumulator turns NaN (as it may from an inf times W's mixed-sign residual pieces),
+// and x6_out takes a large-product sum of +-inf as the result on its own.  So an inf input gives
+// the +-inf (or NaN) the f32 kernels give; a finite |v| above the largest bf16 (3.39e38, which
+// rounds to inf) is the one case that differs.  (Round 3 also clamped each residual to a finite
+// value with a v_med3 per element; x6_out makes that redundant.)
 __device__ __forceinline__ unsigned short x6_bf16(float f) {
   return __bfloat16_as_ushort(__float2bfloat16(f));   // round to nearest even (v_cvt_pk_bf16_f32)
 }
 __device__ __forceinline__ float x6_f32(unsigned short b) {
   return __uint_as_float(((unsigned)b) << 16);
 }
-// the residual after a piece, clamped to +-2^100: finite residuals (|r| <= 2^-8 |v|) pass
-// unchanged; v = +-inf gives inf - inf = NaN and a v near FLT_MAX whose piece rounded to inf
-// gives -+inf — both become a finite residual that cannot turn the inf product x1 w1 into NaN.
-// v_med3_f32 with IEEE NaN handling (a NaN operand yields the median of the other two, here
-// 2^100; scripts/probe_minmax.hip on the GPU) is one instruction where the isfinite test and its
-// select were two per element.
+// the residual after a piece (exact: v and its bf16 rounding share the exponent range)
 __device__ __forceinline__ float x6_res(float v, unsigned short piece) {
-  const float r = v - x6_f32(piece);
-  float c;
-  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(c) : "v"(r), "v"(-0x1p100f), "v"(0x1p100f));
-  return c;
+  return v - x6_f32(piece);
 }
 __device__ __forceinline__ void x6_split1(float v, unsigned short& a1, unsigned short& a2,
                                           unsigned short& a3) {
@@ -156,9 +150,14 @@ __device__ __forceinline__ void x6_split4(const float4& u, bf16x4_t& p1, bf16x4_
     p3[j] = (short)a3;
   }
 }
-// hi + lo of the split's two accumulators, hi alone when it is +-inf (see above)
+// hi + lo of the split's two accumulators, hi alone when it is +-inf (see above): lo clamped to
+// +-FLT_MAX by one v_med3_f32 (IEEE mode: a NaN lo yields the median of the bounds, +FLT_MAX),
+// so an infinite hi survives the add and a finite hi gets its finite lo unchanged.  One
+// instruction in place of the class test and select (probe: scripts/probe_minmax.hip)
 __device__ __forceinline__ float x6_out(float hi, float lo) {
-  return __builtin_isinf(hi) ? hi : hi + lo;
+  float c;
+  asm("v_med3_f32 %0, %1, %2, %3" : "=v"(c) : "v"(lo), "v"(-0x1.fffffep127f), "v"(0x1.fffffep127f));
+  return hi + c;
 }
 
 // acc_hi += w1 x1; acc_lo += w2 x2 + w3 x1 + w1 x3 + w2 x1 + w1 x2 (small terms first)

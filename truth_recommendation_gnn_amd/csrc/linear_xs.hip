@@ -25,6 +25,12 @@
 #include <stdlib.h>
 #include <type_traits>
 
+#ifndef HGNN_XS_LDSPF
+#define HGNN_XS_LDSPF 2
+#endif
+#ifndef HGNN_XS_LDSPF_DXWG
+#define HGNN_XS_LDSPF_DXWG 1
+#endif
 #ifndef HGNN_XS_STAGGER
 #define HGNN_XS_STAGGER 1
 #endif
@@ -209,6 +215,34 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
       __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
       const unsigned short* p = pl[b];
       f32x4 hi[RT], lo[RT];
+#if HGNN_XS_LDSPF
+      // software-pipelined sweep: step q = (r, s) reads its three fragments LDSPF steps ahead,
+      // pinned as [3 ds_read (step q + LDSPF)] [6 MFMA (step q)] by scheduling barriers (the
+      // compiler otherwise issues each step's reads right before its MFMAs and waits on them)
+      {
+        constexpr int NQ = RT * KS, PF = HGNN_XS_LDSPF;
+        bf16x8_t fr[PF + 1][3];
+        auto ld = [&](int q, bf16x8_t (&f)[3]) {
+          const int r = q / KS, s2 = q % KS;
+          f[0] = row8<LDP>(p, 16 * r, 32 * s2, i, g);
+          f[1] = row8<LDP>(p + PS, 16 * r, 32 * s2, i, g);
+          f[2] = row8<LDP>(p + 2 * PS, 16 * r, 32 * s2, i, g);
+        };
+#pragma unroll
+        for (int r = 0; r < RT; ++r) hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < PF; ++q) ld(q, fr[q]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
+          __builtin_amdgcn_sched_barrier(0);
+          x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
+                 hi[q / KS], lo[q / KS]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
         hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -220,6 +254,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
           x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
         }
       }
+#endif
       // the stored rows' registers are reserved until here (see above)
 #pragma unroll
       for (int r = 0; r < RT; ++r)
@@ -380,6 +415,65 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
       const unsigned short* z = zp[b];
       f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
+#if HGNN_XS_LDSPF
+      // the sweeps software-pipelined as in the forward: each step's fragments are read PF
+      // steps ahead, pinned by scheduling barriers
+      constexpr int PF = DX && WG ? HGNN_XS_LDSPF_DXWG : HGNN_XS_LDSPF;   // registers: see the header
+      if constexpr (DX) {
+        constexpr int NQ = (R / 16) * HS;
+        bf16x8_t fr[PF + 1][3];
+        auto ld = [&](int q, bf16x8_t (&f)[3]) {
+          const int r = q / HS, s2 = q % HS;
+          f[0] = row8<LDZ>(z, 16 * r, 32 * s2, i, g);
+          f[1] = row8<LDZ>(z + ZS, 16 * r, 32 * s2, i, g);
+          f[2] = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s2, i, g);
+        };
+#pragma unroll
+        for (int r = 0; r < R / 16; ++r)
+#pragma unroll
+          for (int u = 0; u < DT; ++u) dh[u][r] = dl[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < PF; ++q) ld(q, fr[q]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
+          __builtin_amdgcn_sched_barrier(0);
+          const bf16x8_t(&f)[3] = fr[q % (PF + 1)];
+#pragma unroll
+          for (int u = 0; u < DT; ++u)
+            x6_mma(wt[u][q % HS], f[0], f[1], f[2], dh[u][q / HS], dl[u][q / HS]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (WG) {
+        const unsigned short* x = xp[b];
+        bf16x8_t xb[KT][3];
+#pragma unroll
+        for (int u = 0; u < KT; ++u)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) xb[u][q] = tr8<LDX>(x + q * XS, 16 * (KT * w + u), lane);
+        bf16x8_t za[PF + 1][3];
+#pragma unroll
+        for (int h = 0; h < PF; ++h)
+#pragma unroll
+          for (int q = 0; q < 3; ++q) za[h][q] = tr8<LDZ>(z + q * ZS, 16 * h, lane);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 8; ++h) {
+          if (h + PF < 8) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              za[(h + PF) % (PF + 1)][q] = tr8<LDZ>(z + q * ZS, 16 * (h + PF), lane);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int u = 0; u < KT; ++u)
+            x6_mma(za[h % (PF + 1)], xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
       if constexpr (DX) {
 #pragma unroll
         for (int r = 0; r < R / 16; ++r) {
@@ -411,6 +505,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
           for (int u = 0; u < KT; ++u) x6_mma(za, xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
         }
       }
+#endif
       if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
 #pragma unroll
         for (int u = 0; u < DT; ++u)
