@@ -54,10 +54,10 @@ typedef __attribute__((address_space(3))) v4s lds_v4s;
 // t is f = t + 512 j, row f / (K / 4), column 4 (f % (K / 4)) — a thread's column (and therefore
 // its 16-column chunk of the ChunkTab) is fixed, its rows step by 512 / (K / 4).  Row indices
 // are 32-bit (the host checks n < 2^31): one v_mad_u64_u32 per row address.
-template <int K, int R>
+template <int K, int R, int THR = kThr>
 struct XStage {
-  static constexpr int NL = R * K / 4 / kThr;
-  static constexpr int RSTEP = kThr / (K / 4);
+  static constexpr int NL = R * K / 4 / THR;
+  static constexpr int RSTEP = THR / (K / 4);
   struct Regs {
     float4 v[NL];
   };
@@ -191,7 +191,10 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   // iteration earlier — and sweep after, so each SIMD pairs one wave's MFMAs with its partner's
   // split.  Both orders write the other buffer and read this one between the same two barriers.
   // A/B at the cfg4 9M-row shapes: K = 256 3.75 -> 3.59 ms, K = 128 + add 2.74 -> 2.67 ms, the
-  // backward unchanged (within noise); `s_setprio 1` for waves 4-7 on top was slower.
+  // backward unchanged (within noise); `s_setprio 1` for waves 4-7 on top was slower.  Also
+  // measured and not kept: 4 waves of 512 registers, each with 32 output columns (half the LDS
+  // reads per MFMA) and the next tile's split interleaved into its own sweep by scheduling group
+  // barriers — correct, but 3.39 -> 3.78 ms at K = 256, 2.59 -> 2.84 ms at K = 128 + add.
   // (Measured and not kept: a prefetch two tiles deep in a second register set, with the added
   // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256.)
   auto loop = [&](auto late_c) {
@@ -418,7 +421,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
 #if HGNN_XS_LDSPF
       // the sweeps software-pipelined as in the forward: each step's fragments are read PF
       // steps ahead, pinned by scheduling barriers
-      constexpr int PF = DX && WG ? HGNN_XS_LDSPF_DXWG : HGNN_XS_LDSPF;   // registers: see the header
+      // the fused dgrad + wgrad kernels are at the register limit: fewer fragments ahead there
+      constexpr int PF = DX && WG ? (ACC ? 0 : HGNN_XS_LDSPF_DXWG) : HGNN_XS_LDSPF;
       if constexpr (DX) {
         constexpr int NQ = (R / 16) * HS;
         bf16x8_t fr[PF + 1][3];
