@@ -252,15 +252,22 @@ __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
   }
 }
 
+// HGNN_GATHER_LDS (a measurement build, scripts/fuse_occupancy_probe.py): dynamic LDS per block
+// that caps the waves per CU, to time the gather at the occupancy a kernel fused with K3 would have
+#ifndef HGNN_GATHER_LDS
+#define HGNN_GATHER_LDS 0
+#endif
+
 template <int LPR, int VPL, int W, int UNROLL>
 static int launch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) {
   const dim3 grid((unsigned)cdiv(a.n_items, 4)), block(256);
+  constexpr unsigned lds = HGNN_GATHER_LDS;
   if (a.score)
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false, true>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false, true>), grid, block, lds, stream, a);
   else if (has_w)
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, lds, stream, a);
   else
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, 0, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, lds, stream, a);
   return check_launch("k_gather");
 }
 
