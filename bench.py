@@ -113,7 +113,7 @@ def parse(argv=None):
                         "cfg4's 1/8 shard, ~62 s each on 16 cores, else 3)")
     p.add_argument("--cpu-shard", type=int, default=None,
                    help="full-batch configs: time rank 0's 1/S destination shard on the CPU oracle "
-                        "(default: cfg4 64, cfg2/cfg3 1 = the whole graph)")
+                        "(default: cfg4 8, cfg2/cfg3 1 = the whole graph)")
     p.add_argument("--profile-steps", action="store_true",
                    help="no per-kernel-event run (for rocprofv3 runs)")
     p.add_argument("--dist-backend", default="nccl",
@@ -213,9 +213,9 @@ def cpu_baseline(cfg, threads=None, scale=None):
 
 
 # SURVEY §8d's CPU baseline for the full-batch configs: cfg2 / cfg3 whole, cfg4 (which needs
-# >100 GB per materialised [E, d] relation on the oracle) as a destination shard.  The default
-# cfg4 shard keeps the bench's CPU leg to ~30 s; `--cpu-shard 8` is the verdict's 1/8 shard
-# (about 2 minutes, recorded separately under profiles/).
+# >100 GB per materialised [E, d] relation on the oracle) as a destination shard: the 1/8 shard
+# SURVEY §8d names (rank 0 of the 8-GPU split), one timed step after one warm-up, ~2 minutes of
+# the bench's wall time on 16 cores.
 CPU_SHARD = {"cfg4": 8}
 
 
@@ -767,8 +767,6 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     if sharded:
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    # one rank: the step (forward, loss, backward, Adam) replayed as a HIP graph over
-    # static-capacity blocks (minibatch.py); the sampler stays eager (two syncs per hop)
     # the step (forward, loss, backward, Adam) replayed as a HIP graph over static-capacity
     # blocks (minibatch.py); the sampler stays eager (two syncs per hop).  N > 1: the forward +
     # loss + backward graph, the eager all-reduce of the gradients, then the Adam graph.

@@ -145,10 +145,21 @@ int exclusive_scan_i32(const int32_t* in, int32_t* out, int64_t n, void* ws, siz
 // ------------------------------------------------------------------------------------------
 // Stable LSD radix sort of (key32, idx32) pairs, 8-bit digits.
 // ------------------------------------------------------------------------------------------
-constexpr int kSortThreads = 256;
-constexpr int kSortRounds = 16;                           // one item per thread per round
-constexpr int kSortTile = kSortThreads * kSortRounds;     // 4096 items per block
-constexpr int kMaxRadix = 512;
+// 8192-item tiles (512 threads x 16 rounds; round 4): per 7-bit digit a tile writes runs of ~64
+// items instead of ~32.  A/B on the cfg4 negatives (200M draws over 1M posts, scripts/
+// gpu_sort_ab.sh): 3.03 ms at 256 x 16, 3.42 at 256 x 32, 2.87 at 512 x 16; two passes of
+// 10-bit digits (32 B per pair moved instead of ~52) measured 4.1-4.7 ms at every tile size —
+// the ranking's ballots and the 1024-digit tables cost more than the third pass's bytes.
+#ifndef HGNN_SORT_THREADS
+#define HGNN_SORT_THREADS 512
+#endif
+#ifndef HGNN_SORT_ROUNDS
+#define HGNN_SORT_ROUNDS 16
+#endif
+constexpr int kSortThreads = HGNN_SORT_THREADS;
+constexpr int kSortRounds = HGNN_SORT_ROUNDS;             // one item per thread per round
+constexpr int kSortTile = kSortThreads * kSortRounds;     // 8192 items per block
+constexpr int kMaxRadix = 1024;
 
 // key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
 __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
@@ -204,7 +215,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
     counts[(int64_t)dd * gridDim.x + tile] = hist[dd];
 }
 
-// Stable scatter, block-local sort first.  Tile = 4096 items; wave w owns the contiguous
+// Stable scatter, block-local sort first.  Tile = kSortTile items; wave w owns the contiguous
 // items [w*1024, (w+1)*1024) and walks them in 16 rounds of 64, ranking each item among equal
 // digits with BITS ballots and a wave-private running count in LDS (no block barrier per round).
 // The tile is then reordered by (digit, original index) in LDS and written out in per-digit
@@ -422,7 +433,7 @@ static void radix_plan(int64_t n_keys, int* passes, int* bits) {
   *bits = best;
   *passes = (b + best - 1) / best;
   static const int forced = getenv("HGNN_SORT_BITS") ? atoi(getenv("HGNN_SORT_BITS")) : 0;
-  if (forced >= 6 && forced <= 9) {   // measurement override
+  if (forced >= 6 && forced <= 10) {   // measurement override
     *bits = forced;
     *passes = (b + forced - 1) / forced;
   }
@@ -434,6 +445,7 @@ static void radix_plan(int64_t n_keys, int* passes, int* bits) {
     case 6: M(6); break;          \
     case 7: M(7); break;          \
     case 8: M(8); break;          \
+    case 10: M(10); break;        \
     default: M(9); break;         \
   }
 
