@@ -197,7 +197,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   // barriers — correct, but 3.39 -> 3.78 ms at K = 256, 2.59 -> 2.84 ms at K = 128 + add; and
   // specialised waves (12 per block: 8 MFMA waves as here, 4 that only load and split, one per
   // SIMD) — 3.41 -> 3.37 ms and 2.61 -> 2.50 ms, at the 168-register limit of three waves per
-  // SIMD (spills at K = 256 + add): too little for a second forward kernel.
+  // SIMD (spills at K = 256 + add): too little for a second forward kernel.  Larger tiles (48
+  // rows at K = 256, 80 at K = 128: fewer barriers and epilogue phases per MFMA) measured the
+  // same (3.52 / 3.49 ms, 2.68 / 2.69 ms).
   // (Measured and not kept: a prefetch two tiles deep in a second register set, with the added
   // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256.)
   auto loop = [&](auto late_c) {
