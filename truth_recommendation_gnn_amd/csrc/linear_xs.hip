@@ -71,7 +71,9 @@ struct XStage {
     base = tab.x[c] + tab.col[c] + (col & 15);
     ld = (uint32_t)tab.ld[c];
   }
-  // rows past the end are clamped to the last row (loaded, never stored)
+  // rows past the end are clamped to the last row (loaded, never stored).  (Measured and not
+  // kept: a uniform in-range test per tile taking one v_mad_u64_u32 and 64-bit adds for the row
+  // addresses — fewer VALU, but 3.42 -> 3.46 ms at K = 256 forward, 3.55 -> 3.64 backward.)
   __device__ __forceinline__ void issue(Regs& x, int64_t r0, int32_t last) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
