@@ -109,7 +109,8 @@ __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1
 // the +-inf (or NaN) the f32 kernels give; a finite |v| above the largest bf16 (3.39e38, which
 // rounds to inf) is the one case that differs.  (Round 3 also clamped each residual to a finite
 // value with a v_med3 per element; x6_out makes that redundant.)
-// two values at once: one v_cvt_pk_bf16_f32 per piece pair, whose packed word is already the
+
+// The split, two values at once: one v_cvt_pk_bf16_f32 per piece pair, whose packed word is already the
 // operand layout (a in the low half); the pieces' f32 values are the word shifted (low half) or
 // masked (high half); the residuals are exact.  (Element-wise, the compiler emits one
 // convert per value plus a v_perm per pair to pack them — ~7.75 instead of 5.5 VALU per value.)
