@@ -4,7 +4,8 @@ cfg4 (the north-star graph: 9M users, 1M posts, 200M engages + the reverse relat
 ``HeteroSAGE`` with 2 layers as the bench builds it — the layer-2 post -> user relation
 pre-projected (``ops.use_pre_projection``), the gathers over the 4.6 GB user-side tables in
 source-block passes (``ops.gather_blocks``) — then ``ops.edge_bce_loss`` with a ``NegativeDraw``
-(the bench's counter-based negatives, drawn and grouped inside the loss) and ``backward()``.
+(the bench's counter-based negatives, grouped by post on a side stream under the forward as the
+bench does, ``presorted=``) and ``backward()``.
 The loss, both layers' outputs and EVERY parameter gradient are compared with
 ``tests/f64_step.py`` (plain torch float64 on the GPU, aggregate-then-project, hand-written
 backward) at the north_star's rtol 1e-4, read against each tensor's largest entry.  The negatives
@@ -56,9 +57,17 @@ def test_bench_step_matches_float64(name):
     timer = ops.KernelTimer()            # only to see which launches the step made
     ops.set_timer(timer)
     try:
+        # as the bench: the negatives grouped by post on a side stream under the forward
+        main, side = torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            pre = ops.presort_negatives(cfg.num_users, cfg.num_posts, pos, draw)
+        pre.rowptr.record_stream(main)
+        pre.users.record_stream(main)
         out = model(g.x_dict, e)
+        main.wait_stream(side)
         loss = ops.edge_bce_loss(out["user"], out["post"], pos, draw, pw, neg_order="user",
-                                 check=False, cscale=cscale)
+                                 check=False, cscale=cscale, presorted=pre)
         loss.backward()
     finally:
         ops.set_timer(None)

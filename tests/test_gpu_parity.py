@@ -710,6 +710,44 @@ def test_fused_loss_negative_draw_equals_materialised():
 
 
 @pytest.mark.parametrize("neg_kind", ["int32", "draw"])
+def test_autograd_loss_presorted_on_side_stream_is_bitwise(neg_kind):
+    """edge_bce_loss(presorted=...) with the grouping done ahead on a side stream (the bench's N = 1
+    step) gives bitwise the loss and gradients of the grouping inside the loss; presorted
+    negatives of other draws are refused."""
+    z, x, e, params = _fixture_cfg1()
+    model = WeightedRGCN(hidden_dim=64).to(DEV)
+    model.load_state_dict(params)
+    with torch.no_grad():
+        out = model(x, e)
+    pos = e[synth.ENGAGES]
+    pw = torch.from_numpy(z["pos_weights"]).to(DEV)
+    nu, np_ = out["user"].shape[0], out["post"].shape[0]
+    dr = ops.draw_negatives(pos, np_, generator=torch.Generator(device=DEV).manual_seed(5))
+    neg = dr if neg_kind == "draw" else dr.tensor()
+    res = []
+    for presort in (False, True):
+        U, P = out["user"].clone().requires_grad_(), out["post"].clone().requires_grad_()
+        pre = None
+        if presort:
+            main, side = torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                pre = ops.presort_negatives(nu, np_, pos, neg)
+            pre.rowptr.record_stream(main)
+            pre.users.record_stream(main)
+            main.wait_stream(side)
+        loss = ops.edge_bce_loss(U, P, pos, neg, pw, neg_order="user", presorted=pre)
+        loss.backward()
+        res.append((loss.detach(), U.grad, P.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    other = ops.draw_negatives(pos, np_, generator=torch.Generator(device=DEV).manual_seed(6))
+    with pytest.raises(ValueError):
+        ops.edge_bce_loss(out["user"], out["post"], pos, other, pw, neg_order="user",
+                          presorted=pre)
+
+
+@pytest.mark.parametrize("neg_kind", ["int32", "draw"])
 def test_loss_dp_gather_in_row_blocks_is_bitwise_one_pass(neg_kind):
     """The sharded step's dP gather over the post table as it lands in row blocks (p_chunks: each
     block's positives a rowptr slice with its own skew plan, _row_range) gives bitwise the loss,

@@ -1054,8 +1054,9 @@ class _EdgeBCELoss(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
-                ready=None):
-        loss, dU, dP = _edge_bce(U, P, csr, neg_u_order, cscale, check, n_total, ready)
+                ready=None, presorted=None):
+        loss, dU, dP = _edge_bce(U, P, csr, neg_u_order, cscale, check, n_total, ready,
+                                 presorted=presorted)
         ctx.grads = (dU, dP)
         ctx.save_for_backward(U, P)
         ctx.args = (csr, neg_u_order, cscale, n_total)
@@ -1076,14 +1077,15 @@ class _EdgeBCELoss(torch.autograd.Function):
         for t in (dU, dP):   # in place; a no-op launch for loss.backward()'s gradient of 1
             N.check(lib.hgnn_scale_unless_one(N.ptr(t), t.numel(), N.ptr(g), s),
                     "hgnn_scale_unless_one")
-        return dU, dP, None, None, None, None, None, None
+        return dU, dP, None, None, None, None, None, None, None
 
 
 def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
                   neg_p: torch.Tensor, pos_weights: Optional[torch.Tensor],
                   neg_order: str = "edge", check: bool = True,
                   n_edges_total: Optional[int] = None,
-                  cscale: Optional[torch.Tensor] = None, ready=None) -> torch.Tensor:
+                  cscale: Optional[torch.Tensor] = None, ready=None,
+                  presorted: Optional["PresortedNegatives"] = None) -> torch.Tensor:
     """Fused HIP version of :func:`link_loss` (same value, same gradients).
 
     ``neg_order='edge'``: ``neg_p[e]`` is the negative of COO edge e (the reference's layout);
@@ -1092,7 +1094,9 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
     ``n_edges_total`` / ``cscale`` (= mean of ALL pos_weights) let a shard of the positive edges
     produce its additive share of the global loss (parallel.py); ``ready()``, if given, is
     called once the negatives sort is enqueued and before any kernel reads ``post_emb`` (the
-    sharded path's post-table all-gather finishes under the sort)."""
+    sharded path's post-table all-gather finishes under the sort).  ``presorted``: the grouping
+    of these negatives from :func:`presort_negatives`, done ahead (e.g. on a side stream under the
+    forward; the caller orders the streams)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     if neg_p.shape[0] != csr.num_edges:
         raise ValueError("one negative per positive edge is required (train_gnn.py:272)")
@@ -1100,7 +1104,10 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
     if cscale is None:
         cscale = pos_weights.to(torch.float32).mean()
     n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
-    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total, ready)
+    if presorted is not None and presorted.key[3:] != (id(neg_p), neg_order):
+        raise ValueError("edge_bce_loss: presorted negatives of other draws")
+    return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total, ready,
+                              presorted)
 
 
 def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
