@@ -743,7 +743,8 @@ def _projection(kern):
            "flops_per_launch": int(r["flops"] / r["launches"]),
            "flops_formula": "2*N*K*H (K = sum of the input segments)",
            "hbm_frac": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "bytes_formula": "4*N*(K+H) (inputs read once, output written once)"}
+           "bytes_formula": "4*N*(K+H) (inputs read once, output written once; + 4*N*H for an added "
+                            "row block, + 16*N for the ReLU mask bits)"}
     if x6:
         # H = 128, K = 128/256 run on bf16 MFMA as an fp32-exact three-piece split:
         # six bf16 products per fp32 product, so its own MFMA ceiling is 1/6 of the dense bf16

@@ -298,7 +298,8 @@ def linear_fwd(segs: Sequence[torch.Tensor], w: torch.Tensor, b: Optional[torch.
     dev = w.device
     out = torch.empty(n, h, dtype=torch.float32, device=dev)
     k = sum(ks)
-    with _timed(f"linear_fwd[{n}x{k}->{h}]", 4 * n * (k + h), flops=2 * n * k * h):
+    nb = 4 * n * (k + h + (h if add is not None else 0)) + (16 * n if mask_out is not None else 0)
+    with _timed(f"linear_fwd[{n}x{k}->{h}]", nb, flops=2 * n * k * h):
         N.check(N.lib().hgnn_linear_fwd_mask(len(segs), N.ptr_array(segs), N.int_array(ks), n,
                                              N.ptr(w), h, N.ptr(b), N.ptr(add),
                                              1 if relu else 0, N.ptr(out), N.ptr(mask_out),
