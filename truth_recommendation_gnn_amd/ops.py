@@ -338,7 +338,7 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     k_dx = sum(k for k, dx in zip(ks, dxs) if dx is not None)
     bits = mask is not None and out_act is not None
     nb = 4 * n * (h + (h if out_act is not None and not bits else 0) + sum(ks) + k_dx) + \
-        (16 * n if bits else 0)
+        (16 * n if bits else 0) + (4 * n * h if dz_out is not None else 0)
     fl = 2 * n * h * k_dx + (2 * n * sum(ks) * h if need_w else 0)   # dgrad + wgrad
     acc = 0
     for i, on in enumerate(dx_add):
