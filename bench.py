@@ -108,9 +108,9 @@ def parse(argv=None):
                    help="default: the box's allotted CPUs (OMP_NUM_THREADS / affinity)")
     p.add_argument("--cpu-sample-scale", type=float, default=None,
                    help="cfg5: the CPU baseline's down-scaled sample")
-    p.add_argument("--cpu-steps", type=int, default=None,
-                   help="timed CPU-baseline steps (median; after one warm-up; default 1 for "
-                        "cfg4's 1/8 shard, ~62 s each on 16 cores, else 3)")
+    p.add_argument("--cpu-steps", type=int, default=3,
+                   help="timed CPU-baseline steps of the full-batch configs (median, after one "
+                        "warm-up; cfg4's 1/8 shard takes ~60 s a step on 16 cores)")
     p.add_argument("--cpu-shard", type=int, default=None,
                    help="full-batch configs: time rank 0's 1/S destination shard on the CPU oracle "
                         "(default: cfg4 8, cfg2/cfg3 1 = the whole graph)")
@@ -126,6 +126,11 @@ def parse(argv=None):
     p.add_argument("--autograd-sharded", action="store_true",
                    help="sharded path through autograd (forward + loss + backward()) instead of "
                         "UserShard.step's explicit collective schedule")
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds a collective may wait before the process group aborts the job "
+                        "(a rank that issues another collective schedule fails within minutes, "
+                        "not after the default 10; graph setup runs before the first collective "
+                        "on every rank alike)")
     p.add_argument("--rccl-normal-priority", action="store_true",
                    help="RCCL collectives on a normal-priority stream (default: high priority)")
     p.add_argument("--same-device", action="store_true",
@@ -217,8 +222,8 @@ def cpu_baseline(cfg, threads=None, scale=None):
 
 # SURVEY §8d's CPU baseline for the full-batch configs: cfg2 / cfg3 whole, cfg4 (which needs
 # >100 GB per materialised [E, d] relation on the oracle) as a destination shard: the 1/8 shard
-# SURVEY §8d names (rank 0 of the 8-GPU split), one timed step after one warm-up, ~2 minutes of
-# the bench's wall time on 16 cores.
+# SURVEY §8d names (rank 0 of the 8-GPU split), the median of 3 timed steps after one warm-up,
+# ~4 minutes of the bench's wall time on 16 cores.
 CPU_SHARD = {"cfg4": 8}
 
 
@@ -453,7 +458,13 @@ def run(args, impl=None):
         if "MASTER_ADDR" not in os.environ:          # plain `python bench.py --dist`
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                               RANK="0", WORLD_SIZE="1")
+        # a mismatched collective schedule (tests/test_collective_schedule.py guards against
+        # one) must fail inside the driver's time limit: bounded timeout, and RCCL's watchdog
+        # tears the process group down on it instead of leaving the ranks blocked
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        import datetime
         dist.init_process_group("gloo" if on_cpu else args.dist_backend,
+                                timeout=datetime.timedelta(seconds=args.dist_timeout),
                                 pg_options=_pg_options(args))
     dev = torch.device("cpu") if on_cpu else torch.device("cuda", local)
     try:
@@ -504,7 +515,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                 main = torch.cuda.current_stream(dev)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    pre = ops.presort_negatives(cfg.num_users, cfg.num_posts, pos, neg)
+                    pre = ops.presort_negatives(cfg.num_users, cfg.num_posts, pos, neg, "user")
                 pre.rowptr.record_stream(main)
                 pre.users.record_stream(main)
             out = model(g.x_dict, g.edge_index_dict)
@@ -606,7 +617,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     if not args.no_cpu_baseline and world == 1 and not on_cpu and not sharded:
         if set(et for et, _ in rels) == {synth.ENGAGES, synth.REV_ENGAGES}:
             cpu = cpu_baseline_shard(cfg, g, rels, args.cpu_threads, args.cpu_shard,
-                                     steps=args.cpu_steps or (1 if cfg.name == "cfg4" else 3))
+                                     steps=args.cpu_steps)
         else:
             cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
     strong = world == 1 or not args.weak
@@ -632,15 +643,11 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                          "note": "per-kernel HIP events, separate run after the timed region, "
                                 "every kernel on one stream (the timed steps group the loss's "
                                 "negatives on a side stream under the forward)"},
-        "kernels": {k: {"launches": v["launches"],
-                        "ms_per_step": round(v["ms"] / args.timer_steps, 4),
-                        "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
-                        "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
-                                            if v["ms"] else None),
-                        "pmc_traffic_over_algorithmic": _pmc_ratio(cfg.name, world, k),
-                        **({"TFLOP/s": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)}
-                           if v["flops"] and v["ms"] else {})}
-                    for k, v in sorted(kern.items())},
+        "kernels": _kernel_rows(kern, args.timer_steps, cfg.name, world),
+        "kernels_note": ("GB/s = algorithmic bytes (SURVEY §8d) / HIP-event time; pmc_GB/s = "
+                         "the committed PMC bytes (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_r*.json) "
+                         "/ the same time; cache_assisted: the algorithmic rate exceeds the 8 TB/s "
+                         "peak, i.e. source rows come from L2 / the Infinity Cache"),
         "loss": float(loss_t),
         "setup_s": round(setup_s, 1),
     }
@@ -723,39 +730,89 @@ def _one_pass_k1(g, cfg, roof):
             "note": "the same gather in one pass over the 4.6 GB user table (HGNN_GATHER_BLOCK_GB=0)"}
 
 
+MFMA_CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: peak engine clock the MFMA peaks are quoted at
+N_SIMDS = 1024               # 256 CUs x 4 SIMDs
+BF16_MFMA_CYCLES = 16        # v_mfma_f32_16x16x32_bf16 on one SIMD (16*16*32*2 flop / 1024 per cycle)
+
+
+def _k3_roof(n, k, h, bytes_per_launch, x6):
+    """The K3 launch's own floor in ms: max(its bytes over 8 TB/s, its matrix-core time).  On
+    the bf16x6 split every 16x16x32 fp32 tile product is 6 ``v_mfma_f32_16x16x32_bf16`` of
+    ``BF16_MFMA_CYCLES`` on one of the 1024 SIMDs at the peak clock; on the f32-input kernels
+    the flops over the fp32 MFMA peak."""
+    hbm_ms = bytes_per_launch / (HBM_PEAK_GBS * 1e9) * 1e3
+    if x6:
+        mfma = 6 * (n / 16) * (h / 16) * (k / 32)
+        mfma_ms = mfma * BF16_MFMA_CYCLES / N_SIMDS / (MFMA_CLOCK_GHZ * 1e9) * 1e3
+    else:
+        mfma_ms = 2.0 * n * k * h / (FP32_MFMA_PEAK_TFS * 1e12) * 1e3
+    return hbm_ms, mfma_ms
+
+
 def _projection(kern):
-    """The dense projection (K3) against the fp32 MFMA peak: the largest forward launch."""
+    """The dense projection (K3), the largest forward launch, against ITS OWN roof: the launch's
+    floor is max(HBM bytes / 8 TB/s, matrix-core time of the instructions it must issue) —
+    ``_k3_roof`` — and ``frac`` = floor / measured time (never above 1).  ``achieved`` and
+    ``peak`` are in fp32-GEMM TFLOP/s (2*N*K*H per launch): ``peak`` is the rate the launch
+    would reach at its floor."""
     lin = {k: v for k, v in kern.items() if k.startswith("linear_fwd[") and v["flops"]}
     if not lin:
         return None
     name = max(lin, key=lambda k: lin[k]["flops"] / lin[k]["launches"])
     r = lin[name]
-    tfs = r["flops"] / (r["ms"] * 1e-3) / 1e12
     import re
     m = re.search(r"\[(\d+)x(\d+)->(\d+)\]", name)
-    x6 = (os.environ.get("HGNN_K3_X6", "1") != "0" and m is not None and m.group(3) == "128"
-          and m.group(2) in ("128", "256"))
-    out = {"bound": "mfma", "kernel": f"k_linear_fwd K3 {name}",
-           "achieved": round(tfs, 1), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-           "frac": round(tfs / FP32_MFMA_PEAK_TFS, 4),
-           "hbm_GB/s": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9, 1),
-           "avg_launch_us": round(r["ms"] / r["launches"] * 1e3, 1),
-           "flops_per_launch": int(r["flops"] / r["launches"]),
+    n, k, h = (int(m.group(1)), int(m.group(2)), int(m.group(3))) if m else (0, 0, 0)
+    x6 = (os.environ.get("HGNN_K3_X6", "1") != "0" and h == 128 and k in (128, 256))
+    per_ms = r["ms"] / r["launches"]
+    per_bytes = r["bytes"] / r["launches"]
+    per_flops = r["flops"] / r["launches"]
+    hbm_ms, mfma_ms = _k3_roof(n, k, h, per_bytes, x6)
+    floor_ms = max(hbm_ms, mfma_ms)
+    tfs = per_flops / (per_ms * 1e-3) / 1e12
+    out = {"bound": "hbm" if hbm_ms >= mfma_ms else "mfma", "kernel": f"k_linear_fwd K3 {name}",
+           "achieved": round(tfs, 1), "peak": round(per_flops / (floor_ms * 1e-3) / 1e12, 1),
+           "unit": "TFLOP/s (fp32-GEMM equivalent)", "frac": round(floor_ms / per_ms, 4),
+           "floor_ms": {"hbm": round(hbm_ms, 4), "mfma": round(mfma_ms, 4)},
+           "avg_launch_us": round(per_ms * 1e3, 1),
+           "hbm_GB/s": round(per_bytes / (per_ms * 1e-3) / 1e9, 1),
+           "hbm_frac": round(per_bytes / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "flops_per_launch": int(per_flops),
            "flops_formula": "2*N*K*H (K = sum of the input segments)",
-           "hbm_frac": round(r["bytes"] / (r["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "bytes_per_launch": int(per_bytes),
            "bytes_formula": "4*N*(K+H) (inputs read once, output written once; + 4*N*H for an added "
                             "row block, + 16*N for the ReLU mask bits)"}
     if x6:
-        # H = 128, K = 128/256 run on bf16 MFMA as an fp32-exact three-piece split (DESIGN §5):
-        # six bf16 products per fp32 product, so its own MFMA ceiling is 1/6 of the dense bf16
-        # peak; achieved/frac stay in fp32-GEMM flops against the fp32 MFMA peak
         out["method"] = ("bf16x6: fp32-exact 3-piece bf16 split, 6 v_mfma_f32_16x16x32_bf16 "
                          "products per fp32 product, f32 accumulate")
-        out["split_mfma_ceiling_TFLOPs"] = round(BF16_MFMA_PEAK_TFS / 6, 1)
-        out["note"] = ("on the split the kernel's roof is HBM (hbm_frac; the split's MFMA "
-                       "ceiling is 2.5 PF / 6 at the nominal clock); `frac` keeps the fp32-MFMA "
-                       "view of earlier rounds")
+        out["floor_note"] = (f"mfma floor = 6*(N/16)*(H/16)*(K/32) MFMAs x {BF16_MFMA_CYCLES} "
+                             f"cycles / {N_SIMDS} SIMDs at {MFMA_CLOCK_GHZ} GHz (the launches "
+                             "measured ~1.85 GHz under load, DESIGN §5); hbm floor = bytes / "
+                             "8 TB/s")
+    else:
+        out["method"] = "f32-input MFMA (v_mfma_f32_16x16x4_f32)"
     return out
+
+
+def _kernel_rows(kern, steps, cfg_name, world):
+    """The per-kernel table: algorithmic rate, compulsory rate, and where the committed PMC
+    passes hold the kernel, the PMC byte rate beside them.  An algorithmic rate above the HBM
+    peak is marked ``cache_assisted`` (its source rows hit L2 / the Infinity Cache)."""
+    rows = {}
+    for k, v in sorted(kern.items()):
+        gbs = v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else None
+        ratio = _pmc_ratio(cfg_name, world, k)
+        row = {"launches": v["launches"], "ms_per_step": round(v["ms"] / steps, 4),
+               "GB/s": round(gbs, 1) if gbs is not None else None,
+               "compulsory_GB/s": (round(v["cbytes"] / (v["ms"] * 1e-3) / 1e9, 1)
+                                   if v["ms"] else None),
+               "pmc_traffic_over_algorithmic": ratio,
+               "pmc_GB/s": round(gbs * ratio, 1) if (gbs is not None and ratio) else None,
+               "cache_assisted": bool(gbs is not None and gbs > HBM_PEAK_GBS)}
+        if v["flops"] and v["ms"]:
+            row["TFLOP/s"] = round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 1)
+        rows[k] = row
+    return rows
 
 
 # ----------------------------------------------------------------------------- cfg5 mini-batch
@@ -850,6 +907,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         return link_loss(out)
 
     loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
+    loss_of.partial_seeds = True                 # both forms read the seed rows by local id
 
     def sync():
         parallel.sync_grads(model, env)          # no-op at world size 1
@@ -944,10 +1002,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    + (", next batch sampled on a side stream" if side is not None else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),
         "cpu_baseline": cpu,
-        "kernels": {k: {"launches": v["launches"],
-                        "ms_per_step": round(v["ms"] / args.timer_steps, 4),
-                        "GB/s": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None}
-                    for k, v in sorted(kern.items())},
+        "kernels": _kernel_rows(kern, args.timer_steps, cfg.name, world),
         "loss": float(loss.detach()), "setup_s": round(setup_s, 1),
     }
 

@@ -1,29 +1,18 @@
-"""Experiment: the loss's dP gather (hgnn_score_gather2: positives + negatives grouped by post,
-U rows from the 4.6 GB user table) at cfg4 as one pass vs B passes over user blocks (positives
-and negatives of block b per pass, accumulating into dP).  Prints ms per full dP gather.
-usage: python scripts/score_block_bench.py [B ...]"""
+"""A/B of the loss's dP gather at cfg4: one pass over the 4.6 GB user table
+(hgnn_score_gather2, nt row loads) against B source-block passes (ops._score_gather2_blocked:
+the positives from the K1 blocks of the same relation, the negatives split per block by
+hgnn_segment_bounds, passes 2.. accumulating; default-policy or nt row loads).  Times the
+`score_gather` entry of ops.KernelTimer inside the real loss call (same launches the bench
+step issues) and checks each variant's dP against the one pass.  One JSON line per variant.
+usage: python scripts/score_block_bench.py [B:cached ...]   (default 1:1 8:1 8:0 4:1 12:1)"""
+import json
 import sys
 import time
 
 import torch
 
 sys.path.insert(0, ".")
-from truth_recommendation_gnn_amd import _native as N, graph, ops, synth  # noqa: E402
-
-
-def timed(fn, reps=5):
-    fn()
-    torch.cuda.synchronize()
-    ts = []
-    for _ in range(reps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ev[0].record()
-        fn()
-        ev[1].record()
-        torch.cuda.synchronize()
-        ts.append(ev[0].elapsed_time(ev[1]))
-    ts.sort()
-    return ts[len(ts) // 2]
+from truth_recommendation_gnn_amd import ops, synth  # noqa: E402
 
 
 def main():
@@ -31,49 +20,45 @@ def main():
     cfg = synth.CONFIGS["cfg4"]
     t0 = time.time()
     g = synth.make_graph(cfg, device=dev, device_gen=True)
-    pos = g.edge_index_dict[synth.ENGAGES]            # user -> post
+    pos = g.edge_index_dict[synth.ENGAGES]
     n_u, n_p, d = cfg.num_users, cfg.num_posts, cfg.hidden
     del g
-    U = torch.randn(n_u, d, device=dev) * 0.1
-    P = torch.randn(n_p, d, device=dev) * 0.1
-    neg = torch.stack([pos[0], torch.randint(0, n_p, (pos.shape[1],), device=dev)])
-    print(f"setup {time.time() - t0:.1f}s", flush=True)
-    pc = graph.relation_csr(pos, n_u, n_p)
-    nc = graph.RelationCSR(neg, n_u, n_p, chunk=graph.NO_SPLIT)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    U = torch.randn(n_u, d, device=dev, generator=gen) * 0.1
+    P = torch.randn(n_p, d, device=dev, generator=gen) * 0.1
+    neg = ops.draw_negatives(pos, n_p, generator=gen)
     c = torch.tensor(1.3, device=dev)
-    inv_e = 1.0 / pos.shape[1]
-    ref = torch.empty(n_p, d, device=dev)
-    t_one = timed(lambda: ops._score_gather2(U, P, pc.fwd, nc.fwd, c, inv_e, ref))
-    print(f"B=1 {t_one:.3f} ms", flush=True)
-    for B in [int(b) for b in sys.argv[1:]] or [4, 8]:
-        pp, _ = pc.blocks("fwd", B)
-        npass, _ = nc.blocks("fwd", B)
-        out = torch.empty_like(ref)
-        lib = N.lib()
-
-        def run():
-            s = N.stream_ptr(dev)
-            for b in range(B):
-                gp, gn = pp[b], npass[b]
-                p = gp.plan
-                slab = (torch.empty(p.n_chunks * d, device=dev) if p.n_heavy else None)
-                if b == 0:
-                    N.check(lib.hgnn_score_gather2(
-                        N.ptr(U), n_u, N.ptr(P), d, N.ptr(gp.rowptr), N.ptr(gp.col),
-                        N.ptr(gn.rowptr), N.ptr(gn.col), n_p, N.ptr(c), inv_e,
-                        N.ptr(p.heavy_rows), N.ptr(p.heavy_first), p.n_heavy, p.n_chunks,
-                        p.chunk, N.ptr(slab), N.ptr(out), s), "sg2")
-                else:   # accumulate: positives then negatives as two score gathers
-                    for grp, mode in ((gp, 1), (gn, 2)):
-                        q = grp.plan
-                        sl = (torch.empty(q.n_chunks * d, device=dev) if q.n_heavy else None)
-                        N.check(lib.hgnn_score_gather(
-                            N.ptr(U), n_u, N.ptr(P), d, N.ptr(grp.rowptr), N.ptr(grp.col), n_p,
-                            mode, N.ptr(c), inv_e, N.ptr(q.heavy_rows), N.ptr(q.heavy_first),
-                            q.n_heavy, q.n_chunks, q.chunk, N.ptr(sl), N.ptr(out), 1, s), "sg")
-        t = timed(run)
-        err = float((out - ref).abs().max() / ref.abs().max())
-        print(f"B={B} {t:.3f} ms ({t_one / t:.3f}x) rel_err={err:.2e}", flush=True)
+    E = int(pos.shape[1])
+    print(f"setup {time.time() - t0:.1f}s", flush=True)
+    variants = [tuple(int(x) for x in a.split(":")) for a in sys.argv[1:]] or \
+        [(1, 1), (8, 1), (8, 0), (4, 1), (12, 1)]
+    ref = None
+    for B, cached in variants:
+        ops.DP_BLOCKS, ops.DP_CACHED = str(B), bool(cached)
+        out = ops.edge_bce_loss_raw(U, P, pos, neg, E, c)        # warm-up (blocks built here)
+        dp = out[2].clone()
+        del out
+        timer = ops.KernelTimer()
+        ops.set_timer(timer)
+        reps = 3
+        for _ in range(reps):
+            out = ops.edge_bce_loss_raw(U, P, pos, neg, E, c)
+            del out
+        ops.set_timer(None)
+        summ = timer.summary()
+        k = [n for n in summ if n.startswith("score_gather")][0]
+        ms = summ[k]["ms"] / summ[k]["launches"]
+        gbs = summ[k]["bytes"] / summ[k]["launches"] / (ms * 1e-3) / 1e9
+        rec = {"B": B, "cached_loads": bool(cached) if B > 1 else False, "dp_gather_ms": round(ms, 3),
+               "algorithmic_GB/s": round(gbs, 1), "frac_8TBs": round(gbs / 8000, 4),
+               "edge_score_ms": round(summ["edge_score_d128"]["ms"] / reps, 3)}
+        if ref is None and B == 1:
+            ref = dp
+        if ref is not None:
+            rec["dP_rel_err_vs_one_pass"] = float((dp - ref).abs().max() / ref.abs().max())
+        print(json.dumps(rec), flush=True)
+        del dp
+    ops.DP_BLOCKS = "1"
 
 
 if __name__ == "__main__":

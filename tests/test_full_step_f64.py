@@ -61,7 +61,7 @@ def test_bench_step_matches_float64(name):
         main, side = torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            pre = ops.presort_negatives(cfg.num_users, cfg.num_posts, pos, draw)
+            pre = ops.presort_negatives(cfg.num_users, cfg.num_posts, pos, draw, "user")
         pre.rowptr.record_stream(main)
         pre.users.record_stream(main)
         out = model(g.x_dict, e)

@@ -189,6 +189,12 @@ def test_captured_step_layouts(case):
     with pytest.raises(ValueError, match="exceed"):
         step.step(s.sample({"user": torch.arange(n + 1, device=DEV),
                             "post": torch.arange(n, device=DEV)}))
+    # a short batch would feed padded rows to this loss (it reads every seed row): refused
+    # unless the loss reads rows by id (LinkLoss sets partial_seeds)
+    assert not step.blocks.partial_seeds
+    with pytest.raises(ValueError, match="partial_seeds"):
+        step.step(s.sample({"user": torch.arange(n - 1, device=DEV),
+                            "post": torch.arange(n, device=DEV)}))
 
 
 # ----------------------------------------------------------------------------- link batches (cfg5)
@@ -246,6 +252,7 @@ def test_captured_link_step_matches_reference_loss():
     model = make_model()
     ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
     step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, None, slack=16)
+    assert step.blocks.partial_seeds              # LinkLoss reads seed rows by local id
     lb0 = batch(0)
     ll.load(lb0.pu, lb0.pp, lb0.pn)
     step.capture(lb0.mb)

@@ -21,6 +21,7 @@ if os.environ.get("HGNN_LIB"):
 
 HGNN_MEAN = 1
 HGNN_ACCUMULATE = 2
+HGNN_CACHED_LOADS = 4
 MAX_SEG = 6
 
 _c_i32, _c_i64, _c_sz, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p
@@ -69,6 +70,10 @@ _SIGS = {
                                    _c_i32, _p]),
     "hgnn_score_gather2": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _c_i64, _p,
                                     ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
+    "hgnn_score_gather2_ex": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _c_i64, _p,
+                                       ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p,
+                                       _c_i32, _p]),
+    "hgnn_segment_bounds": (_c_i32, [_p, _p, _c_i64, _p, _c_i32, _p, _p]),
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_hop_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_hop_count": (_c_i32, [_c_i32, _p, _p, _p, _p, _c_i32, _p, _p, _p, _c_sz, _p]),

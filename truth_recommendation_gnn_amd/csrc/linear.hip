@@ -702,87 +702,6 @@ __global__ void __launch_bounds__(512, (H <= 64 && K <= 128 ? 4 : (K <= 128 ? 3 
   }
 }
 
-// Forward v5 (persistent, same tiling and W image as v4), reorganised for 2 waves per SIMD (the
-// K = 256 W image takes 135 KB of LDS, so one 8-wave block per CU):
-//  * k-step-major over the NT accumulators: consecutive MFMAs are independent, so no MFMA waits
-//    on the 40-cycle dependent-accumulator latency (v4's 4-deep chains did, with LDS reads issued
-//    just before their use);
-//  * each W fragment of chunk c+1 is read from LDS right after its last use in chunk c, a whole
-//    k-sweep (NT MFMAs) ahead of its first use;
-//  * the next tile's X chunk c is loaded into av[c] as soon as chunk c has been consumed (no second
-//    tile of registers): every chunk still has one tile of MFMAs (~16k cycles at K = 256) to
-//    arrive, and the VGPRs v4 spent on the prefetch copy (64 at K = 256) are free.  Rows past the
-//    end are clamped to the last row (loaded, never stored), so the loads carry no branches.
-template <int H, int K, bool ADD, bool S8 = false>
-__global__ void __launch_bounds__(512, 2) k_linear_fwd_v5(const LinArgs a, const ChunkTab tab,
-                                                          int64_t n_tiles) {
-  constexpr int NT = H / 16, KC = K / 16, LDW = K + 8;
-  __shared__ __attribute__((aligned(16))) float ws[H * LDW];
-  for (int idx = threadIdx.x; idx < H * K / 4; idx += 512) {
-    const int j = idx / (K / 4), k = (idx % (K / 4)) * 4;
-    *reinterpret_cast<float4*>(ws + j * LDW + k) =
-        *reinterpret_cast<const float4*>(a.w + (int64_t)j * K + k);
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const int64_t nw = (int64_t)gridDim.x * 8;
-  const int64_t last = a.n - 1;
-  auto src = [&](int64_t t, int c) { return x_chunk<S8>(tab, min<int64_t>(t * 16 + i, last), c, g); };
-  int64_t t = (int64_t)blockIdx.x * 8 + wave;
-  float4 av[KC];
-  if (t < n_tiles) {
-#pragma unroll
-    for (int c = 0; c < KC; ++c) av[c] = *src(t, c);
-  }
-  __syncthreads();
-  const int wl0 = i * LDW + 4 * g;
-  for (; t < n_tiles; t += nw) {
-    // the last tile of a wave re-loads itself (cached, never used) instead of branching
-    const int64_t tn = t + nw < n_tiles ? t + nw : t;
-    int wo = wl0;
-    asm volatile("" : "+v"(wo));   // W fragments stay per-tile LDS reads (see v4)
-    const float* wl = ws + wo;
-    const int64_t row = t * 16 + i;
-    Epi<NT, ADD> ep;               // the added rows, in flight during the sweep (see v4)
-    ep.load(a, row, H, g);
-    f32x4 acc[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float4 bw[NT];
-#pragma unroll
-    for (int tt = 0; tt < NT; ++tt) bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW);
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].x, av[c].x, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].y, av[c].y, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) acc[tt] = mfma4(bw[tt].z, av[c].z, acc[tt]);
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        acc[tt] = mfma4(bw[tt].w, av[c].w, acc[tt]);
-        if (c + 1 < KC)
-          bw[tt] = *reinterpret_cast<const float4*>(wl + tt * 16 * LDW + (c + 1) * 16);
-      }
-      av[c] = *src(tn, c);
-    }
-    if (row < a.n) {
-      uint32_t mbits = 0;   // ReLU mask bits of this lane's columns (mask_out)
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        float4 v = ep.sum(acc[tt], tt, a, g);
-        if (a.relu) {
-          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        mbits |= relu_bits(v, 4 * tt);
-        *reinterpret_cast<float4*>(a.out + row * H + tt * 16 + 4 * g) = v;
-      }
-      if (a.mask_out) a.mask_out[row * 4 + g] = mbits;
-    }
-  }
-}
-
 // Backward v4: two roles per SIMD.  512 threads; waves 0-3 ("dz waves") load the masked dz
 // fragments of 16 rows each, run dgrad (dX^T = W^T dz^T, straight from registers) and the bias
 // sums, and publish dz to LDS; waves 4-7 ("X waves") stage the X tile and run wgrad.  dz / X
@@ -1112,28 +1031,6 @@ __global__ void __launch_bounds__(512) k_linear_wgrad_v5(const LinArgs a, const 
   }
 }
 
-// T-row tiles need every one of the 512 threads to stage at least one float4 of dz and of X
-template <int H, int K, int T>
-constexpr bool wgrad5_valid() { return T * H / 4 >= 512 && T * K / 4 >= 512; }
-
-template <int H, int K>
-static void launch_wgrad5(int t, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
-                          const LinArgs& a, const ChunkTab& tab, int64_t n_tiles) {
-  if constexpr (wgrad5_valid<H, K, 16>()) {
-    if (t == 16) {
-      hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 16>), grid, block, lds, stream, a, tab, n_tiles);
-      return;
-    }
-  }
-  if constexpr (wgrad5_valid<H, K, 32>()) {
-    if (t == 32) {
-      hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 32>), grid, block, lds, stream, a, tab, n_tiles);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((k_linear_wgrad_v5<H, K, 64>), grid, block, lds, stream, a, tab, n_tiles);
-}
-
 static size_t wgrad5_lds(int h, int k, int t) {
   return std::max<size_t>(((size_t)2 * t * (h + 16) + (size_t)2 * t * (k + 16)) * 4, 512 * 16);
 }
@@ -1227,7 +1124,7 @@ __global__ void __launch_bounds__(512) k_linear_dgrad_v4(const LinArgs a, const 
 
 static size_t dgrad4_lds(int h, int k) { return (size_t)k * (h + 8) * 4; }
 
-// dgrad v5: v4's tiling and W^T image, reorganised like fwd v5 for 2 waves per SIMD: G column
+// dgrad v5: v4's tiling and W^T image, reorganised for 2 waves per SIMD: G column
 // tiles in flight (G independent accumulators, k-step-major), W^T fragments read one k-sweep ahead
 // (across column-group boundaries too), and the next tile's raw dout / out fragments held as
 // loaded — the ReLU mask is applied when the tile becomes current, so no load is waited for at
@@ -1466,28 +1363,19 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, 8),
                                                                       256 * per_cu))),
         block(512);
-    // v5 measured faster only at H = K = 128 (2.87 vs 3.24 ms at N = 9M); v4 elsewhere (K = 256:
-    // 5.12 vs 5.45 ms; H = 64, K = 128: 1.61 vs 1.65 ms at N = 1M).  With the 128-column segment
-    // addressing (S8, round 3) v4 wins at every cfg3/cfg4 shape (N = 9M: K = 128 2.94 vs v5's
-    // 3.01-3.03 ms, + add 3.42-3.45 vs 3.44-3.46, K = 256 5.27-5.32 vs 5.32-5.36); v5 with S8
-    // crosses 128 VGPRs at K = 128 (3.27 ms), so S8 shapes take v4.
-    static const int fwd_env = getenv("HGNN_K3_FWD") ? atoi(getenv("HGNN_K3_FWD")) : 0;
-    static const bool s8_env = !getenv("HGNN_K3_S8") || atoi(getenv("HGNN_K3_S8")) != 0;
-    const bool s8 = s8_env && h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
     // the fp32-exact bf16x6 split at H = 128, K = 128 / 256 (linear_xs.hip), the default
-    // (HGNN_K3_X6=0: the f32-input MFMA kernels below)
+    // (hgnn_set_k3_split(0) / HGNN_K3_X6=0: the f32-input MFMA kernel below, the one fallback)
     if (x6_enabled() && h == 128 && (a.k_total == 128 || a.k_total == 256))
       return xs_linear_fwd(a, tab, stream);
-    const int fwd_ver = fwd_env ? fwd_env : (!s8 && h == 128 && a.k_total == 128 ? 5 : 4);
-#define HGNN_FWD4S(HV, KV, AV, SV)                                                               \
-  if (fwd_ver == 4)                                                                              \
-    hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV, SV>), grid, block, 0, stream, a, tab,        \
-                       n_tiles);                                                                 \
-  else                                                                                           \
-    hipLaunchKernelGGL((k_linear_fwd_v5<HV, KV, AV, SV>), grid, block, 0, stream, a, tab,        \
-                       n_tiles);
-#define HGNN_FWD4A(HV, KV, AV) \
-  if (s8) { HGNN_FWD4S(HV, KV, AV, true) } else { HGNN_FWD4S(HV, KV, AV, false) }
+    // 128-column segment addressing where every 8 chunks are one segment (round 3: -2.5 % at
+    // K = 128, -1 % at K = 256 on the cfg4 shapes; the v5 schedule measured slower with it and
+    // is no longer built)
+    const bool s8 = h == 128 && a.k_total >= 128 && chunks_in_segments_of_8(tab, a.k_total);
+#define HGNN_FWD4A(HV, KV, AV)                                                                    \
+  if (s8) hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV, (HV == 128 && KV >= 128)>), grid, block, \
+                             0, stream, a, tab, n_tiles);                                        \
+  else hipLaunchKernelGGL((k_linear_fwd_v4<HV, KV, AV, false>), grid, block, 0, stream, a, tab,  \
+                          n_tiles);
 #define HGNN_FWD4(HV, KV) \
   if (add) { HGNN_FWD4A(HV, KV, true) } else { HGNN_FWD4A(HV, KV, false) }
     switch (h * 1000 + a.k_total) {
@@ -1500,7 +1388,6 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     }
 #undef HGNN_FWD4
 #undef HGNN_FWD4A
-#undef HGNN_FWD4S
     return check_launch("k_linear_fwd_v4");
   }
   // v2 (W in LDS, A prefetched): 279 vs 321 us at N=1M, K=128, h=64 — the default when it fits
@@ -1631,9 +1518,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     const int K = a.k_total;
     // H = K = 128: persistent dgrad v5 + wgrad v5 (T = 16) beat the fused two-role kernel
     // (6.21 vs 8.29 ms at N = 9M); H = 64, K = 128: the fused kernel wins (3.18 vs 3.94 ms)
-    static const int split_env =
-        getenv("HGNN_K3_BWD_SPLIT") ? atoi(getenv("HGNN_K3_BWD_SPLIT")) : -1;
-    const bool split = split_env >= 0 ? split_env != 0 : (h == 128 && K == 128);
+    const bool split = h == 128 && K == 128;
     const bool fused = !split && any_dx && (dw || db) && K <= 128 &&
                        v4_bwd_lds(h, K, true) <= 160 * 1024;
     if (x6_enabled() && h == 128 && (K == 128 || K == 256)) {
@@ -1661,14 +1546,12 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
           block(512);
       const size_t lds = dgrad4_lds(h, K);
       {
-      // v5 at H = 128 (K = 256: 5.06 vs 5.70 ms; K = 128: 3.22 vs 3.25 ms at N = 9M)
-      static const int dg_env = getenv("HGNN_K3_DGRAD") ? atoi(getenv("HGNN_K3_DGRAD")) : 0;
-      const int dg_ver = dg_env ? dg_env : (h == 128 ? 5 : 4);
+      // v5 at H = 128 (K = 256: 5.06 vs 5.70 ms; K = 128: 3.22 vs 3.25 ms at N = 9M), v4 at H = 64
 #define HGNN_DG4(HV, KV)                                                                        \
-  if (dg_ver == 4)                                                                              \
-    hipLaunchKernelGGL((k_linear_dgrad_v4<HV, KV>), grid, block, lds, stream, a, tab, n16);     \
+  if constexpr (HV == 128)                                                                      \
+    hipLaunchKernelGGL((k_linear_dgrad_v5<HV, KV>), grid, block, lds, stream, a, tab, n16);     \
   else                                                                                          \
-    hipLaunchKernelGGL((k_linear_dgrad_v5<HV, KV>), grid, block, lds, stream, a, tab, n16);
+    hipLaunchKernelGGL((k_linear_dgrad_v4<HV, KV>), grid, block, lds, stream, a, tab, n16);
       switch (h * 1000 + K) {
         case 64064: HGNN_DG4(64, 64); break;
         case 64128: HGNN_DG4(64, 128); break;
@@ -1692,12 +1575,8 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     // wgrad v5 (every wave on MFMAs), 16-row tiles: H = K = 128 2.86 vs 4.73 ms (v4) at N = 9M;
     // v4 kept elsewhere (K = 256: v5 6.44 / 9.51 ms at T = 16 / 32 vs 5.65; H = 64 needs T >= 32,
     // which measured slower than v4: 2.44 vs 1.94 ms)
-    static const int wg_env = getenv("HGNN_K3_WGRAD") ? atoi(getenv("HGNN_K3_WGRAD")) : 0;
-    const int wg_ver = wg_env ? wg_env : (h == 128 && K == 128 ? 5 : 4);
-    static const int wg_t = getenv("HGNN_K3_WGRAD_T") ? atoi(getenv("HGNN_K3_WGRAD_T")) : 16;
-    if (!fused && wg_ver == 5 && (h == 64 || h == 128) && (wg_t == 16 || wg_t == 32 || wg_t == 64) &&
-        (int64_t)wg_t * K / 4 >= 512 && (int64_t)wg_t * h / 4 >= 512 &&
-        wgrad5_lds(h, K, wg_t) <= 160 * 1024) {
+    constexpr int wg_t = 16;
+    if (!fused && h == 128 && K == 128) {
       const int64_t n_tiles = cdiv(n_rows, wg_t);
       const size_t lds = wgrad5_lds(h, K, wg_t);
       const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
@@ -1706,14 +1585,8 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       if (ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
       a.slab = static_cast<float*>(ws);
       const dim3 grid(G), block(512);
-      switch (h * 1000 + K) {
-        case 64064: launch_wgrad5<64, 64>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-        case 64128: launch_wgrad5<64, 128>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-        case 64256: launch_wgrad5<64, 256>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-        case 128064: launch_wgrad5<128, 64>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-        case 128128: launch_wgrad5<128, 128>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-        default: launch_wgrad5<128, 256>(wg_t, grid, block, lds, stream, a, tab, n_tiles); break;
-      }
+      hipLaunchKernelGGL((k_linear_wgrad_v5<128, 128, wg_t>), grid, block, lds, stream, a, tab,
+                         n_tiles);
       if (int rc = check_launch("k_linear_wgrad_v5")) return rc;
       const int64_t total = (int64_t)h * (K + 1);
       hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,

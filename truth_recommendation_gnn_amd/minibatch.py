@@ -66,11 +66,18 @@ def capacities(relations, n_seeds: Mapping[str, int], fanouts, slack: int = SLAC
 
 
 class StaticBlocks:
-    """Fixed-capacity buffers for the blocks of one sampler configuration (see module doc)."""
+    """Fixed-capacity buffers for the blocks of one sampler configuration (see module doc).
 
-    def __init__(self, smp: NeighborSampler, n_seeds: Mapping[str, int], slack: int = SLACK):
+    ``partial_seeds``: a batch may hold FEWER seeds than ``n_seeds`` (the rest are padded level-0
+    rows).  Only a loss that reads the seed rows by their local ids may allow it (``LinkLoss``:
+    a link batch's distinct endpoints vary in number); a loss over all seed rows would be fed
+    the padding, so by default a batch must have exactly ``n_seeds`` seeds per type."""
+
+    def __init__(self, smp: NeighborSampler, n_seeds: Mapping[str, int], slack: int = SLACK,
+                 partial_seeds: bool = False):
         self.smp = smp
         self.n_seeds = {t: int(n) for t, n in n_seeds.items()}
+        self.partial_seeds = bool(partial_seeds)
         if slack < 1:
             raise ValueError("slack: at least one padded row per level")
         self.slack = int(slack)
@@ -96,9 +103,12 @@ class StaticBlocks:
         seeds = mb.nodes[-1]
         got = {t: int(v.numel()) for t, v in seeds.items()}
         if set(got) != set(self.n_seeds) or any(got[t] > self.n_seeds[t] for t in got):
-            # fewer seeds than the capacity leave padded level-0 rows (a link batch's unique
-            # endpoints vary in number; its loss reads the seed rows by their local ids)
             raise ValueError(f"batch seeds {got} exceed the captured capacity {self.n_seeds}")
+        if not self.partial_seeds and got != self.n_seeds:
+            # fewer seeds than the capacity leave padded level-0 rows, which a loss over all
+            # the seed rows would read: allowed only with partial_seeds (see the class doc)
+            raise ValueError(f"batch seeds {got} differ from the captured {self.n_seeds} "
+                             "(partial_seeds=False)")
         L = self.L
         rp, col, mp, nd, e, rpo, colo, dcap, ecap, dummy, spread = ([] for _ in range(11))
         for h in range(L):
@@ -208,16 +218,22 @@ class CapturedStep:
     ``between`` (data-parallel ranks): an eager call between the backward and the optimizer step
     — ``parallel.sync_grads``'s all-reduce of the gradients — so the step is two replays, the
     forward + loss + backward graph and the optimizer graph, around it.  A ``loss_fn`` with a
-    ``make_csr()`` method (``LinkLoss``) gets fresh structures before each recorded pass."""
+    ``make_csr()`` method (``LinkLoss``) gets fresh structures before each recorded pass.
+
+    ``partial_seeds`` (``StaticBlocks``): None takes the loss's own ``partial_seeds`` attribute
+    (``LinkLoss`` sets it: it reads seed rows by local id), else False."""
 
     def __init__(self, model: HeteroSAGE, x_dict: Mapping[str, torch.Tensor],
                  smp: NeighborSampler, n_seeds: Mapping[str, int],
                  loss_fn: Callable[[Dict[str, torch.Tensor]], torch.Tensor],
                  optimizer: Optional[torch.optim.Optimizer] = None, slack: int = SLACK,
-                 between: Optional[Callable[[], None]] = None):
+                 between: Optional[Callable[[], None]] = None,
+                 partial_seeds: Optional[bool] = None):
         self.model, self.x_dict, self.loss_fn, self.opt = model, x_dict, loss_fn, optimizer
         self.between = between
-        self.blocks = StaticBlocks(smp, n_seeds, slack)
+        if partial_seeds is None:
+            partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
+        self.blocks = StaticBlocks(smp, n_seeds, slack, partial_seeds=partial_seeds)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
@@ -319,7 +335,10 @@ class LinkLoss:
     negatives; no sync) groups the pairs by user into them, ``make_csr()`` makes fresh
     structures over them (their post grouping is built on first use: inside a capture, per
     replay).  ``n_total`` = the positives of ALL ranks, so per-rank losses add up to the global
-    batch's mean (data-parallel gradients are summed)."""
+    batch's mean (data-parallel gradients are summed).  It reads the seed rows by local id, so
+    a batch with fewer distinct endpoints than the capacity is fine (``partial_seeds``)."""
+
+    partial_seeds = True
 
     def __init__(self, n_edges: int, n_users: int, n_posts: int, device, n_total: int = 0):
         i32 = dict(dtype=torch.int32, device=device)

@@ -232,6 +232,55 @@ def _score_gather2(U, P, pos, negs, cscale, inv_e, out):
 
 _SCORE2 = os.environ.get("HGNN_SCORE2", "1") == "1"   # 0: the two separate dP gathers (A/B)
 
+# The dP gather over the user table in source-block passes, as K1: pass b sums
+# the positives and negatives whose user lies in block b, accumulating into dP; every pass
+# re-reads its rows' P vectors and dP.  HGNN_DP_BLOCKS: 1 one pass, N passes, "auto" the K1
+# rule (ops.gather_blocks); HGNN_DP_CACHED=1: default-policy user-row loads in the passes.
+DP_BLOCKS = os.environ.get("HGNN_DP_BLOCKS", "1")
+DP_CACHED = os.environ.get("HGNN_DP_CACHED", "1") == "1"
+
+
+def dp_blocks(U: torch.Tensor, n_edges: int) -> int:
+    if DP_BLOCKS == "auto":
+        return gather_blocks(U, n_edges)
+    return max(1, int(DP_BLOCKS))
+
+
+def _score_gather2_blocked(U, P, csr: RelationCSR, rowptr_n, nu_s, cscale, inv_e, out, B: int,
+                           cached: bool = True):
+    """``_score_gather2`` as ``B`` source-block passes over the user table: the positives from
+    ``csr.blocks("fwd", B)`` (the K1 passes of the same relation: built once, shared), the
+    negatives as each post's sub-segment per block (their users ascend within a post: the
+    stable sort of user-grouped positions), found by one ``hgnn_segment_bounds`` launch.  Sums
+    per row in block order (fp32 reassociation against the one pass, like the blocked K1)."""
+    dev = out.device
+    d = int(out.shape[1])
+    n = csr.n_dst
+    nu = int(U.shape[0])
+    passes, _ = csr.blocks("fwd", B)
+    bs = -(-nu // B)
+    lib, s = N.lib(), N.stream_ptr(dev)
+    E = csr.num_edges + int(nu_s.numel())
+    nb = gather_bytes(E, n, d, False) + 4 * (n + 1) + 4 * n * d
+    cb = gather_compulsory_bytes(E, n, nu, d, False) + 4 * (n + 1) + 4 * n * d
+    thr = torch.tensor([b * bs for b in range(1, B)], dtype=torch.int32, device=dev)
+    bounds = torch.empty(max((B - 1) * n, 1), dtype=torch.int32, device=dev)
+    with _timed(f"score_gather[{n}<-{nu}]x{d}", nb, cb):
+        N.check(lib.hgnn_segment_bounds(N.ptr(rowptr_n), N.ptr(nu_s), n, N.ptr(thr), B - 1,
+                                        N.ptr(bounds), s), "hgnn_segment_bounds")
+        for b, g in enumerate(passes):
+            p = g.plan
+            slab = (torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
+                    if p.n_heavy else None)
+            beg = rowptr_n if b == 0 else bounds[(b - 1) * n:b * n]
+            end = bounds[b * n:(b + 1) * n] if b < B - 1 else rowptr_n[1:]
+            flags = (N.HGNN_ACCUMULATE if b > 0 else 0) | (N.HGNN_CACHED_LOADS if cached else 0)
+            N.check(lib.hgnn_score_gather2_ex(
+                N.ptr(U), nu, N.ptr(P), d, N.ptr(g.rowptr), N.ptr(g.col), N.ptr(beg), N.ptr(end),
+                N.ptr(nu_s), n, N.ptr(cscale), inv_e, N.ptr(p.heavy_rows), N.ptr(p.heavy_first),
+                p.n_heavy, p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out), flags, s),
+                "hgnn_score_gather2_ex")
+
 
 def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -910,10 +959,26 @@ def _sort_negatives(csr, neg_u_order, draw, neg, neg32: bool, uop, E: int, np_: 
 
 class PresortedNegatives:
     """The loss's negatives already grouped by post (``presort_negatives``): the sharded step
-    sorts them under a collective, ahead of the loss that consumes them."""
+    sorts them under a collective, ahead of the loss that consumes them.  It holds the grouping
+    and the draws it was made from (the objects themselves, compared with ``is``: an id could be
+    reused by a new object once the old one is freed), so a loss over other edges or other
+    draws is refused."""
 
-    def __init__(self, key, rowptr, users):
-        self.key, self.rowptr, self.users = key, rowptr, users
+    def __init__(self, csr, neg_p, neg_order: str, n_posts: int, rowptr, users):
+        self.csr, self.neg_p, self.neg_order = csr, neg_p, neg_order
+        self.n_posts = int(n_posts)
+        self.rowptr, self.users = rowptr, users
+
+    def check_draws(self, neg_p, neg_order: str, where: str) -> None:
+        if neg_order != self.neg_order:
+            raise ValueError(f"{where}: presorted negatives were grouped with neg_order="
+                             f"{self.neg_order!r}, the loss got neg_order={neg_order!r}")
+        if neg_p is not self.neg_p:
+            raise ValueError(f"{where}: presorted negatives of other draws")
+
+    def check_edges(self, csr, n_posts: int) -> None:
+        if csr is not self.csr or int(n_posts) != self.n_posts:
+            raise ValueError("edge_bce_loss: the presorted negatives are for other edges")
 
 
 def _neg_inputs(neg_u_order):
@@ -927,9 +992,11 @@ def _neg_inputs(neg_u_order):
 
 
 def presort_negatives(n_users: int, n_posts: int, pos_edges: torch.Tensor, neg_p,
-                      neg_order: str = "user") -> PresortedNegatives:
+                      neg_order: str) -> PresortedNegatives:
     """The grouping ``edge_bce_loss_raw`` would sort its negatives into, done now (it needs
-    only the edges and the draws, not the embeddings); pass it back as ``presorted=``."""
+    only the edges and the draws, not the embeddings); pass it back as ``presorted=`` with the
+    same ``neg_p`` and ``neg_order`` (required here: the two loss entry points default to
+    different orders)."""
     csr = relation_csr_for_loss(pos_edges, n_users, n_posts)
     neg_u = _negatives_user_order(csr, neg_p, neg_order)
     draw, neg32, neg = _neg_inputs(neg_u)
@@ -938,7 +1005,7 @@ def presort_negatives(n_users: int, n_posts: int, pos_edges: torch.Tensor, neg_p
     E = csr.num_edges
     rp, us = _sort_negatives(csr, neg_u, draw, neg, neg32, _user_of_pos(csr), E, n_posts, err,
                              dev)
-    return PresortedNegatives((id(csr), E, n_posts, id(neg_p), neg_order), rp, us)
+    return PresortedNegatives(csr, neg_p, neg_order, n_posts, rp, us)
 
 
 def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total: int,
@@ -988,8 +1055,7 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     lanes = _Lanes(dev, 2)
     with lanes.ctx(1):
         if presorted is not None:
-            if presorted.key[:3] != (id(csr), E, np_):
-                raise ValueError("edge_bce_loss: the presorted negatives are for other edges")
+            presorted.check_edges(csr, np_)
             rowptr_n, nu_s = presorted.rowptr, presorted.users
         else:
             rowptr_n, nu_s = _sort_negatives(csr, neg_u_order, draw, neg, neg32, uop, E, np_,
@@ -1011,6 +1077,9 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
                     ng = GroupedEdges(rowptr_n[lo:hi + 1], nu_s, None,
                                       Plan(NO_SPLIT, 0, 0, None, None), hi - lo)
                     _score_gather2(U, P[lo:hi], _row_range(pf, lo, hi), ng, c, inv_e, dP[lo:hi])
+        elif _SCORE2 and dp_blocks(U, E) > 1:
+            _score_gather2_blocked(U, P, csr, rowptr_n, nu_s, c, inv_e, dP, dp_blocks(U, E),
+                                   DP_CACHED)
         elif _SCORE2:
             _score_gather2(U, P, pf, negs, c, inv_e, dP)
         else:
@@ -1105,8 +1174,8 @@ def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: tor
     if cscale is None:
         cscale = pos_weights.to(torch.float32).mean()
     n_total = csr.num_edges if n_edges_total is None else int(n_edges_total)
-    if presorted is not None and presorted.key[3:] != (id(neg_p), neg_order):
-        raise ValueError("edge_bce_loss: presorted negatives of other draws")
+    if presorted is not None:
+        presorted.check_draws(neg_p, neg_order, "edge_bce_loss")
     return _EdgeBCELoss.apply(user_emb, post_emb, csr, neg_u, cscale, check, n_total, ready,
                               presorted)
 
@@ -1121,8 +1190,8 @@ def edge_bce_loss_raw(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges:
     edges and draws)."""
     csr = relation_csr_for_loss(pos_edges, user_emb.shape[0], post_emb.shape[0])
     neg_u = _negatives_user_order(csr, neg_p, neg_order)
-    if presorted is not None and presorted.key[3:] != (id(neg_p), neg_order):
-        raise ValueError("edge_bce_loss_raw: presorted negatives of other draws")
+    if presorted is not None:
+        presorted.check_draws(neg_p, neg_order, "edge_bce_loss_raw")
     return _edge_bce(user_emb, post_emb, csr, neg_u, cscale, False, int(n_edges_total), ready,
                      on_dP, p_chunks, presorted)
 
