@@ -96,6 +96,9 @@ def parse(argv=None):
                    help="cfg5 mini-batch: the link loss as torch ops instead of the fused kernels")
     p.add_argument("--no-graph", action="store_true",
                    help="cfg5 mini-batch: run the step eagerly instead of replaying its HIP graph")
+    p.add_argument("--eager-allreduce", action="store_true",
+                   help="cfg5 mini-batch over RCCL: the gradient all-reduce eagerly between two "
+                        "graph replays instead of recorded inside the one graph")
     p.add_argument("--no-prefetch", action="store_true",
                    help="cfg5 mini-batch: no side-stream sampling of the next batch")
     p.add_argument("--prefetch", action="store_true",
@@ -909,14 +912,22 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
     loss_of.partial_seeds = True                 # both forms read the seed rows by local id
 
+    # over RCCL the gradient all-reduce is recorded inside the step's graph (one replay per
+    # step; with --dist at world 1 it is still issued, as a rehearsal of the captured
+    # collective); gloo's collectives run on the host, so there it stays an eager call between
+    # two replays
+    capture_ar = (sharded and use_graph and args.dist_backend == "nccl" and dev.type == "cuda"
+                  and not args.eager_allreduce)
+
     def sync():
-        parallel.sync_grads(model, env)          # no-op at world size 1
+        parallel.sync_grads(model, env, force=capture_ar)   # no-op at world size 1 otherwise
 
     captured = None
     if use_graph:
         # the capture's two warm-up passes are training steps on batch 0 (then recorded once)
         captured = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_of, opt,
-                                          between=sync if world > 1 else None)
+                                          between=sync if (world > 1 or capture_ar) else None,
+                                          capture_between=capture_ar)
         lb0 = sample(0)[0]
         link_loss.load(lb0.pu, lb0.pp, lb0.pn)
         captured.capture(lb0.mb, warmup=2)
@@ -993,11 +1004,16 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    "edges_per_step": round(edges / args.steps),
                    "global_batch": nb * world,
                    "batches_per_s": round(world * args.steps / elapsed, 1),
+                   "graph_replays_per_step": (None if captured is None else
+                                              1 if captured.graph_opt is None else 2),
                    "parallelism": f"data-parallel x{world}" if world > 1 else "single",
-                   "execution": (("one HIP graph replay per step over static-capacity blocks "
-                                  if world == 1 else "HIP graph replays per step (forward + loss "
-                                  "+ backward; eager gradient all-reduce; Adam) over "
-                                  "static-capacity blocks ") + "(sampler eager)"
+                   "execution": ((("one HIP graph replay per step (forward + loss + backward + "
+                                   "RCCL gradient all-reduce + Adam) over static-capacity blocks "
+                                   if capture_ar else
+                                   "one HIP graph replay per step over static-capacity blocks "
+                                   if world == 1 else "HIP graph replays per step (forward + loss "
+                                   "+ backward; eager gradient all-reduce; Adam) over "
+                                   "static-capacity blocks ") + "(sampler eager)")
                                  if captured is not None else "eager")
                    + (", next batch sampled on a side stream" if side is not None else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),

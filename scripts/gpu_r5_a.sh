@@ -6,7 +6,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_parity.py -k "segment_bounds or source_blocks or presorted or linear or k3 or split or dp_gather" \
+  tests/test_gpu_parity.py -k "segment_bounds or source_blocks or presorted or dp_gather" \
   > gpurun_out/r5a_tests.log 2>&1 || { tail -30 gpurun_out/r5a_tests.log; exit 1; }
 tail -3 gpurun_out/r5a_tests.log
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \

@@ -185,6 +185,8 @@ def main():
         t1 = r["recv_bytes"] / (XGMI_LINK_GBS * 1e9) * 1e3
         t7 = t1 / XGMI_LINKS
         colls.append({"op": r["op"], "recv_MB_per_rank": round(r["recv_bytes"] / 1e6, 1),
+                      "issue_ms": round(env.t0.elapsed_time(r["issue"]), 3),
+                      "wait_ms": round(env.t0.elapsed_time(r["wait"]), 3) if "wait" in r else None,
                       "cover_ms": None if cover is None else round(cover, 3),
                       "est_ms_1link_ring": round(t1, 3), "est_ms_7links": round(t7, 3),
                       "cover_over_1link": None if cover is None else round(cover / t1, 2) if t1 else None,
@@ -192,6 +194,7 @@ def main():
     env.log = None
     print(json.dumps({"world": args.world, "rank": args.rank, "config": gcfg.name,
                       "chunked_last_gather": parallel.CHUNKED_LAST_GATHER,
+                      "chunk_group": parallel.CHUNK_GROUP, "chunk_first": parallel.CHUNK_FIRST,
                       "collectives": colls,
                       "link_timeline": timeline,
                       "scaling": "strong" if args.strong else "weak",

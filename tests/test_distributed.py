@@ -105,6 +105,16 @@ def test_sharded_step_with_other_partial_sum_splits(world, kind, split, monkeypa
     _run_and_check(world, kind, False)
 
 
+@pytest.mark.parametrize("mode,group", [("1", "2"), ("2", "2"), ("3", "3"), ("0", "2")])
+def test_sharded_step_with_other_last_gather_chunkings(mode, group, monkeypatch):
+    """The loss's post table as one all-gather (0), one dP launch per broadcast block (1), own /
+    below / above (2, round 3-4), or landing-order groups of 3 blocks (the default mode 3 takes
+    groups of 2): the same oracle step at world 4 (blocks split around the own one)."""
+    monkeypatch.setenv("HGNN_CHUNKED_GATHER", mode)      # read at import by the spawned ranks
+    monkeypatch.setenv("HGNN_CHUNK_GROUP", group)
+    _run_and_check(4, "engage2", True)
+
+
 def _run_and_check(world, kind, slice_inputs):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -795,9 +795,10 @@ def test_segment_bounds_matches_searchsorted():
     col = np.concatenate([np.sort(rng.integers(0, n_col, k)) for k in deg]).astype(np.int32)
     thr = np.array([1, 700, 2500, 2501, 4999, 5000, 9000], dtype=np.int32)
     out = torch.full((len(thr) * n_rows,), -1, dtype=torch.int32, device=DEV)
-    Nn.check(Nn.lib().hgnn_segment_bounds(
-        Nn.ptr(torch.from_numpy(rowptr).to(DEV)), Nn.ptr(torch.from_numpy(col).to(DEV)), n_rows,
-        Nn.ptr(torch.from_numpy(thr).to(DEV)), len(thr), Nn.ptr(out), Nn.stream_ptr(DEV)), "b")
+    d_rp, d_col, d_thr = (torch.from_numpy(v).to(DEV) for v in (rowptr, col, thr))
+    Nn.check(Nn.lib().hgnn_segment_bounds(Nn.ptr(d_rp), Nn.ptr(d_col), n_rows, Nn.ptr(d_thr),
+                                          len(thr), Nn.ptr(out), Nn.stream_ptr(torch.device(DEV))),
+             "hgnn_segment_bounds")
     want = np.array([[rowptr[r] + np.searchsorted(col[rowptr[r]:rowptr[r + 1]], t)
                       for r in range(n_rows)] for t in thr]).reshape(-1)
     assert np.array_equal(out.cpu().numpy(), want)

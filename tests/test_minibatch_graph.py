@@ -305,3 +305,59 @@ def test_captured_link_step_with_gradient_hook_trains_like_eager():
     for (n, p), (_, r) in zip(model.named_parameters(), ref.named_parameters()):
         _close(p.detach(), r.detach(), n)
     assert all(np.isfinite(losses))
+
+
+def test_captured_link_step_with_rccl_allreduce_in_the_graph():
+    """over RCCL the data-parallel step is ONE replay — forward + loss + backward,
+    parallel.sync_grads' flat all-reduce (issued at world 1 too: force=True) and the Adam step
+    recorded in one HIP graph — and it trains like the eager steps (an all-reduce over one rank
+    is the identity; the hook's scaling inside the graph shows the recorded call runs)."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from truth_recommendation_gnn_amd import minibatch, parallel, sampler
+    if dist.is_initialized():
+        pytest.skip("a process group is already up in this process")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        env = parallel.DistEnv.from_torch()
+        g, s, batch, make_model, _, _, n_seeds = _link_setup()
+        B = n_seeds["user"]
+        model, ref = make_model(), make_model()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=True)
+        ref_opt = torch.optim.Adam(ref.parameters(), lr=1e-3, fused=True)
+
+        def hook(m):
+            for p in m.parameters():
+                if p.grad is not None:
+                    p.grad.mul_(0.5)
+
+        def between():
+            parallel.sync_grads(model, env, force=True)
+            hook(model)
+        ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
+        step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, opt, slack=16,
+                                      between=between, capture_between=True)
+        lb0 = batch(0)
+        ll.load(lb0.pu, lb0.pp, lb0.pn)
+        step.capture(lb0.mb, warmup=2)
+        assert step.graph_opt is None               # one graph: the collective is inside it
+        losses = []
+        for lb in [lb0, lb0] + [batch(b) for b in (1, 2, 3)]:
+            if lb is not lb0:
+                ll.load(lb.pu, lb.pp, lb.pn)
+                losses.append(float(step.step(lb.mb)))
+            ref_opt.zero_grad(set_to_none=True)
+            _ref_link_loss(sampler.forward_blocks(ref, lb.mb, g.x_dict), lb).backward()
+            hook(ref)
+            ref_opt.step()
+        torch.cuda.synchronize()
+        for (n, p), (_, r) in zip(model.named_parameters(), ref.named_parameters()):
+            _close(p.detach(), r.detach(), n)
+        assert all(np.isfinite(losses))
+    finally:
+        dist.destroy_process_group()

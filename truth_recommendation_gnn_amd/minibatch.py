@@ -215,10 +215,13 @@ class CapturedStep:
     (``torch.optim.Adam(..., capturable=True)``); gradients live in the graph's memory pool and
     are rewritten by every replay (zeroed once before capture).
 
-    ``between`` (data-parallel ranks): an eager call between the backward and the optimizer step
-    — ``parallel.sync_grads``'s all-reduce of the gradients — so the step is two replays, the
-    forward + loss + backward graph and the optimizer graph, around it.  A ``loss_fn`` with a
-    ``make_csr()`` method (``LinkLoss``) gets fresh structures before each recorded pass.
+    ``between`` (data-parallel ranks): a call between the backward and the optimizer step —
+    ``parallel.sync_grads``'s all-reduce of the gradients.  With ``capture_between`` (RCCL: its
+    collectives are graph-capturable) it is recorded INSIDE the one graph, so a step is one
+    replay; otherwise (gloo, whose collectives run on the host) it runs eagerly and the step is
+    two replays, the forward + loss + backward graph and the optimizer graph, around it.  A
+    ``loss_fn`` with a ``make_csr()`` method (``LinkLoss``) gets fresh structures before each
+    recorded pass.
 
     ``partial_seeds`` (``StaticBlocks``): None takes the loss's own ``partial_seeds`` attribute
     (``LinkLoss`` sets it: it reads seed rows by local id), else False."""
@@ -228,9 +231,10 @@ class CapturedStep:
                  loss_fn: Callable[[Dict[str, torch.Tensor]], torch.Tensor],
                  optimizer: Optional[torch.optim.Optimizer] = None, slack: int = SLACK,
                  between: Optional[Callable[[], None]] = None,
-                 partial_seeds: Optional[bool] = None):
+                 partial_seeds: Optional[bool] = None, capture_between: bool = False):
         self.model, self.x_dict, self.loss_fn, self.opt = model, x_dict, loss_fn, optimizer
         self.between = between
+        self.capture_between = bool(capture_between) and between is not None
         if partial_seeds is None:
             partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
         self.blocks = StaticBlocks(smp, n_seeds, slack, partial_seeds=partial_seeds)
@@ -249,6 +253,8 @@ class CapturedStep:
         out = self.blocks.forward(self.model, self.x_dict)
         loss = self.loss_fn(out)
         loss.backward()
+        if self.capture_between:
+            self.between()
         if self.opt is not None and with_opt:
             self.opt.step()
         return out, loss
@@ -258,7 +264,7 @@ class CapturedStep:
         these are training steps), then record the step."""
         dev = self.blocks.smp.device
         self.blocks.load(first)
-        split = self.between is not None and self.opt is not None
+        split = self.between is not None and self.opt is not None and not self.capture_between
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):

@@ -185,8 +185,16 @@ class _AllOf:
 # The last forward gather of the post table (the loss's input) as per-source broadcasts whose
 # row blocks the loss's dP gather consumes as they land (DistEnv.broadcast_slices_async):
 # HGNN_CHUNKED_GATHER=1 one dP launch per block, 2 three launches (own block, the blocks below,
-# the blocks above), 0 one all-gather and one dP launch.
-CHUNKED_LAST_GATHER = int(os.environ.get("HGNN_CHUNKED_GATHER", "2"))
+# the blocks above), 3 the own block and then the others in landing order in groups of
+# HGNN_CHUNK_GROUP (2) blocks, 0 one all-gather and one dP launch.  The broadcasts land one by one
+# (one link: ~0.42 ms per 64 MB block at N = 8) and the dP gather of a block takes ~0.49 ms, so
+# groups of two keep the gather just behind the link where mode 2's "blocks above" waited for all
+# seven (rank 0: 2.3 ms stalled on the one-link replay, round 4).
+CHUNKED_LAST_GATHER = int(os.environ.get("HGNN_CHUNKED_GATHER", "3"))
+CHUNK_GROUP = int(os.environ.get("HGNN_CHUNK_GROUP", "2"))
+# the first group's size: the own block's dP gather (~0.66 ms at N = 8) covers one landed block,
+# not two (HGNN_CHUNK_FIRST)
+CHUNK_FIRST = int(os.environ.get("HGNN_CHUNK_FIRST", "1"))
 
 # user->post partial sums at world > 1 in this many row ranges of every slice (1 = one
 # reduce-scatter of the whole padded table, round 3).  With 2, the first range's reduce-scatter
@@ -1062,6 +1070,25 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     order = [r] + [q for q in range(W) if q != r]   # own, then as they land
                     st["p_chunks"] = [(q * S, (q + 1) * S, None if q == r else works[q].wait)
                                       for q in order]
+                elif CHUNKED_LAST_GATHER == 3:    # own block, then groups in landing order
+                    others = [q for q in range(W) if q != r]
+                    first = max(1, CHUNK_FIRST)
+                    groups = [others[:first]] + [
+                        others[i:i + max(1, CHUNK_GROUP)]
+                        for i in range(first, len(others), max(1, CHUNK_GROUP))]
+                    groups = [grp for grp in groups if grp]
+                    st["p_chunks"] = [(r * S, (r + 1) * S, None)]
+                    for grp in groups:
+                        # a group of blocks contiguous in rows (the own block splits at most one)
+                        runs = []
+                        for q in grp:
+                            if runs and runs[-1][1] == q * S:
+                                runs[-1][1] = (q + 1) * S
+                            else:
+                                runs.append([q * S, (q + 1) * S])
+                        wait = (lambda qs: (lambda: [works[q].wait() for q in qs]))(grp)
+                        for k, (lo, hi) in enumerate(runs):
+                            st["p_chunks"].append((lo, hi, wait if k == 0 else None))
                 else:                             # own block, blocks below it, blocks above it
                     # each range waits on every broadcast it reads (stream waits, free): no
                     # reliance on the backend finishing them in issue order
@@ -1259,17 +1286,22 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
     return loss
 
 
-def sync_grads(model: torch.nn.Module, env: DistEnv) -> None:
+def sync_grads(model: torch.nn.Module, env: DistEnv, force: bool = False) -> None:
     """Sum parameter gradients over ranks with one flat all-reduce.  Every rank contributes every
     trainable parameter (zeros where its backward produced no gradient — a rank whose shard holds
     no edge of some relation), so the flat buffers line up across ranks.  One concatenation in,
-    one multi-tensor copy out (not a copy kernel per parameter)."""
-    if env.world == 1:
+    one multi-tensor copy out (not a copy kernel per parameter).  No host sync: the whole
+    function can be recorded in a HIP graph over RCCL (``minibatch.CapturedStep``).  ``force``:
+    issue the all-reduce at world size 1 too (rehearsal of the captured collective on one GPU)."""
+    if env.world == 1 and not force:
         return
     params = [p for p in model.parameters() if p.requires_grad]
     flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
                       for p in params])
-    env.all_reduce_(flat)
+    if env.world > 1:
+        env.all_reduce_(flat)
+    elif force:
+        dist.all_reduce(flat, group=env.group)
     views = [v.view_as(p) for v, p in zip(torch.split(flat, [p.numel() for p in params]), params)]
     have = [i for i, p in enumerate(params) if p.grad is not None]
     if have:
