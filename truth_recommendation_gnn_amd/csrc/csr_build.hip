@@ -160,6 +160,13 @@ constexpr int kSortThreads = HGNN_SORT_THREADS;
 constexpr int kSortRounds = HGNN_SORT_ROUNDS;             // one item per thread per round
 constexpr int kSortTile = kSortThreads * kSortRounds;     // 8192 items per block
 constexpr int kMaxRadix = 1024;
+// HGNN_SORT_LEADER: in the scatter's ranking only the first lane of each digit group reads the
+// wave's running count (the others get it by ds_bpermute from that lane: no bank conflicts) —
+// 64 random LDS reads per round become ~40.  The reorder's two lookups per item (the run's global
+// start and its tile-local start) are one table of their difference.
+#ifndef HGNN_SORT_LEADER
+#define HGNN_SORT_LEADER 1
+#endif
 
 // key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
 __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
@@ -243,6 +250,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   __shared__ int wcount[NW][R];                  // running count -> wave offset within tile
   __shared__ int dstart[R];                      // tile-local start of each digit
   __shared__ int gbase[R];                       // global start of this tile's digit run
+                                                 // (LEADER: global start - tile-local start)
   __shared__ int skey[TILE];
   __shared__ int sa[TILE];
   __shared__ int sb[HAS_B ? TILE : 1];
@@ -284,11 +292,23 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
       const unsigned long long m = __ballot((digit >> bit) & 1);
       match &= ((digit >> bit) & 1) ? m : ~m;
     }
+#if HGNN_SORT_LEADER
+    const int below = __popcll(match & lt_mask);
+    const bool leader = valid && below == 0;
+    int before = leader ? wcount[wid][digit] : 0;        // the group's first lane reads ...
+    const int src = valid ? (int)__builtin_ctzll(match) : lane;
+    before = __builtin_amdgcn_ds_bpermute(src << 2, before);   // ... and hands it to the group
+    rank[r] = valid ? before + below : -1;
+    __builtin_amdgcn_wave_barrier();
+    if (leader) wcount[wid][digit] = before + __popcll(match);
+    __builtin_amdgcn_wave_barrier();
+#else
     const int before = valid ? wcount[wid][digit] : 0;    // read, then the leader bumps it
     rank[r] = valid ? before + __popcll(match & lt_mask) : -1;
     __builtin_amdgcn_wave_barrier();
     if (valid && __popcll(match & lt_mask) == 0) wcount[wid][digit] = before + __popcll(match);
     __builtin_amdgcn_wave_barrier();
+#endif
   }
   __syncthreads();
   // tile-local digit starts (exclusive scan over digits of the tile totals) and wave offsets
@@ -319,7 +339,11 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     for (int q = 0; q < DPT; ++q) {
       const int dd = threadIdx.x * DPT + q;
       if (dd < R) {
+#if HGNN_SORT_LEADER
+        gbase[dd] -= run;                          // the run's global start minus its tile start
+#else
         dstart[dd] = run;
+#endif
         int o = run;
         for (int w = 0; w < NW; ++w) {
           const int c = wcount[w][dd];
@@ -346,7 +370,11 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   for (int j = threadIdx.x; j < n_tile; j += kSortThreads) {
     const int k = skey[j];
     const int digit = (k >> shift) & (R - 1);
+#if HGNN_SORT_LEADER
+    const int64_t pos = (int64_t)gbase[digit] + j;
+#else
     const int64_t pos = (int64_t)gbase[digit] + (j - dstart[digit]);
+#endif
     keys_out[pos] = k;
     a_out[pos] = sa[j];
     if (HAS_B) b_out[pos] = sb[j];

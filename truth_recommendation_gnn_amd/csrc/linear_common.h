@@ -79,6 +79,23 @@ __device__ __forceinline__ uint32_t relu_bits(float4 v, int shift) {
           (v.w > 0.f ? 8u : 0u)) << shift;
 }
 
+// relu_bits of a ReLU OUTPUT (every element +0, -0 or positive; relu1 maps NaN to 0): v > 0 is
+// exactly "the bits as a signed int are >= 1", so one v_med3_i32(bits, 0, 1) per element gives
+// the bit and three v_lshl_or_b32 pack them — 8 VALU where the compares and selects took 11 plus
+// the VCC hazard nops between them
+__device__ __forceinline__ uint32_t pos_bit(float v) {
+  uint32_t r;
+  asm("v_med3_i32 %0, %1, 0, 1" : "=v"(r) : "v"(v));
+  return r;
+}
+__device__ __forceinline__ uint32_t relu_out_bits(float4 v, int shift) {
+  uint32_t r = pos_bit(v.x) << shift;
+  r |= pos_bit(v.y) << (shift + 1);
+  r |= pos_bit(v.z) << (shift + 2);
+  r |= pos_bit(v.w) << (shift + 3);
+  return r;
+}
+
 // dX fragment store of the persistent kernels: stored, or added into what dx holds (the
 // gradient of a node table that another update already wrote — one pass instead of a torch add)
 __device__ __forceinline__ void store_dx4(float* p, bool add, float a0, float a1, float a2,

@@ -34,6 +34,9 @@
 #ifndef HGNN_XS_STAGGER
 #define HGNN_XS_STAGGER 1
 #endif
+#ifndef HGNN_XS_MASKMED
+#define HGNN_XS_MASKMED 1
+#endif
 
 namespace hgnn {
 
@@ -278,7 +281,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         }
         if (a.relu) v = relu4(v);
         po[r] = v;
+#if HGNN_XS_MASKMED
+        if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_out_bits(v, 4 * w));
+#else
         if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
+#endif
       }
       if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
       __syncthreads();
