@@ -160,13 +160,6 @@ constexpr int kSortThreads = HGNN_SORT_THREADS;
 constexpr int kSortRounds = HGNN_SORT_ROUNDS;             // one item per thread per round
 constexpr int kSortTile = kSortThreads * kSortRounds;     // 8192 items per block
 constexpr int kMaxRadix = 1024;
-// HGNN_SORT_LEADER: in the scatter's ranking only the first lane of each digit group reads the
-// wave's running count (the others get it by ds_bpermute from that lane: no bank conflicts) —
-// 64 random LDS reads per round become ~40.  The reorder's two lookups per item (the run's global
-// start and its tile-local start) are one table of their difference.
-#ifndef HGNN_SORT_LEADER
-#define HGNN_SORT_LEADER 1
-#endif
 
 // key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
 __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
@@ -248,9 +241,8 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   constexpr int TILE = kSortThreads * RR;
   constexpr int PER_WAVE = TILE / NW;
   __shared__ int wcount[NW][R];                  // running count -> wave offset within tile
-  __shared__ int dstart[R];                      // tile-local start of each digit
-  __shared__ int gbase[R];                       // global start of this tile's digit run
-                                                 // (LEADER: global start - tile-local start)
+  __shared__ int gbase[R];                       // global start of this tile's digit run, then
+                                                 // minus its tile-local start
   __shared__ int skey[TILE];
   __shared__ int sa[TILE];
   __shared__ int sb[HAS_B ? TILE : 1];
@@ -292,7 +284,9 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
       const unsigned long long m = __ballot((digit >> bit) & 1);
       match &= ((digit >> bit) & 1) ? m : ~m;
     }
-#if HGNN_SORT_LEADER
+    // only the first lane of each digit group reads the wave's running count; the others get
+    // it from that lane by ds_bpermute (64 random LDS reads per round become ~40; round 5:
+    // 2.884 -> 2.872 ms for the cfg4 negatives)
     const int below = __popcll(match & lt_mask);
     const bool leader = valid && below == 0;
     int before = leader ? wcount[wid][digit] : 0;        // the group's first lane reads ...
@@ -302,13 +296,6 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     __builtin_amdgcn_wave_barrier();
     if (leader) wcount[wid][digit] = before + __popcll(match);
     __builtin_amdgcn_wave_barrier();
-#else
-    const int before = valid ? wcount[wid][digit] : 0;    // read, then the leader bumps it
-    rank[r] = valid ? before + __popcll(match & lt_mask) : -1;
-    __builtin_amdgcn_wave_barrier();
-    if (valid && __popcll(match & lt_mask) == 0) wcount[wid][digit] = before + __popcll(match);
-    __builtin_amdgcn_wave_barrier();
-#endif
   }
   __syncthreads();
   // tile-local digit starts (exclusive scan over digits of the tile totals) and wave offsets
@@ -327,7 +314,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     }
     part[threadIdx.x] = s;
     __syncthreads();
-    // Hillis-Steele inclusive scan of the 256 per-thread sums
+    // Hillis-Steele inclusive scan of the kSortThreads per-thread sums
     for (int o = 1; o < kSortThreads; o <<= 1) {
       const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
       __syncthreads();
@@ -339,11 +326,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     for (int q = 0; q < DPT; ++q) {
       const int dd = threadIdx.x * DPT + q;
       if (dd < R) {
-#if HGNN_SORT_LEADER
-        gbase[dd] -= run;                          // the run's global start minus its tile start
-#else
-        dstart[dd] = run;
-#endif
+        gbase[dd] -= run;   // the run's global start minus its tile start: one lookup per item
         int o = run;
         for (int w = 0; w < NW; ++w) {
           const int c = wcount[w][dd];
@@ -370,11 +353,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   for (int j = threadIdx.x; j < n_tile; j += kSortThreads) {
     const int k = skey[j];
     const int digit = (k >> shift) & (R - 1);
-#if HGNN_SORT_LEADER
     const int64_t pos = (int64_t)gbase[digit] + j;
-#else
-    const int64_t pos = (int64_t)gbase[digit] + (j - dstart[digit]);
-#endif
     keys_out[pos] = k;
     a_out[pos] = sa[j];
     if (HAS_B) b_out[pos] = sb[j];
@@ -445,9 +424,11 @@ __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
 }
 
 // Digit width: the one of 6..9 bits minimising passes x measured per-pass time (counts + scan +
-// scatter, 20M pairs on MI355X: 6 bits 108 us, 7 bits 117, 8 bits 147, 9 bits 183 — fewer digits
-// mean longer per-digit runs per 4096-item tile, so a 6-bit pass writes ~256-B runs where a 9-bit
-// one writes ~32-B runs).  17-bit post ids: 3 passes of 6 (339 us) beat 2 of 9 (381); 20-bit:
+// scatter, 20M pairs on MI355X: 6 bits 108 us, 7 bits 117, 8 bits 147, 9 bits 183 — measured in
+// round 1 on the then 4096-item tile; fewer digits mean longer per-digit runs per tile, so a
+// 6-bit pass writes ~256-B runs where a 9-bit one writes ~32-B runs, twice that on today's
+// kSortTile of 8192).  The planner still chooses 7 + 7 + 6 bits for the cfg4 negatives, which the
+// round-4 A/B on the 8192-item tile confirmed (scripts/gpu_sort_ab.sh).  17-bit post ids: 3 passes of 6 (339 us) beat 2 of 9 (381); 20-bit:
 // 3 of 7.  (10-bit digits, 2 passes for 19-20-bit ids, were measured slower than 3 passes of 8.)
 static void radix_plan(int64_t n_keys, int* passes, int* bits) {
   int b = 0;
