@@ -34,11 +34,36 @@
 #ifndef HGNN_XS_STAGGER
 #define HGNN_XS_STAGGER 1
 #endif
+#ifndef HGNN_XS_SPLITILP
+#define HGNN_XS_SPLITILP 0
+#endif
 #ifndef HGNN_XS_MASKMED
 #define HGNN_XS_MASKMED 1
 #endif
 
 namespace hgnn {
+
+// HGNN_XS_STAMPS (a diagnostic build only, scripts/k3_stamps.py): lane 0 of every wave of the
+// first 64 blocks records s_memtime at the phase boundaries of 8 loop iterations into a buffer
+// of its own, read back by hgnn_debug_xs_stamps; no output and no other code reads them.
+#ifndef HGNN_XS_STAMPS
+#define HGNN_XS_STAMPS 0
+#endif
+#if HGNN_XS_STAMPS
+constexpr int kStampBlocks = 64, kStampIters = 8, kStampFirst = 40, kStampPts = 8;
+__device__ unsigned long long g_xs_stamps[kStampBlocks * 8 * kStampIters * kStampPts];
+#define XS_STAMP(it, k)                                                                          \
+  do {                                                                                           \
+    if (blockIdx.x < kStampBlocks && (it) >= kStampFirst && (it) < kStampFirst + kStampIters) {   \
+      const unsigned long long ts_ = __builtin_amdgcn_s_memtime();                               \
+      if ((threadIdx.x & 63) == 0)                                                               \
+        g_xs_stamps[(((int)blockIdx.x * 8 + (int)(threadIdx.x >> 6)) * kStampIters +            \
+                     ((it) - kStampFirst)) * kStampPts + (k)] = ts_;                            \
+    }                                                                                            \
+  } while (0)
+#else
+#define XS_STAMP(it, k) do { } while (0)
+#endif
 
 namespace {
 
@@ -52,6 +77,32 @@ __device__ __forceinline__ uint32_t clamp_row(int64_t row, int32_t last) {
   return min((uint32_t)row, (uint32_t)last);   // row < 2^32: n < 2^31 and at most 2 G R past it
 }
 typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// The three-piece split of N float4 at once, level by level (HGNN_XS_SPLITILP): every level's
+// converts, extracts and subtractions are independent across the 2N value pairs, where the
+// per-pair order chains ~11 dependent instructions (in-kernel stamps: a wave's split of 16
+// values took ~900 cycles for ~90 VALU).  pc[level][j][h]: the packed bf16 pair of level
+// `level` for values 2h, 2h+1 of float4 j — the words x6_split4 produces.
+template <int N>
+__device__ __forceinline__ void x6_split_levels(float (&v)[N][4], uint32_t (&pc)[3][N][2]) {
+#pragma unroll
+  for (int lv = 0; lv < 3; ++lv) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pc[lv][j][h] = x6_cvt_pk(v[j][2 * h], v[j][2 * h + 1]);
+    if (lv < 2) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          v[j][2 * h] -= __uint_as_float(pc[lv][j][h] << 16);
+          v[j][2 * h + 1] -= __uint_as_float(pc[lv][j][h] & 0xffff0000u);
+        }
+    }
+  }
+}
+typedef uint32_t xs_u32x2 __attribute__((ext_vector_type(2)));
 
 // One [R x K] fp32 tile of the concatenated input, staged by all 512 threads: float4 j of thread
 // t is f = t + 512 j, row f / (K / 4), column 4 (f % (K / 4)) — a thread's column (and therefore
@@ -90,6 +141,29 @@ struct XStage {
   template <int LDP, int PS, bool ZERO = false>
   __device__ __forceinline__ void put(const Regs& x, unsigned short* pl, int64_t r0,
                                       int64_t n = 0) const {
+#if HGNN_XS_SPLITILP
+    // the split level by level across all NL float4 (2 NL value pairs): each level's converts,
+    // extracts and subtractions are independent, where the per-pair order chained ~11
+    // dependent instructions (stamps: a wave's split took ~900 cycles for ~90 VALU)
+    float v[NL][4];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      float4 u = x.v[j];
+      if (ZERO && r0 + row0 + j * RSTEP >= n) u = make_float4(0.f, 0.f, 0.f, 0.f);
+      v[j][0] = u.x; v[j][1] = u.y; v[j][2] = u.z; v[j][3] = u.w;
+    }
+    uint32_t pc[3][NL][2];
+    x6_split_levels<NL>(v, pc);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      unsigned short* d = pl + (row0 + j * RSTEP) * LDP + col;
+#pragma unroll
+      for (int lv = 0; lv < 3; ++lv)
+        *reinterpret_cast<bf16x4_t*>(d + lv * PS) =
+            __builtin_bit_cast(bf16x4_t, (xs_u32x2){pc[lv][j][0], pc[lv][j][1]});
+    }
+    return;
+#endif
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       float4 v = x.v[j];
@@ -146,6 +220,16 @@ __device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int la
 // kept: loads two tiles ahead in a second register set, the split interleaved into the sweep
 // — 3.84 vs 3.69 ms at 9M rows, K = 256; the kernel runs at a power-limited ~1.75 GHz, so
 // what counts is the instruction count, not the overlap.)
+// HGNN_XS_VMEM_STEP: the sweep step after which the iteration's memory instructions are issued
+// (-1: before the sweep).  In-kernel stamps (scripts/k3_stamps.py) showed each wave spending
+// ~600 cycles at the top of every iteration issuing them — all 8 waves queue ~48 KB of requests
+// on the CU's memory pipe right after the barrier — while its partner split: the matrix pipe sat
+// idle ~670 cycles per iteration.
+#ifndef HGNN_XS_VMEM_STEP
+#define HGNN_XS_VMEM_STEP -1
+#endif
+constexpr int kVmemStep = HGNN_XS_VMEM_STEP;
+
 template <int K, bool ADD>
 __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
                                                         int64_t n_tiles) {
@@ -214,18 +298,26 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
     int it = 0;
     for (; t < n_tiles; t += G, ++it) {
       const int b = it & 1;
+      XS_STAMP(it, 0);
       if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
-      if (it > 0) store_prev(t - G, b ^ 1);
-      if constexpr (ADD) {
+      XS_STAMP(it, 1);
+      // the iteration's memory instructions: the previous tile's output stores, this tile's
+      // added rows, the prefetch
+      auto vmem = [&]() {
+        if (it > 0) store_prev(t - G, b ^ 1);
+        if constexpr (ADD) {
 #pragma unroll
-        for (int r = 0; r < RT; ++r) {
-          const uint32_t row = clamp_row(t * R + 16 * r + i, last);
-          ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+          for (int r = 0; r < RT; ++r) {
+            const uint32_t row = clamp_row(t * R + 16 * r + i, last);
+            ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+          }
+          __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
         }
-        __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
-      }
-      xs.issue(xr, (t + (LATE ? 2 : 1) * G) * R, last);
-      __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of the MFMA sweep
+        xs.issue(xr, (t + (LATE ? 2 : 1) * G) * R, last);
+        __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of what follows
+      };
+      if constexpr (kVmemStep < 0) vmem();
+      XS_STAMP(it, 2);
       const unsigned short* p = pl[b];
       f32x4 hi[RT], lo[RT];
 #if HGNN_XS_LDSPF
@@ -248,6 +340,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
+          if constexpr (kVmemStep >= 0) {
+            if (q == kVmemStep) vmem();   // after the sweep has the matrix pipe going
+          }
           if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
           __builtin_amdgcn_sched_barrier(0);
           x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
@@ -268,6 +363,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         }
       }
 #endif
+      XS_STAMP(it, 3);
       // the stored rows' registers are reserved until here (see above)
 #pragma unroll
       for (int r = 0; r < RT; ++r)
@@ -287,8 +383,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
 #endif
       }
+      XS_STAMP(it, 4);
       if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
+      XS_STAMP(it, 5);
       __syncthreads();
+      XS_STAMP(it, 6);
     }
     store_prev(t - G, (it - 1) & 1);
   };
@@ -364,6 +463,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   };
   float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
   auto put = [&](int64_t tt, int b) {
+#if HGNN_XS_SPLITILP
+    float zs[ZL][4];
+#endif
 #pragma unroll
     for (int j = 0; j < ZL; ++j) {
       const int64_t row = tt * R + zr + 16 * j;
@@ -377,12 +479,28 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       if (row >= a.n) z = make_float4(0.f, 0.f, 0.f, 0.f);
       else if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + row * kH + zc) = z;
       dbacc.x += z.x; dbacc.y += z.y; dbacc.z += z.z; dbacc.w += z.w;
+#if HGNN_XS_SPLITILP
+      zs[j][0] = z.x; zs[j][1] = z.y; zs[j][2] = z.z; zs[j][3] = z.w;
+    }
+    {
+      uint32_t pc[3][ZL][2];
+      x6_split_levels<ZL>(zs, pc);
+#pragma unroll
+      for (int j = 0; j < ZL; ++j) {
+        unsigned short* d = zp[b] + (zr + 16 * j) * LDZ + zc;
+#pragma unroll
+        for (int lv = 0; lv < 3; ++lv)
+          *reinterpret_cast<bf16x4_t*>(d + lv * ZS) =
+              __builtin_bit_cast(bf16x4_t, (xs_u32x2){pc[lv][j][0], pc[lv][j][1]});
+      }
+#else
       bf16x4_t p1, p2, p3;
       x6_split4(z, p1, p2, p3);
       unsigned short* d = zp[b] + (zr + 16 * j) * LDZ + zc;
       *reinterpret_cast<bf16x4_t*>(d) = p1;
       *reinterpret_cast<bf16x4_t*>(d + ZS) = p2;
       *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
+#endif
     }
     if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
   };
@@ -412,24 +530,32 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     __syncthreads();
     for (int it = 0; t < n_tiles; t += G, ++it) {
       const int b = it & 1;
+      XS_STAMP(it, 0);
       if constexpr (LATE) put(t + G, b ^ 1);
+      XS_STAMP(it, 1);
       // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
       // wait leaves the prefetch in flight
       float4 dxo[DT][ACC ? R / 16 : 1];
-      if constexpr (ACC) {
+      auto vmem = [&]() {
+        if constexpr (ACC) {
 #pragma unroll
-        for (int u = 0; u < DT; ++u) {
-          if (dxp[u]) {
+          for (int u = 0; u < DT; ++u) {
+            if (dxp[u]) {
 #pragma unroll
-            for (int r = 0; r < R / 16; ++r)
-              dxo[u][r] = *reinterpret_cast<const float4*>(
-                  dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
+              for (int r = 0; r < R / 16; ++r)
+                dxo[u][r] = *reinterpret_cast<const float4*>(
+                    dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
+            }
           }
+          __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      issue(t + (LATE ? 2 : 1) * G);   // consumed by the next put(), unconditionally (see forward)
-      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMA sweep
+        issue(t + (LATE ? 2 : 1) * G);   // consumed by the next put(), unconditionally (see forward)
+        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of what follows
+      };
+      // the memory instructions before the first sweep, or inside it (HGNN_XS_VMEM_STEP, see the
+      // forward): in the dgrad sweep when there is one, else in the wgrad sweep
+      if constexpr (kVmemStep < 0) vmem();
+      XS_STAMP(it, 2);
       const unsigned short* z = zp[b];
       f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
 #if HGNN_XS_LDSPF
@@ -455,6 +581,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
+          if constexpr (kVmemStep >= 0) {
+            if (q == kVmemStep) vmem();
+          }
           if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
           __builtin_amdgcn_sched_barrier(0);
           const bf16x8_t(&f)[3] = fr[q % (PF + 1)];
@@ -464,6 +593,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      XS_STAMP(it, 3);
       if constexpr (WG) {
         const unsigned short* x = xp[b];
         bf16x8_t xb[KT][3];
@@ -479,6 +609,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
+          if constexpr (kVmemStep >= 0 && !DX) {
+            if (h == (kVmemStep < 8 ? kVmemStep : 7)) vmem();
+          }
           if (h + PF < 8) {
 #pragma unroll
             for (int q = 0; q < 3; ++q)
@@ -524,6 +657,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         }
       }
 #endif
+      XS_STAMP(it, 4);
       if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
 #pragma unroll
         for (int u = 0; u < DT; ++u)
@@ -543,8 +677,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
             }
           }
       }
+      XS_STAMP(it, 5);
       if constexpr (!LATE) put(t + G, b ^ 1);
+      XS_STAMP(it, 6);
       __syncthreads();
+      XS_STAMP(it, 7);
     }
   };
 #if HGNN_XS_STAGGER
@@ -589,6 +726,15 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
 }
 
 }  // namespace
+
+#if HGNN_XS_STAMPS
+extern "C" int hgnn_debug_xs_stamps(unsigned long long* host, size_t n) {
+  const size_t have = sizeof(g_xs_stamps) / sizeof(g_xs_stamps[0]);
+  if (n > have) n = have;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xs_stamps), n * sizeof(unsigned long long)) ==
+                 hipSuccess ? (int)n : -1;
+}
+#endif
 
 int64_t xs_bwd_grid(int64_t n_rows) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_rows, 32), 256));
