@@ -4,7 +4,7 @@ diagnostic build: `python scripts/build_variant.py stamps -DHGNN_XS_STAMPS=1 --o
 run with HGNN_LIB=libhgnn_stamps.so).  Lane 0 of every wave of blocks 0-63 stamps 7 points of
 iterations 40-47: 0 top, 1 after the late waves' split, 2 after the output stores + the prefetch
 issue, 3 after the MFMA sweep is issued, 4 after the epilogue, 5 after the early waves' split,
-6 after the barrier.  The backward kernel stamps 8 points: top, after the late waves'
+6 after the barrier (8 / 9: after an explicit wait for the loads before the late / early split).  The backward kernel stamps 8 points: top, after the late waves'
 put, after the memory issue, after the dgrad sweep, after the wgrad sweep, after the dX stores,
 after the early waves' put, after the barrier.  Prints the mean cycles of each phase for waves
 0-3 (early) and 4-7 (late) per shape, as one JSON line each.
@@ -20,7 +20,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from truth_recommendation_gnn_amd import _native as N, ops  # noqa: E402
 
-BLOCKS, WAVES, ITERS, PTS = 64, 8, 8, 8
+BLOCKS, WAVES, ITERS, PTS = 64, 8, 8, 12
 NAMES = {"fwd": ["late_split", "stores+issue", "sweep_issue", "epilogue", "early_split", "barrier"],
          "bwd": ["late_put", "vmem_issue", "dgrad_sweep", "wgrad_sweep", "dx_stores", "early_put",
                  "barrier"]}
@@ -72,6 +72,15 @@ def main():
             ph = d[:, lo:hi].reshape(-1, npts - 1).mean(0)
             rec[tag] = {k: round(float(v), 1) for k, v in zip(names, ph)}
             rec[tag]["iteration"] = round(float(tot[:, lo:hi].mean()), 1)
+        # the split's wait for its loads (points 8 / 9, an explicit vmcnt(0) before the split)
+        sp = len(names) - 2   # the point before the early split
+        late_w = (s[:, 4:8, :, 8] - s[:, 4:8, :, 0]).mean()
+        early_w = (s[:, 0:4, :, 9] - s[:, 0:4, :, sp]).mean()
+        rec["late"]["split_load_wait"] = round(float(late_w), 1)
+        rec["early"]["split_load_wait"] = round(float(early_w), 1)
+        if kind == "bwd":   # the late put: dz part (8 -> 10), X part (10 -> 11)
+            rec["late"]["put_dz"] = round(float((s[:, 4:8, :, 10] - s[:, 4:8, :, 8]).mean()), 1)
+            rec["late"]["put_x"] = round(float((s[:, 4:8, :, 11] - s[:, 4:8, :, 10]).mean()), 1)
         print(json.dumps(rec), flush=True)
 
 

@@ -40,6 +40,12 @@
 #ifndef HGNN_XS_MASKMED
 #define HGNN_XS_MASKMED 1
 #endif
+// HGNN_XS_PROBE (timing probes only, wrong results): 1 = no HBM traffic in the forward (every
+// tile's loads hit the first R rows, no output stores); 2 = no MFMA sweep in the forward; 3 = as 1
+// with the stores kept; 4 = the loads kept, no stores
+#ifndef HGNN_XS_PROBE
+#define HGNN_XS_PROBE 0
+#endif
 
 namespace hgnn {
 
@@ -50,7 +56,7 @@ namespace hgnn {
 #define HGNN_XS_STAMPS 0
 #endif
 #if HGNN_XS_STAMPS
-constexpr int kStampBlocks = 64, kStampIters = 8, kStampFirst = 40, kStampPts = 8;
+constexpr int kStampBlocks = 64, kStampIters = 8, kStampFirst = 40, kStampPts = 12;
 __device__ unsigned long long g_xs_stamps[kStampBlocks * 8 * kStampIters * kStampPts];
 #define XS_STAMP(it, k)                                                                          \
   do {                                                                                           \
@@ -61,8 +67,16 @@ __device__ unsigned long long g_xs_stamps[kStampBlocks * 8 * kStampIters * kStam
                      ((it) - kStampFirst)) * kStampPts + (k)] = ts_;                            \
     }                                                                                            \
   } while (0)
+// points 8 / 9: after an explicit wait for every outstanding memory operation right before the
+// late / early waves' split — how much of a split phase is waiting for its loads
+#define XS_WAIT_STAMP(it, k)                                                                     \
+  do {                                                                                           \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                            \
+    XS_STAMP(it, k);                                                                             \
+  } while (0)
 #else
 #define XS_STAMP(it, k) do { } while (0)
+#define XS_WAIT_STAMP(it, k) do { } while (0)
 #endif
 
 namespace {
@@ -128,10 +142,16 @@ struct XStage {
   // rows past the end are clamped to the last row (loaded, never stored).  (Measured and not
   // kept: a uniform in-range test per tile taking one v_mad_u64_u32 and 64-bit adds for the row
   // addresses — fewer VALU, but 3.42 -> 3.46 ms at K = 256 forward, 3.55 -> 3.64 backward.)
+  __device__ __forceinline__ void issue_one(Regs& x, int64_t r0, int32_t last, int j) const {
+    const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(row0 + j * RSTEP)
+                                                                    : clamp_row(r0 + row0 + j * RSTEP, last);
+    x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
+  }
   __device__ __forceinline__ void issue(Regs& x, int64_t r0, int32_t last) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const uint32_t row = clamp_row(r0 + row0 + j * RSTEP, last);
+      const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(row0 + j * RSTEP)
+                                              : clamp_row(r0 + row0 + j * RSTEP, last);
       x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
     }
   }
@@ -229,6 +249,21 @@ __device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int la
 #define HGNN_XS_VMEM_STEP -1
 #endif
 constexpr int kVmemStep = HGNN_XS_VMEM_STEP;
+#ifndef HGNN_XS_BIASINIT
+#define HGNN_XS_BIASINIT 0
+#endif
+constexpr bool kBiasInit = HGNN_XS_BIASINIT != 0;
+// HGNN_XS_VMEM_SPREAD (default on, round 5): the iteration's memory instructions one or two per
+// sweep step (the added rows first, then the previous tile's stores and mask words, then the
+// prefetch) instead of one burst after the barrier.  Probes (HGNN_XS_PROBE) put ~1 ms of the
+// K = 256 forward's 3.45 ms in its loads and stores (no HBM traffic: 2.52 ms; stores only 2.96;
+// loads only 3.12), and the stamps showed all 8 waves stalled ~600 cycles issuing them at once.
+// A/B at the cfg4 shapes: K = 128 + add 2.589 -> 2.512 ms, K = 128 (preprojection, 1M rows)
+// 0.219 -> 0.198, K = 256 unchanged (3.433 / 3.436).
+#ifndef HGNN_XS_VMEM_SPREAD
+#define HGNN_XS_VMEM_SPREAD 1
+#endif
+constexpr bool kSpread = HGNN_XS_VMEM_SPREAD != 0;
 
 template <int K, bool ADD>
 __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
@@ -259,15 +294,29 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   float4 po[RT];   // the previous tile's output rows
 #pragma unroll
   for (int r = 0; r < RT; ++r) po[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto store_one = [&](int64_t tp, int r) {
+    const int64_t row = tp * R + 16 * r + i;
+    if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n)
+      *reinterpret_cast<float4*>(a.out + row * kH + 16 * w + 4 * g) = po[r];
+  };
+  auto mask_one = [&](int64_t tp, int bp) {
+    if (mask_out && threadIdx.x < R * 4) {
+      const int64_t row = tp * R + (threadIdx.x >> 2);
+      if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n)
+        a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
+      mk[bp][threadIdx.x] = 0u;
+    }
+  };
   auto store_prev = [&](int64_t tp, int bp) {
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const int64_t row = tp * R + 16 * r + i;
-      if (row < a.n) *reinterpret_cast<float4*>(a.out + row * kH + 16 * w + 4 * g) = po[r];
+      if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n)
+        *reinterpret_cast<float4*>(a.out + row * kH + 16 * w + 4 * g) = po[r];
     }
     if (mask_out && threadIdx.x < R * 4) {   // its mask words are complete (last barrier)
       const int64_t row = tp * R + (threadIdx.x >> 2);
-      if (row < a.n) a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
+      if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n) a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
       mk[bp][threadIdx.x] = 0u;
     }
   };
@@ -299,6 +348,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
     for (; t < n_tiles; t += G, ++it) {
       const int b = it & 1;
       XS_STAMP(it, 0);
+      if constexpr (LATE) XS_WAIT_STAMP(it, 8);
       if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
       XS_STAMP(it, 1);
       // the iteration's memory instructions: the previous tile's output stores, this tile's
@@ -308,7 +358,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         if constexpr (ADD) {
 #pragma unroll
           for (int r = 0; r < RT; ++r) {
-            const uint32_t row = clamp_row(t * R + 16 * r + i, last);
+            const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(16 * r + i)
+                                                    : clamp_row(t * R + 16 * r + i, last);
             ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
           }
           __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
@@ -316,7 +367,31 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         xs.issue(xr, (t + (LATE ? 2 : 1) * G) * R, last);
         __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of what follows
       };
-      if constexpr (kVmemStep < 0) vmem();
+      // the same instructions spread over the sweep (HGNN_XS_VMEM_SPREAD): piece k at step
+      // k * NQ / NP — the added rows, the stores, the mask words, the prefetch
+      auto vmem_step = [&](int q) {
+        constexpr int NA = ADD ? RT : 0, NX = XStage<K, R>::NL, NP = NA + RT + 1 + NX;
+        constexpr int NQ = RT * (K / 32);
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+          if (k * NQ / NP != q) continue;
+          if (k < NA) {
+            if constexpr (ADD) {
+              const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3)
+                                       ? (uint32_t)(16 * k + i)
+                                       : clamp_row(t * R + 16 * k + i, last);
+              ad[k] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+            }
+          } else if (k < NA + RT) {
+            if (it > 0) store_one(t - G, k - NA);
+          } else if (k == NA + RT) {
+            if (it > 0) mask_one(t - G, b ^ 1);
+          } else {
+            xs.issue_one(xr, (t + (LATE ? 2 : 1) * G) * R, last, k - NA - RT - 1);
+          }
+        }
+      };
+      if constexpr (kVmemStep < 0 && !kSpread) vmem();
       XS_STAMP(it, 2);
       const unsigned short* p = pl[b];
       f32x4 hi[RT], lo[RT];
@@ -334,7 +409,12 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
           f[2] = row8<LDP>(p + 2 * PS, 16 * r, 32 * s2, i, g);
         };
 #pragma unroll
-        for (int r = 0; r < RT; ++r) hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < RT; ++r) {
+          // HGNN_XS_BIASINIT: the bias as the large-term accumulator's initial value (a GEMM
+          // with C = bias), not an add per element in the epilogue
+          hi[r] = kBiasInit ? f32x4{bb.x, bb.y, bb.z, bb.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+          lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
         for (int q = 0; q < PF; ++q) ld(q, fr[q]);
         __builtin_amdgcn_sched_barrier(0);
@@ -343,17 +423,21 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
           if constexpr (kVmemStep >= 0) {
             if (q == kVmemStep) vmem();   // after the sweep has the matrix pipe going
           }
+          if constexpr (kSpread) vmem_step(q);
           if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
           __builtin_amdgcn_sched_barrier(0);
-          x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
-                 hi[q / KS], lo[q / KS]);
+          if constexpr (HGNN_XS_PROBE != 2)
+            x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
+                   hi[q / KS], lo[q / KS]);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
 #else
+      static_assert(!kSpread, "HGNN_XS_VMEM_SPREAD needs HGNN_XS_LDSPF");
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        hi[r] = lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+        hi[r] = kBiasInit ? f32x4{bb.x, bb.y, bb.z, bb.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+        lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
@@ -370,8 +454,14 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        float4 v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
-                               x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
+        float4 v;
+        if constexpr (kBiasInit) {
+          v = make_float4(x6_out(hi[r][0], lo[r][0]), x6_out(hi[r][1], lo[r][1]),
+                          x6_out(hi[r][2], lo[r][2]), x6_out(hi[r][3], lo[r][3]));
+        } else {
+          v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
+                          x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
+        }
         if constexpr (ADD) {
           v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
         }
@@ -384,6 +474,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
 #endif
       }
       XS_STAMP(it, 4);
+      if constexpr (!LATE) XS_WAIT_STAMP(it, 9);
       if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
       XS_STAMP(it, 5);
       __syncthreads();
@@ -462,7 +553,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     if constexpr (WG) xs.issue(xr, tt * R, last32);
   };
   float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto put = [&](int64_t tt, int b) {
+  auto put = [&](int64_t tt, int b, int sit) {   // sit: the iteration for stamp 10 / 11, or -1
 #if HGNN_XS_SPLITILP
     float zs[ZL][4];
 #endif
@@ -502,7 +593,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
 #endif
     }
+    XS_STAMP(sit, 10);
     if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
+    XS_STAMP(sit, 11);
   };
   f32x4 hw[WG ? 8 : 1][KT], lw[WG ? 8 : 1][KT];
 #pragma unroll
@@ -522,7 +615,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   }
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   issue(t);
-  put(t, 0);
+  put(t, 0, -1);
   // staggered halves as in the forward: waves 4-7 put the next tile first, then sweep
   auto loop = [&](auto late_c) {
     constexpr bool LATE = decltype(late_c)::value;
@@ -531,7 +624,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     for (int it = 0; t < n_tiles; t += G, ++it) {
       const int b = it & 1;
       XS_STAMP(it, 0);
-      if constexpr (LATE) put(t + G, b ^ 1);
+      if constexpr (LATE) XS_WAIT_STAMP(it, 8);
+      if constexpr (LATE) put(t + G, b ^ 1, it);
       XS_STAMP(it, 1);
       // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
       // wait leaves the prefetch in flight
@@ -678,7 +772,8 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
           }
       }
       XS_STAMP(it, 5);
-      if constexpr (!LATE) put(t + G, b ^ 1);
+      if constexpr (!LATE) XS_WAIT_STAMP(it, 9);
+      if constexpr (!LATE) put(t + G, b ^ 1, -1);
       XS_STAMP(it, 6);
       __syncthreads();
       XS_STAMP(it, 7);
