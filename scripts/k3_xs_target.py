@@ -22,3 +22,18 @@ for _ in range(3):
     y2 = ops.linear_fwd([X], W1, b, True, add=add, mask_out=m2)
     ops.linear_bwd([X], W1, dout, y2, [dX], True, True, dz_out=dz, mask=m2)
 torch.cuda.synchronize()
+# algorithmic bytes per launch of the four launches, as the bench's per-kernel timer counts them
+# (one more iteration under ops.KernelTimer; scripts/pmc_k3_traffic_summarize.py divides the PMC
+# bytes by these)
+import json  # noqa: E402
+timer = ops.KernelTimer()
+ops.set_timer(timer)
+y1 = ops.linear_fwd([A, X], W2, b, True, mask_out=m1)
+ops.linear_bwd([A, X], W2, dout, y1, [None, None], True, True, mask=m1)
+y2 = ops.linear_fwd([X], W1, b, True, add=add, mask_out=m2)
+ops.linear_bwd([X], W1, dout, y2, [dX], True, True, dz_out=dz, mask=m2)
+ops.set_timer(None)
+torch.cuda.synchronize()
+summ = timer.summary()
+print("K3_ALG " + json.dumps({"n": n, "bytes": {k: v["bytes"] / v["launches"] for k, v in summ.items()}}),
+      flush=True)
