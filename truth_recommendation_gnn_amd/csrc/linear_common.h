@@ -55,11 +55,18 @@ struct ChunkTab {
 // the lane (i, g) that holds columns 16 c + 4 g .. +3 (c = 0 .. H/16 - 1) of row i finds them in
 // word row * 4 + g, bits 4 c .. 4 c + 3 (H <= 128, a multiple of 16): one 4-B word per lane per
 // row, no cross-lane exchange in the forward, 16 B per row instead of the output's 4 H.
+// Each element kept or zeroed by its bit: v_bfe_i32(word, bit, 1) is 0 or all ones, ANDed with
+// the element's bits — two VALU per element, no compare, select or VCC hazard (a zeroed element
+// is +0, a NaN with its bit clear too, as the select gave)
+__device__ __forceinline__ float mask1(float v, uint32_t word, int bit) {
+  const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)word, (unsigned)bit, 1u);
+  return __uint_as_float(__float_as_uint(v) & m);
+}
 __device__ __forceinline__ float4 mask4(float4 v, uint32_t word, int shift) {
-  v.x = (word >> shift) & 1u ? v.x : 0.f;
-  v.y = (word >> (shift + 1)) & 1u ? v.y : 0.f;
-  v.z = (word >> (shift + 2)) & 1u ? v.z : 0.f;
-  v.w = (word >> (shift + 3)) & 1u ? v.w : 0.f;
+  v.x = mask1(v.x, word, shift);
+  v.y = mask1(v.y, word, shift + 1);
+  v.z = mask1(v.z, word, shift + 2);
+  v.w = mask1(v.w, word, shift + 3);
   return v;
 }
 

@@ -596,6 +596,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
     XS_STAMP(sit, 11);
   };
+  // (Measured and not kept: a uniform branch to a copy of the put without the per-row zeroing
+  // on every tile but the last — within noise at the cfg4 shapes, and the K = 256 wgrad kernel
+  // spills with the second copy.)
   f32x4 hw[WG ? 8 : 1][KT], lw[WG ? 8 : 1][KT];
 #pragma unroll
   for (int h = 0; h < (WG ? 8 : 1); ++h)
