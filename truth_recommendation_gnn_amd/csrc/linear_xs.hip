@@ -338,7 +338,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   // rows at K = 256, 80 at K = 128: fewer barriers and epilogue phases per MFMA) measured the
   // same (3.52 / 3.49 ms, 2.68 / 2.69 ms).
   // (Measured and not kept: a prefetch two tiles deep in a second register set, with the added
-  // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256.)
+  // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256; round 5
+  // again for the early waves only, the loop unrolled by two so the sets alternate at compile
+  // time: 3.575 / 3.574 ms at K = 256, 2.614 / 2.613 at K = 128 + add.)
   auto loop = [&](auto late_c) {
     constexpr bool LATE = decltype(late_c)::value;
     if constexpr (LATE) xs.issue(xr, (t + G) * R, last);
