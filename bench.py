@@ -764,12 +764,14 @@ def _projection(kern):
     name = max(lin, key=lambda k: lin[k]["flops"] / lin[k]["launches"])
     r = lin[name]
     import re
-    m = re.search(r"\[(\d+)x(\d+)->(\d+)\]", name)
-    n, k, h = (int(m.group(1)), int(m.group(2)), int(m.group(3))) if m else (0, 0, 0)
-    x6 = (os.environ.get("HGNN_K3_X6", "1") != "0" and h == 128 and k in (128, 256))
+    # "[NxK->H]", or "[*xK->H]" for the sampled blocks' varying row counts (cfg5)
+    m = re.search(r"\[(\d+|\*)x(\d+)->(\d+)\]", name)
+    k, h = (int(m.group(2)), int(m.group(3))) if m else (0, 0)
+    x6 = (os.environ.get("HGNN_K3_X6", "1") != "0" and h == 128 and k in (128, 256, 384, 512))
     per_ms = r["ms"] / r["launches"]
     per_bytes = r["bytes"] / r["launches"]
     per_flops = r["flops"] / r["launches"]
+    n = (int(m.group(1)) if m.group(1) != "*" else int(per_flops / (2 * k * h))) if m else 0
     hbm_ms, mfma_ms = _k3_roof(n, k, h, per_bytes, x6)
     floor_ms = max(hbm_ms, mfma_ms)
     tfs = per_flops / (per_ms * 1e-3) / 1e12
@@ -787,7 +789,9 @@ def _projection(kern):
                             "row block, + 16*N for the ReLU mask bits)"}
     if x6:
         out["method"] = ("bf16x6: fp32-exact 3-piece bf16 split, 6 v_mfma_f32_16x16x32_bf16 "
-                         "products per fp32 product, f32 accumulate")
+                         "products per fp32 product, f32 accumulate"
+                         + (" (K > 256: two column-block launches, the second adding the "
+                            "first's rows)" if k > 256 else ""))
         out["floor_note"] = (f"mfma floor = 6*(N/16)*(H/16)*(K/32) MFMAs x {BF16_MFMA_CYCLES} "
                              f"cycles / {N_SIMDS} SIMDs at {MFMA_CLOCK_GHZ} GHz (the launches "
                              "measured ~1.85 GHz under load, DESIGN §5); hbm floor = bytes / "

@@ -297,7 +297,8 @@ int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_use
 
 /* K3 at H = 128 and K = 128 / 256 runs on bf16 MFMA as an fp32-exact three-piece split (each
  * fp32 operand = three bf16 pieces, six piece products per fp32 product, f32 accumulation:
- * fp32-class error; each operand element split once per block) unless
+ * fp32-class error; each operand element split once per block), and K = 384 / 512
+ * (every segment a multiple of 16 columns) as two column blocks on the same kernels, unless
  * HGNN_K3_X6=0.  on = 1 / 0 selects the split or the f32-input MFMA kernels for the calls that
  * follow (process-wide, not thread-safe against calls in flight); on < 0 only queries.  Returns
  * the previous setting. */

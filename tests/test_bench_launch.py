@@ -140,6 +140,15 @@ def test_bench_measurement_tail_runs_on_injected_summaries(monkeypatch):
     assert abs(proj["floor_ms"]["hbm"] - hbm_ms) < 1e-3 and abs(proj["floor_ms"]["mfma"] - mfma_ms) < 1e-3
     assert proj["bound"] == "hbm" and abs(proj["frac"] - hbm_ms / 3.12) < 1e-3
     assert proj["achieved"] <= proj["peak"]
+    # cfg5's sampled blocks: "[*xK->H]" labels, K = 384 on the split as two column blocks
+    n5 = 17_000
+    k5 = {"linear_fwd[*x384->128]": {"launches": 4, "ms": 4 * 0.0317,
+                                     "bytes": 4 * 4 * n5 * 512, "flops": 4 * 2 * n5 * 384 * 128,
+                                     "cbytes": 0}}
+    p5 = bench._projection(k5)
+    assert p5["method"].startswith("bf16x6") and "two column-block" in p5["method"]
+    mfma5 = 6 * (n5 / 16) * 8 * 12 * 16 / 1024 / 2.4e9 * 1e3
+    assert abs(p5["floor_ms"]["mfma"] - round(mfma5, 4)) < 1e-9 and 0 < p5["frac"] <= 1.0
 
     rows = bench._kernel_rows(kern, 5, "cfg4", 1)
     assert rows["gather_fwd[9000000<-1000000]x128"]["cache_assisted"]       # > 8 TB/s

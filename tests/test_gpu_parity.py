@@ -195,7 +195,9 @@ def test_gather_is_deterministic_bitwise():
                                   ([128, 128], 128), ([3, 5], 7), ([16], 200), ([64, 4], 100),
                                   ([64], 128), ([32], 16), ([64, 32], 32), ([64, 64], 128),
                                   ([16, 48, 64], 64), ([32, 96], 64), ([48, 16], 128),
-                                  ([128, 128], 64), ([64, 64, 128], 128), ([128], 128)])
+                                  ([128, 128], 64), ([64, 64, 128], 128), ([128], 128),
+                                  ([128, 128, 128], 128), ([128, 128, 128, 128], 128),
+                                  ([64, 256, 64], 128)])
 @pytest.mark.parametrize("n", [1, 37, 1000, 20000])
 def test_linear_fwd_bwd_matches_torch(ks, h, n):
     gen = torch.Generator().manual_seed(n + h)
@@ -249,7 +251,8 @@ def _linear_bwd_ref(segs, w, dout, out_act):
 
 
 @pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 64), ([64, 64], 128), ([16, 48], 128),
-                                  ([128, 128], 128), ([128, 128], 64), ([64, 64, 128], 128)])
+                                  ([128, 128], 128), ([128, 128], 64), ([64, 64, 128], 128),
+                                  ([128, 128, 128], 128), ([64, 256, 64], 128)])
 @pytest.mark.parametrize("mode", ["no_relu", "dx_subset", "wgrad_only", "db_only", "dgrad_only"])
 def test_linear_bwd_variants(ks, h, mode):
     """The compile-time-shape K3 backward (two-role, double-buffered tiles) under every operand
@@ -287,7 +290,8 @@ def test_linear_bwd_variants(ks, h, mode):
 
 
 @pytest.mark.parametrize("ks,h", [([64, 64], 64), ([64], 128), ([128, 128], 128), ([128], 128),
-                                  ([16, 48], 128), ([3, 5], 7), ([64, 64, 128], 128)])
+                                  ([16, 48], 128), ([3, 5], 7), ([64, 64, 128], 128),
+                                  ([128, 128, 128], 128)])
 @pytest.mark.parametrize("masked", [False, True])
 def test_linear_bwd_dx_accumulate_bitwise(ks, h, masked):
     """hgnn_linear_bwd_ex's accumulate bits (dX added into what the buffer holds, for tables with
@@ -370,7 +374,7 @@ def _unpack_relu_bits(mask, n, h):
 
 @pytest.mark.parametrize("ks,h", [([128, 128], 128), ([128], 128), ([64, 64], 64),
                                   ([64, 64, 128], 128), ([16, 48], 128), ([64], 48),
-                                  ([64, 64], 112)])
+                                  ([64, 64], 112), ([128, 128, 128], 128)])
 @pytest.mark.parametrize("mode", ["all", "wgrad_only", "dz_out"])
 def test_linear_relu_bits_equal_float_mask(ks, h, mode):
     """hgnn_linear_fwd_mask writes out > 0 as bits (persistent kernels, or k_relu_mask for other
@@ -1152,9 +1156,11 @@ def _k3_split(on):
 
 
 @pytest.mark.parametrize("split", [False, True])
-@pytest.mark.parametrize("ks", [[128], [128, 128], [64, 64, 128], [64, 64]])
+@pytest.mark.parametrize("ks", [[128], [128, 128], [64, 64, 128], [64, 64], [128, 128, 128],
+                                [64, 256, 64]])
 def test_linear_h128_on_both_k3_paths(split, ks):
-    """The H = 128 shapes the split covers (K = 128 and 256, 128-column segments and others),
+    """The H = 128 shapes the split covers (K = 128 and 256, 128-column segments and others;
+    K = 384 / 512 as two column blocks, a segment straddling the block edge included),
     through forward (with the added input and the ReLU bits), every backward mode and the
     accumulating dX, on the split and on the f32-input MFMA kernels it replaces by default."""
     with _k3_split(split):
@@ -1202,6 +1208,32 @@ def test_linear_split_passes_inf_and_nan_like_f32_kernels(ks, relu):
         assert bool(torch.isinf(a).any()) or relu
         scale = float(a[fin].abs().max())
         assert float((a[fin] - c[fin]).abs().max()) <= 2e-5 * scale
+
+
+@pytest.mark.parametrize("ks", [[128, 128, 128], [128, 128, 128, 128]])
+def test_k3_split_wide_matches_f32_kernels_closely(ks):
+    """K = 384 / 512 (cfg5's sampled blocks: [aggr_1 | aggr_2 | root]) on the split as two column
+    blocks — the second launch adding the first one's output rows, dW reduced per column block —
+    against the f32-input general kernels, at a block-sized row count: within 2e-5 of each
+    tensor's max."""
+    gen = torch.Generator().manual_seed(13)
+    n = 17_003
+    segs = [torch.randn(n, k, generator=gen).to(DEV) for k in ks]
+    w = (torch.randn(128, sum(ks), generator=gen) * 0.1).to(DEV)
+    b = torch.randn(128, generator=gen).to(DEV)
+    add = torch.randn(n, 128, generator=gen).to(DEV)
+    dout = torch.randn(n, 128, generator=gen).to(DEV)
+    res = {}
+    for split in (False, True):
+        with _k3_split(split):
+            mk = ops.relu_mask_for(n, 128, True, torch.device(DEV))
+            out = ops.linear_fwd(segs, w, b, True, add=add, mask_out=mk)
+            dxs = [torch.empty_like(s) for s in segs]
+            dw, db = ops.linear_bwd(segs, w, dout, out, dxs, True, True, mask=mk)
+            res[split] = [out, *dxs, dw, db]
+    for a, c in zip(res[False], res[True]):
+        scale = float(a.abs().max())
+        assert float((a - c).abs().max()) <= 2e-5 * scale, (float((a - c).abs().max()), scale)
 
 
 def test_k3_split_matches_f32_kernels_closely():

@@ -325,8 +325,10 @@ __global__ void __launch_bounds__(256) k_linear_wgrad(const LinArgs a) {
 }
 
 // dw[j][k] = sum_b slab[b][j][k] (k < K), db[j] = sum_b slab[b][j][K]; fixed b order.
+// ldd: dw's row stride (kext - 1, or the whole dW's K for a column block of it)
 __global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
-                                                       int32_t kext, float* dw, float* db) {
+                                                       int32_t kext, float* dw, float* db,
+                                                       int32_t ldd) {
   // 64 outputs per block (lanes), 16 waves each sum a contiguous range of slabs with 4
   // independent accumulators, then wave 0 adds the 16 partials in order: a fixed summation
   // order for a given nb (deterministic), and enough loads in flight to stream the slabs
@@ -354,7 +356,7 @@ __global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_
 #pragma unroll
     for (int w = 0; w < 16; ++w) v += part[w][lane];
     const int j = (int)(e / kext), k = (int)(e % kext);
-    if (k < kext - 1) { if (dw) dw[(int64_t)j * (kext - 1) + k] = v; }
+    if (k < kext - 1) { if (dw) dw[(int64_t)j * ldd + k] = v; }
     else if (db) db[j] = v;
   }
 }
@@ -1248,10 +1250,11 @@ static bool fwd4_ok(const LinArgs& a, bool vec) {
   return true;
 }
 
-static ChunkTab chunk_table(const LinArgs& a) {
+// the chunks of columns [c0, c0 + kp) of the concatenated input (every segment a multiple of 16)
+static ChunkTab chunk_table_range(const LinArgs& a, int c0, int kp) {
   ChunkTab t{};
-  for (int c = 0; c < a.k_total / 16 && c < kMaxChunks; ++c) {
-    const int k = c * 16;
+  for (int c = 0; c < kp / 16 && c < kMaxChunks; ++c) {
+    const int k = c0 + c * 16;
     int s = 0;
     while (s + 1 < a.n_seg && k >= a.seg[s].off + a.seg[s].k) ++s;
     t.x[c] = a.seg[s].x;
@@ -1261,6 +1264,68 @@ static ChunkTab chunk_table(const LinArgs& a) {
     t.col[c] = k - a.seg[s].off;
   }
   return t;
+}
+static ChunkTab chunk_table(const LinArgs& a) { return chunk_table_range(a, 0, a.k_total); }
+
+// K = 384 / 512 at H = 128 (the sampled blocks' [aggr_1 | aggr_2 | root] at d = 128) on the
+// split-once kernels as two column blocks, [0, 256) and [256, K): the forward's second launch
+// adds the first one's output rows (its own `add`, read before the same block stores them)
+// and applies the bias, activation and mask; the backward runs each block's dgrad / wgrad and
+// reduces its dW columns in place (db with the first).  Replaces the f32-input general kernels
+// there (51 / 65 us per launch at cfg5's ~17k rows).
+static bool xs_wide_ok(const LinArgs& a, bool vec) {
+  if (!vec || a.h != 128 || a.k_total <= 256 || a.k_total > 512 || a.k_total % 128 != 0)
+    return false;
+  for (int s = 0; s < a.n_seg; ++s)
+    if (a.seg[s].k % 16) return false;
+  return x6_enabled();
+}
+
+static int xs_fwd_wide(const LinArgs& a, hipStream_t stream) {
+  LinArgs A = a;
+  A.k_total = 256;
+  A.bias = nullptr;
+  A.relu = 0;
+  A.mask_out = nullptr;   // A.add: the caller's rows, if any
+  if (int rc = xs_linear_fwd(A, chunk_table_range(a, 0, 256), stream)) return rc;
+  LinArgs B = a;
+  B.k_total = a.k_total - 256;
+  B.w = a.w + 256;
+  B.add = a.out;
+  return xs_linear_fwd(B, chunk_table_range(a, 256, B.k_total), stream);
+}
+
+static int xs_bwd_wide(const LinArgs& a, float* dw, float* db, void* ws, size_t ws_bytes,
+                       hipStream_t stream) {
+  const bool wg = dw || db;
+  for (int part = 0; part < 2; ++part) {
+    const int c0 = part ? 256 : 0, kp = part ? a.k_total - 256 : 256;
+    LinArgs P = a;
+    P.k_total = kp;
+    P.w = a.w + c0;
+    P.dz_out = nullptr;
+    const ChunkTab tab = chunk_table_range(a, c0, kp);
+    bool pdx = false;
+    for (int c = 0; c < kp / 16; ++c) pdx |= tab.dx[c] != nullptr;
+    P.slab = nullptr;
+    if (wg) {
+      const size_t need = (size_t)xs_bwd_grid(a.n) * a.h * (kp + 1) * 4;
+      if (!ws || ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+      P.slab = static_cast<float*>(ws);
+    }
+    int G = 0;
+    if (pdx || wg) {
+      if (int rc = xs_linear_bwd(P, tab, pdx, &G, stream)) return rc;
+    }
+    if (wg) {
+      const int64_t total = (int64_t)a.h * (kp + 1);
+      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
+                         P.slab, (int64_t)G, a.h, kp + 1, dw ? dw + c0 : nullptr,
+                         part == 0 ? db : nullptr, a.k_total);
+      if (int rc = check_launch("k_wgrad_reduce")) return rc;
+    }
+  }
+  return HGNN_OK;
 }
 
 // every 8 consecutive 16-column chunks one 128-column segment (x_chunk<true>'s addressing)
@@ -1291,6 +1356,7 @@ static int fill_args(LinArgs& a, int32_t n_seg, const float* const* xs, const in
   }
   *vec = *vec && reinterpret_cast<uintptr_t>(w) % 16 == 0;
   a.w = w;
+  a.ldw = a.k_total;
   a.n = n_rows;
   a.h = h;
   return HGNN_OK;
@@ -1326,6 +1392,16 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     return fail(HGNN_E_ARG, "linear_fwd_mask: the bit mask needs relu, h %% 16 == 0, h <= 128 (h=%d)",
                 h);
   if (n_rows == 0) return HGNN_OK;
+  if (out && xs_wide_ok(a, vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                               reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&
+                               reinterpret_cast<uintptr_t>(add) % 16 == 0)) {
+    a.bias = bias;
+    a.add = add;
+    a.out = out;
+    a.relu = relu;
+    a.mask_out = mask;
+    return xs_fwd_wide(a, stream);
+  }
   if (mask && !(fwd4_ok(a, vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
                         reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&
                         reinterpret_cast<uintptr_t>(add) % 16 == 0))) {
@@ -1510,7 +1586,9 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     return hgnn_linear_bwd_ex(n_seg, xs, ks, n_rows, w, h, dz_out, nullptr, nullptr, dxs,
                               dx_accumulate, dw, db, nullptr, ws, ws_bytes, stream_);
   }
-  a.dz_out = dz_out;
+  a.dz_out = dz_out;   // (null on the wide split path: dz_out went through the streaming pass)
+  if (xs_wide_ok(a, vec) && (ws || !(dw || db)))
+    return xs_bwd_wide(a, dw, db, ws, ws_bytes, stream);
   if (fwd4_ok(a, vec)) {
     // fused two-role backward when W^T and two dz / X tiles fit the LDS; otherwise persistent
     // dgrad + wgrad-only (T = 32 tiles for K = 256)
@@ -1537,7 +1615,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       if (!wg) return HGNN_OK;
       const int64_t total = (int64_t)h * (K + 1);
       hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                         a.slab, (int64_t)G, h, K + 1, dw, db);
+                         a.slab, (int64_t)G, h, K + 1, dw, db, K);
       return check_launch("k_wgrad_reduce");
     }
     if (any_dx && !fused) {
@@ -1590,7 +1668,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
       if (int rc = check_launch("k_linear_wgrad_v5")) return rc;
       const int64_t total = (int64_t)h * (K + 1);
       hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                         a.slab, (int64_t)G, h, K + 1, dw, db);
+                         a.slab, (int64_t)G, h, K + 1, dw, db, K);
       return check_launch("k_wgrad_reduce");
     }
     const int T = v4_bwd_lds(h, K, fused, 64) <= 160 * 1024 ? 64 : 32;
@@ -1623,7 +1701,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     if (int rc = check_launch("k_linear_bwd_v4")) return rc;
     const int64_t total = (int64_t)h * (K + 1);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                       a.slab, (int64_t)G, h, K + 1, dw, db);
+                       a.slab, (int64_t)G, h, K + 1, dw, db, K);
     return check_launch("k_wgrad_reduce");
   }
   if (fast_path_ok(a, vec) && (dw || db) && ws) {
@@ -1650,7 +1728,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     if (int rc = check_launch("k_linear_bwd_lds")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                       a.slab, (int64_t)G, h, a.k_total + 1, dw, db);
+                       a.slab, (int64_t)G, h, a.k_total + 1, dw, db, a.k_total);
     return check_launch("k_wgrad_reduce");
   }
   if (any_dx) {
@@ -1679,7 +1757,7 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
     if (int rc = check_launch("k_linear_wgrad")) return rc;
     const int64_t total = (int64_t)h * (a.k_total + 1);
     hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                       a.slab, gx, h, a.k_total + 1, dw, db);
+                       a.slab, gx, h, a.k_total + 1, dw, db, a.k_total);
     if (int rc = check_launch("k_wgrad_reduce")) return rc;
   }
   return HGNN_OK;

@@ -23,6 +23,8 @@ struct LinArgs {
   int32_t n_seg;
   int32_t k_total;
   const float* w;
+  int32_t ldw;            // W row stride in floats: k_total, or the whole W's K for a column block
+                          // of it (the split kernels over K = 384 / 512 as two launches)
   const float* bias;
   const float* dout;
   const float* out_act;   // ReLU output for the backward mask (nullable)

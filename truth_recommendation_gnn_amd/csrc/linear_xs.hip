@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   bf16x8_t wa[KS][3];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const float4* p = reinterpret_cast<const float4*>(a.w + (int64_t)(16 * w + i) * K + 32 * s +
+    const float4* p = reinterpret_cast<const float4*>(a.w + (int64_t)(16 * w + i) * a.ldw + 32 * s +
                                                       8 * g);
     x6_split8(p[0], p[1], wa[s][0], wa[s][1], wa[s][2]);
   }
@@ -529,7 +529,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         float f[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          f[e] = a.w[(int64_t)(32 * s + 8 * g + e) * K + 16 * (w + 8 * u) + i];
+          f[e] = a.w[(int64_t)(32 * s + 8 * g + e) * a.ldw + 16 * (w + 8 * u) + i];
         x6_split8(make_float4(f[0], f[1], f[2], f[3]), make_float4(f[4], f[5], f[6], f[7]),
                   wt[u][s][0], wt[u][s][1], wt[u][s][2]);
       }
