@@ -478,7 +478,11 @@ __global__ void k_fill_i32(int32_t* p, int64_t n, int32_t v) {
 // kSortTile of 8192).  The planner still chooses 7 + 7 + 6 bits for the cfg4 negatives, which the
 // round-4 A/B on the 8192-item tile confirmed (scripts/gpu_sort_ab.sh).  17-bit post ids: 3 passes of 6 (339 us) beat 2 of 9 (381); 20-bit:
 // 3 of 7.  (10-bit digits, 2 passes for 19-20-bit ids, were measured slower than 3 passes of 8.)
-static void radix_plan(int64_t n_keys, int* passes, int* bits) {
+// Small sorts (fewer than kSmallSort pairs: a sampled block's transposes, ~0.1M edges) are
+// bound by their launches (count, scan, scatter per pass), not by the ranking: the fewest passes
+// of up to 10 bits (cfg5: 17-bit local ids in 2 passes instead of 3).
+constexpr int64_t kSmallSort = int64_t(1) << 20;
+static void radix_plan(int64_t n_keys, int64_t E, int* passes, int* bits) {
   int b = 0;
   while ((int64_t(1) << b) <= n_keys) ++b;   // keys in [0, n_keys] incl. sentinel
   static const int cost[10] = {0, 0, 0, 0, 0, 0, 108, 117, 147, 183};
@@ -486,6 +490,10 @@ static void radix_plan(int64_t n_keys, int* passes, int* bits) {
   for (int d = 6; d <= 9; ++d) {
     const int c = ((b + d - 1) / d) * cost[d];
     if (c < best_cost) best_cost = c, best = d;
+  }
+  if (E < kSmallSort) {
+    const int np = std::max(1, (b + 9) / 10);
+    best = std::max(6, std::min(10, (b + np - 1) / np));
   }
   *bits = best;
   *passes = (b + best - 1) / best;
@@ -529,7 +537,7 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
   int32_t* counts = w.take<int32_t>(nb * kMaxRadix + 1);
   int32_t* offs = w.take<int32_t>(nb * kMaxRadix + 1);
   int passes, bits;
-  radix_plan(n_keys, &passes, &bits);
+  radix_plan(n_keys, E, &passes, &bits);
   // the last pass takes only the bits left (>= 6: narrower digits measured no faster), e.g. 7 + 7
   // + 6 for 20-bit keys: fewer ranking ballots and longer runs per digit in its scatter
   int key_bits = 0;
