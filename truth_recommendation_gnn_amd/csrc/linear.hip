@@ -1270,9 +1270,9 @@ static ChunkTab chunk_table(const LinArgs& a) { return chunk_table_range(a, 0, a
 // K = 384 / 512 at H = 128 (the sampled blocks' [aggr_1 | aggr_2 | root] at d = 128) on the
 // split-once kernels as two column blocks, [0, 256) and [256, K): the forward's second launch
 // adds the first one's output rows (its own `add`, read before the same block stores them)
-// and applies the bias, activation and mask; the backward runs each block's dgrad / wgrad and
-// reduces its dW columns in place (db with the first).  Replaces the f32-input general kernels
-// there (51 / 65 us per launch at cfg5's ~17k rows).
+// and applies the bias, activation and mask; the backward runs each block's dgrad / wgrad into
+// its columns of one shared [G][h][K + 1] slab, reduced once.  Replaces the f32-input general
+// kernels there (51 / 65 us per launch at cfg5's ~17k rows).
 static bool xs_wide_ok(const LinArgs& a, bool vec) {
   if (!vec || a.h != 128 || a.k_total <= 256 || a.k_total > 512 || a.k_total % 128 != 0)
     return false;
@@ -1298,6 +1298,12 @@ static int xs_fwd_wide(const LinArgs& a, hipStream_t stream) {
 static int xs_bwd_wide(const LinArgs& a, float* dw, float* db, void* ws, size_t ws_bytes,
                        hipStream_t stream) {
   const bool wg = dw || db;
+  const int K = a.k_total;
+  int G = 0;
+  if (wg) {   // one slab [G][h][K + 1] for both column blocks, one reduce
+    const size_t need = (size_t)xs_bwd_grid(a.n) * a.h * (K + 1) * 4;
+    if (!ws || ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
+  }
   for (int part = 0; part < 2; ++part) {
     const int c0 = part ? 256 : 0, kp = part ? a.k_total - 256 : 256;
     LinArgs P = a;
@@ -1307,25 +1313,18 @@ static int xs_bwd_wide(const LinArgs& a, float* dw, float* db, void* ws, size_t 
     const ChunkTab tab = chunk_table_range(a, c0, kp);
     bool pdx = false;
     for (int c = 0; c < kp / 16; ++c) pdx |= tab.dx[c] != nullptr;
-    P.slab = nullptr;
-    if (wg) {
-      const size_t need = (size_t)xs_bwd_grid(a.n) * a.h * (kp + 1) * 4;
-      if (!ws || ws_bytes < need) return fail(HGNN_E_WS, "linear_bwd: workspace too small");
-      P.slab = static_cast<float*>(ws);
-    }
-    int G = 0;
+    P.slab = wg ? static_cast<float*>(ws) : nullptr;
+    P.slab_ld = K + 1;
+    P.slab_c0 = c0;
     if (pdx || wg) {
       if (int rc = xs_linear_bwd(P, tab, pdx, &G, stream)) return rc;
     }
-    if (wg) {
-      const int64_t total = (int64_t)a.h * (kp + 1);
-      hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
-                         P.slab, (int64_t)G, a.h, kp + 1, dw ? dw + c0 : nullptr,
-                         part == 0 ? db : nullptr, a.k_total);
-      if (int rc = check_launch("k_wgrad_reduce")) return rc;
-    }
   }
-  return HGNN_OK;
+  if (!wg) return HGNN_OK;
+  const int64_t total = (int64_t)a.h * (K + 1);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((unsigned)cdiv(total, 64)), dim3(1024), 0, stream,
+                     static_cast<const float*>(ws), (int64_t)G, a.h, K + 1, dw, db, K);
+  return check_launch("k_wgrad_reduce");
 }
 
 // every 8 consecutive 16-column chunks one 128-column segment (x_chunk<true>'s addressing)

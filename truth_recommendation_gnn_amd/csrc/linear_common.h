@@ -35,6 +35,8 @@ struct LinArgs {
   uint32_t dx_acc;        // backward: bit s set = segment s's dX is added into dx, not stored
   float* out;
   float* slab;            // wgrad partials [gx][h][k_total+1]
+  int32_t slab_ld;        // split kernels: the slab's row stride when > 0 ([gx][h][slab_ld], this
+  int32_t slab_c0;        // launch's dW columns at slab_c0.., db at slab_ld - 1), else k_total + 1
   int64_t n;
   int32_t h;
   int32_t relu;

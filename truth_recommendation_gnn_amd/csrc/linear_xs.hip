@@ -793,7 +793,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   loop(std::false_type{});
 #endif
   if constexpr (WG) {
-    constexpr int KEXT = K + 1;
+    // the slab row: [h][K + 1] of its own, or a column block of a shared [h][slab_ld] (the
+    // K = 384 / 512 column blocks, one reduce for both)
+    const int64_t KEXT = a.slab_ld > 0 ? a.slab_ld : K + 1;
+    const int c0 = a.slab_ld > 0 ? a.slab_c0 : 0;
+    const int64_t dbc = KEXT - 1;
     float* slab = a.slab + (int64_t)blockIdx.x * kH * KEXT;
 #pragma unroll
     for (int h = 0; h < 8; ++h)
@@ -801,7 +805,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       for (int u = 0; u < KT; ++u)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          slab[(int64_t)(16 * h + 4 * g + j) * KEXT + 16 * (KT * w + u) + i] =
+          slab[(int64_t)(16 * h + 4 * g + j) * KEXT + c0 + 16 * (KT * w + u) + i] =
               hw[h][u][j] + lw[h][u][j];
     // db: the 16 row groups' column partials, summed in a fixed order (the loop's last barrier
     // retired every plane read, so the planes hold the reduction)
@@ -816,10 +820,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
       const int c = 4 * threadIdx.x;
-      slab[(int64_t)(c + 0) * KEXT + K] = s.x;
-      slab[(int64_t)(c + 1) * KEXT + K] = s.y;
-      slab[(int64_t)(c + 2) * KEXT + K] = s.z;
-      slab[(int64_t)(c + 3) * KEXT + K] = s.w;
+      // (both column blocks write the same db partials: the same dz tiles in the same order)
+      slab[(int64_t)(c + 0) * KEXT + dbc] = s.x;
+      slab[(int64_t)(c + 1) * KEXT + dbc] = s.y;
+      slab[(int64_t)(c + 2) * KEXT + dbc] = s.z;
+      slab[(int64_t)(c + 3) * KEXT + dbc] = s.w;
     }
   }
 }
