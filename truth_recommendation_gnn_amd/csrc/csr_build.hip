@@ -261,7 +261,10 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
   return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
 }
 
-template <int BITS, bool HAS_B, int RR = kSortRounds, bool GEN = false>
+// SINGLE (E <= kSortTile, one tile): the tile's own digit starts are the global ones, so the pass
+// needs no count kernel and no scan — one launch per pass instead of three (the sampled blocks'
+// loss transposes of ~1k pairs inside the cfg5 replay).
+template <int BITS, bool HAS_B, int RR = kSortRounds, bool GEN = false, bool SINGLE = false>
 __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     const int32_t* keys_in, const int32_t* a_in, const int32_t* b_in, int64_t E, int shift,
     const int32_t* offs, int32_t* keys_out, int32_t* a_out, int32_t* b_out, int identity_a,
@@ -285,7 +288,7 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
     for (int w = 0; w < NW; ++w) wcount[w][dd] = 0;
-    gbase[dd] = offs[(int64_t)dd * gridDim.x + tile];
+    gbase[dd] = SINGLE ? 0 : offs[(int64_t)dd * gridDim.x + tile];
   }
   __syncthreads();
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -361,7 +364,8 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     for (int q = 0; q < DPT; ++q) {
       const int dd = threadIdx.x * DPT + q;
       if (dd < R) {
-        gbase[dd] -= run;   // the run's global start minus its tile start: one lookup per item
+        // the run's global start minus its tile start: one lookup per item (SINGLE: both equal)
+        if (!SINGLE) gbase[dd] -= run;
         int o = run;
         for (int w = 0; w < NW; ++w) {
           const int c = wcount[w][dd];
@@ -561,26 +565,37 @@ static int radix_sort_pairs(const int32_t* k_in, int32_t* ka, int64_t E, int64_t
     int32_t* bout = b_in ? (to_out ? b_out : tb) : nullptr;
     const int ident = (p == 0 && a_in == nullptr) ? 1 : 0;
     const bool g0 = p == 0 && gen.seed != nullptr;   // first pass: keys drawn, not loaded
+    const bool single = nb == 1;                     // one tile: no counts, no scan
 #define HGNN_COUNTS(BV)                                                                           \
   if (g0) hipLaunchKernelGGL((k_digit_counts<BV, kSortRounds, true>), dim3(nb), dim3(kSortThreads), \
                              0, stream, kin, E, shift, counts, gen);                              \
   else hipLaunchKernelGGL((k_digit_counts<BV>), dim3(nb), dim3(kSortThreads), 0, stream, kin, E,  \
                           shift, counts, KeyGen{nullptr, 0})
-    HGNN_BITS_SWITCH(pbits, HGNN_COUNTS)
+    if (!single) {
+      HGNN_BITS_SWITCH(pbits, HGNN_COUNTS)
+      if (int rc = check_launch("k_digit_counts")) return rc;
+      if (int rc = exclusive_scan_i32(counts, offs, pcount, scan_ws, &scan_b, stream)) return rc;
+    }
 #undef HGNN_COUNTS
-    if (int rc = check_launch("k_digit_counts")) return rc;
-    if (int rc = exclusive_scan_i32(counts, offs, pcount, scan_ws, &scan_b, stream)) return rc;
-#define HGNN_SCATTER(BV, HB)                                                                 \
-  hipLaunchKernelGGL((k_digit_scatter<BV, HB>), dim3(nb), dim3(kSortThreads), 0, stream, kin, ain, \
-                     bin, E, shift, offs, kout, aout, bout, ident)
+#define HGNN_SCATTER(BV, HB, SG)                                                              \
+  hipLaunchKernelGGL((k_digit_scatter<BV, HB, kSortRounds, false, SG>), dim3(nb),               \
+                     dim3(kSortThreads), 0, stream, kin, ain, bin, E, shift, offs, kout, aout,   \
+                     bout, ident)
+#define HGNN_SCATTER_G(BV, SG)                                                                \
+  hipLaunchKernelGGL((k_digit_scatter<BV, false, kSortRounds, true, SG>), dim3(nb),             \
+                     dim3(kSortThreads), 0, stream, kin, ain, bin, E, shift, offs, kout, aout,   \
+                     bout, ident, gen, gen_out)
 #define HGNN_SCATTER_B(BV)                                                                    \
   if (g0) {                                                                                   \
-    hipLaunchKernelGGL((k_digit_scatter<BV, false, kSortRounds, true>), dim3(nb),              \
-                       dim3(kSortThreads), 0, stream, kin, ain, bin, E, shift, offs, kout, aout, \
-                       bout, ident, gen, gen_out);                                            \
-  } else if (b_in) { HGNN_SCATTER(BV, true); } else { HGNN_SCATTER(BV, false); }
+    if (single) { HGNN_SCATTER_G(BV, true); } else { HGNN_SCATTER_G(BV, false); }             \
+  } else if (b_in) {                                                                          \
+    if (single) { HGNN_SCATTER(BV, true, true); } else { HGNN_SCATTER(BV, true, false); }     \
+  } else {                                                                                    \
+    if (single) { HGNN_SCATTER(BV, false, true); } else { HGNN_SCATTER(BV, false, false); }   \
+  }
     HGNN_BITS_SWITCH(pbits, HGNN_SCATTER_B)
 #undef HGNN_SCATTER_B
+#undef HGNN_SCATTER_G
 #undef HGNN_SCATTER
     if (int rc = check_launch("k_digit_scatter")) return rc;
     kin = kout;
