@@ -900,14 +900,18 @@ def test_weighted_rgcn_fused_loss_step_matches_golden():
         close(p.grad, z["grad:" + name])
 
 
+# digit plans (csr_build.hip radix_plan): under 2^20 pairs the fewest passes of up to 10 bits,
+# one-tile sorts (<= 8192 pairs) without count / scan kernels; larger sorts by the cost table
 @pytest.mark.parametrize("E,nk", [(100000, 70000),       # 17 bits: 2 passes of 9
-                                  (300000, 800000),      # 20 bits: 3 passes of 8
-                                  (200000, 300000),      # 19 bits: 3 passes of 8
-                                  (5000, 900),           # 10 bits: 2 passes of 8
+                                  (300000, 800000),      # 20 bits: 2 passes of 10
+                                  (200000, 300000),      # 19 bits: 2 passes of 10 (last 9)
+                                  (5000, 900),           # 10 bits: 1 pass, one tile
                                   (50000, 3_000_000),    # 22 bits: 3 passes of 8
-                                  (8192, 1000),          # exactly one onesweep tile
+                                  (8192, 1000),          # exactly one tile
+                                  (8000, 2**20 - 1),     # one tile, 20 bits: 2 passes of 10
+                                  (1, 5), (64, 3),       # one tile, a few items
                                   (8193, 100),           # one item in a second tile
-                                  (2_500_001, 100_000),  # 306 tiles of look-back, ragged tail
+                                  (2_500_001, 100_000),  # 17 bits by the cost table, ragged tail
                                   (2**26 + 3, 1_000_000),  # > 2^26 keys, two payloads
                                   (40000, -1)])          # every key equal: one digit holds all
 def test_sort_pairs_matches_numpy(E, nk):
