@@ -223,6 +223,69 @@ def cpu_baseline(cfg, threads=None, scale=None):
                       f"(per-edge work is scale-free, the sample's smaller tables favour the CPU)"}
 
 
+def cpu_baseline_sampled(lb, x_dict, rels, cfg, threads=None, steps=5, warmup=1):
+    """The cfg5 line's CPU baseline on the SAME sampled workload: one link
+    mini-batch's blocks as the GPU step ran them, copied to the host (the input rows of its
+    outermost block, each block's relations as local COO edge lists), then the oracle's step on
+    them — ``oracle/sage_ref.py``'s PyG op pattern per block (materialised ``index_select``,
+    ``scatter_reduce`` mean, ``addmm``; ``hetero_sage_blocks``), the reference's BCE link loss
+    over the batch's positive and negative pairs (``link_loss``, unit edge weights as the GPU
+    line's), backward, Adam.  edges/s = the batch's sampled message edges / the median step."""
+    from oracle import sage_ref
+    phys, allotted = host_cores()
+    threads = threads or allotted
+    torch.set_num_threads(threads)
+    mb = lb.mb
+    x_in = {t: x_dict[t].index_select(0, ids.long()).cpu() for t, ids in mb.nodes[0].items()}
+    blocks, n_edges = [], 0
+    for blk in mb.blocks:
+        eid = {}
+        for et, csr in blk.csr.items():
+            rp, col = csr.fwd.rowptr.long().cpu(), csr.fwd.col.long().cpu()
+            dst = torch.repeat_interleave(torch.arange(rp.numel() - 1), rp[1:] - rp[:-1])
+            eid[et] = torch.stack([col[:dst.numel()], dst])
+            n_edges += int(dst.numel())
+        blocks.append((eid, dict(blk.n_dst)))
+    names = []
+    for l in range(cfg.layers):
+        cin = cfg.dim if l == 0 else cfg.hidden
+        for et, _ in rels:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (cfg.hidden, cin)), (f"{p}.lin_l.bias", (cfg.hidden,)),
+                      (f"{p}.lin_r.weight", (cfg.hidden, cin))]
+    params = {k: v.requires_grad_() for k, v in sage_ref.init_params(names).items()}
+    opt = torch.optim.Adam(params.values(), lr=1e-3)
+    pos = torch.stack([lb.pu.long().cpu(), lb.pp.long().cpu()])
+    neg = lb.pn.long().cpu()
+    ones = torch.ones(pos.shape[1])
+
+    def step():
+        opt.zero_grad()
+        out = sage_ref.hetero_sage_blocks(params, x_in, blocks, rels)
+        loss = sage_ref.link_loss(out["user"], out["post"], pos, neg, ones)
+        loss.backward()
+        opt.step()
+
+    for _ in range(warmup):
+        step()
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t0)
+    dt = statistics.median(times)
+    return {"value": round(n_edges / dt, 1), "unit": "edges/s", "cores": threads,
+            "host_physical_cores": phys, "kind": "port",
+            "sample": (f"one sampled link mini-batch of the GPU line (the sampled blocks: "
+                       f"{', '.join(str(sum(1 for _ in b[0])) + ' relations' for b in blocks)}, "
+                       f"{n_edges} message edges, {pos.shape[1]} positive + {neg.numel()} negative "
+                       f"pairs, input rows {', '.join(f'{t} {v.shape[0]}' for t, v in x_in.items())}"
+                       f"), copied to the host: oracle/sage_ref.py hetero_sage_blocks + link_loss "
+                       f"+ backward + Adam, d=h={cfg.dim}; median of {steps} steps after "
+                       f"{warmup} warm-up ({dt * 1e3:.1f} ms/step), {threads} threads = the CPUs "
+                       f"allotted to this job (host has {phys} physical cores)")}
+
+
 # SURVEY §8d's CPU baseline for the full-batch configs: cfg2 / cfg3 whole, cfg4 (which needs
 # >100 GB per materialised [E, d] relation on the oracle) as a destination shard: the 1/8 shard
 # SURVEY §8d names (rank 0 of the 8-GPU split), the median of 3 timed steps after one warm-up,
@@ -594,18 +657,32 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     elapsed, loss = clock.time(step, args.steps)             # the headline: no events inside
     value = edges_step * args.steps / elapsed                 # edges_step is the global count
     # per-kernel HIP events: a separate run, so the headline carries none of their cost
-    kern, timer_ms = {}, None
-    if not on_cpu and not args.profile_steps and args.timer_steps > 0:
+    kern, timer_ms, dist_rec = {}, None, None
+    if not args.profile_steps and args.timer_steps > 0 and (sharded or not on_cpu):
         # one stream: a kernel's events around its launch then time that kernel alone (the
-        # negatives grouping, overlapped with the forward in the timed steps, runs in the loss)
+        # negatives grouping, overlapped with the forward in the timed steps, runs in the loss).
+        # N > 1: every collective's issue and its consumer's wait marked too (parallel.
+        # CollectiveTrace), so the line says which collective stalled which rank
         if not sharded:
             presort["on"] = False
-        timer = ops.KernelTimer()
+        timer = ops.KernelTimer() if not on_cpu else None
+        trace = parallel.CollectiveTrace(dev) if sharded else None
         ops.set_timer(timer)
-        t_el, _ = clock.time(step, args.timer_steps)
-        ops.set_timer(None)
-        kern = timer.summary()
+        parallel.set_collective_trace(trace)
+
+        def traced_step():
+            if trace is not None:
+                trace.begin_step()
+            return step()
+        try:
+            t_el, _ = clock.time(traced_step, args.timer_steps)
+        finally:
+            parallel.set_collective_trace(None)
+            ops.set_timer(None)
+        kern = timer.summary() if timer is not None else {}
         timer_ms = t_el / args.timer_steps * 1e3
+        if trace is not None:
+            dist_rec = _dist_summary(trace, kern, args.timer_steps, timer_ms, dev)
     # the reference's train() returns the global loss: sum the per-rank shares
     loss_t = loss.detach().to(torch.float64).reshape(1).clone()
     if sharded:
@@ -615,7 +692,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
     roof = _roofline(kern, cfg, world)
     if roof is not None and not on_cpu and not sharded:
         roof["one_pass"] = _one_pass_k1(g, cfg, roof)
-    proj = _projection(kern)
+    proj = _projection(kern, cfg.name)
     cpu = None
     if not args.no_cpu_baseline and world == 1 and not on_cpu and not sharded:
         if set(et for et, _ in rels) == {synth.ENGAGES, synth.REV_ENGAGES}:
@@ -640,7 +717,7 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
                    "parallelism": (f"dst-partitioned x{world} (user shards + post-table slices: "
                                    "RCCL reduce-scatter / all-gather per layer)"
                                    if sharded else "single")},
-        "roofline": roof, "projection": proj, "cpu_baseline": cpu,
+        "roofline": roof, "projection": proj, "cpu_baseline": cpu, "dist": dist_rec,
         "kernel_timer": {"steps": args.timer_steps if kern else 0,
                          "ms_per_step": round(timer_ms, 3) if timer_ms else None,
                          "note": "per-kernel HIP events, separate run after the timed region, "
@@ -654,6 +731,56 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
         "loss": float(loss_t),
         "setup_s": round(setup_s, 1),
     }
+
+
+def _dist_summary(trace, kern, steps, step_ms, dev):
+    """The N > 1 line's collective record (every rank calls this: it all-reduces): per collective
+    position of the step, its op and buffer MB, the time from its issue to its consumer's wait
+    completing (min / max over ranks), the stall it caused the consumer (min / max), the compute
+    issued under it, and the buffer's delivery rate as the consumer saw it (a lower bound on the
+    link rate: MB / the slowest rank's issue-to-wait time); per rank the compute ms per step (the
+    per-kernel HIP events' sum; on the CPU rehearsal the step time minus the stalls) and the sum
+    of its stalls.  The emulation's ``collectives`` / ``link_timeline`` measured for real."""
+    rows = trace.per_position()
+    M = torch.tensor([len(rows)], dtype=torch.int64, device=dev)
+    m_min, m_max = M.clone(), M.clone()
+    dist.all_reduce(m_min, op=dist.ReduceOp.MIN)
+    dist.all_reduce(m_max, op=dist.ReduceOp.MAX)
+    M = int(m_min)
+    rows = rows[:M]
+    v = torch.tensor([[r.get("wait_ms", 0.0), r.get("stall_ms", 0.0), r.get("cover_ms", 0.0)]
+                      for r in rows] or [[0.0, 0.0, 0.0]], dtype=torch.float64, device=dev)
+    stall_sum = sum(r.get("stall_ms", 0.0) for r in rows)
+    compute = (sum(k["ms"] for k in kern.values()) / steps) if kern else step_ms - stall_sum
+    per_rank = torch.tensor([[compute, stall_sum, step_ms]], dtype=torch.float64, device=dev)
+    lo, hi = v.clone(), v.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    r_lo, r_hi = per_rank.clone(), per_rank.clone()
+    dist.all_reduce(r_lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(r_hi, op=dist.ReduceOp.MAX)
+    lo, hi, r_lo, r_hi = lo.tolist(), hi.tolist(), r_lo.tolist()[0], r_hi.tolist()[0]
+    colls = []
+    for j, r in enumerate(rows):
+        mb = r["bytes"] / 1e6
+        colls.append({"i": j, "op": r["op"], "MB": float(f"{mb:.4g}"),
+                      "wait_ms_min": round(lo[j][0], 4), "wait_ms_max": round(hi[j][0], 4),
+                      "stall_ms_min": round(lo[j][1], 4), "stall_ms_max": round(hi[j][1], 4),
+                      "cover_ms_min": round(lo[j][2], 4),
+                      "GBs": (float(f"{mb / 1e3 / (hi[j][0] * 1e-3):.4g}") if hi[j][0] > 0
+                              else None)})
+    return {"collectives_per_step": M, "positions_differ": bool(int(m_max) != M),
+            "collectives": colls,
+            "compute_ms_min": round(r_lo[0], 3), "compute_ms_max": round(r_hi[0], 3),
+            "stall_ms_min": round(r_lo[1], 3), "stall_ms_max": round(r_hi[1], 3),
+            "step_ms_min": round(r_lo[2], 3), "step_ms_max": round(r_hi[2], 3),
+            "steps": steps,
+            "compute_source": "per-kernel HIP events" if kern else "step time minus stalls",
+            "note": ("per collective position of UserShard.step + the weight all-reduce, means over "
+                     "the timer run's steps: wait = issue -> the consumer's wait done (cover + "
+                     "stall), stall = the consumer stream's wait beyond its own work, cover = the "
+                     "compute issued under it; GBs = the buffer MB / the slowest rank's wait (a "
+                     "lower bound on the link rate); stall_ms = per rank, the sum over the step")}
 
 
 def _pool_shapes(kern):
@@ -752,12 +879,36 @@ def _k3_roof(n, k, h, bytes_per_launch, x6):
     return hbm_ms, mfma_ms
 
 
-def _projection(kern):
-    """The dense projection (K3), the largest forward launch, against ITS OWN roof: the launch's
-    floor is max(HBM bytes / 8 TB/s, matrix-core time of the instructions it must issue) —
-    ``_k3_roof`` — and ``frac`` = floor / measured time (never above 1).  ``achieved`` and
-    ``peak`` are in fp32-GEMM TFLOP/s (2*N*K*H per launch): ``peak`` is the rate the launch
-    would reach at its floor."""
+def _pmc_k3(cfg_name, n, k, fwd=True):
+    """MFMA busy of the K3 launch from the newest committed K3 counter pass
+    (profiles/pmc_k3_<cfg>_r<round>.json, scripts/pmc_k3_xs.sh: SQ_VALU_MFMA_BUSY_CYCLES over
+    1024 SIMDs x the launch's GRBM_GUI_ACTIVE / 8), for the cfg4 step's 9M-row launches: the
+    K = 256 forward has no added rows, the K = 128 forward is the pre-projected one (+ add)."""
+    import glob
+    base = cfg_name.split("x")[0]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_k3_{base}_r[0-9]*.json")),
+                   key=lambda f: int(os.path.basename(f).rsplit("_r", 1)[1].split(".")[0]
+                                     .split("_")[0]))
+    files = [f for f in files if os.path.basename(f).rsplit("_r", 1)[1].split(".")[0].isdigit()]
+    if not files or n != 9_000_000 or k not in (128, 256) or not fwd:
+        return None, None
+    key = f"k_lin_fwd_xs<{k}, {'true' if k == 128 else 'false'}>"
+    with open(files[-1]) as f:
+        rec = json.load(f).get("kernels", {}).get(key)
+    if not rec or "mfma_util" not in rec:
+        return None, None
+    return rec["mfma_util"], f"profiles/{os.path.basename(files[-1])} {key}"
+
+
+def _projection(kern, cfg_name=""):
+    """The dense projection (K3), the largest forward launch, in fp32-GEMM-equivalent TFLOP/s
+    (2*N*K*H per launch).  ``peak`` / ``frac``: against the chip's dense bf16 MFMA peak, which
+    the fp32-exact bf16x6 split (6 bf16 products per fp32 product) turns into 2500 / 6 = 416.7
+    fp32-equivalent TF/s, so ``frac`` = ``bf16_mfma_frac`` = 6 x achieved / 2500.  ``mfma_util``:
+    the PMC matrix-pipe busy fraction of the same launch (committed K3 counter pass).
+    ``frac_of_floor``: the launch's own floor — max(HBM bytes / 8 TB/s, its MFMA instructions'
+    cycles at the peak clock), ``_k3_roof`` — over its time, with ``floor_rate`` the TF/s at
+    that floor.  The f32-input kernels read against the fp32 MFMA peak instead."""
     lin = {k: v for k, v in kern.items() if k.startswith("linear_fwd[") and v["flops"]}
     if not lin:
         return None
@@ -775,29 +926,38 @@ def _projection(kern):
     hbm_ms, mfma_ms = _k3_roof(n, k, h, per_bytes, x6)
     floor_ms = max(hbm_ms, mfma_ms)
     tfs = per_flops / (per_ms * 1e-3) / 1e12
+    peak = BF16_MFMA_PEAK_TFS / 6 if x6 else FP32_MFMA_PEAK_TFS
+    util, util_src = _pmc_k3(cfg_name, n, k) if x6 else (None, None)
     out = {"bound": "hbm" if hbm_ms >= mfma_ms else "mfma", "kernel": f"k_linear_fwd K3 {name}",
-           "achieved": round(tfs, 1), "peak": round(per_flops / (floor_ms * 1e-3) / 1e12, 1),
-           "unit": "TFLOP/s (fp32-GEMM equivalent)", "frac": round(floor_ms / per_ms, 4),
+           "achieved": round(tfs, 1), "peak": round(peak, 1),
+           "unit": "TFLOP/s (fp32-GEMM equivalent)", "frac": round(tfs / peak, 4),
+           "mfma_util": util, "mfma_util_source": util_src,
+           "frac_of_floor": round(floor_ms / per_ms, 4),
+           "floor_rate": round(per_flops / (floor_ms * 1e-3) / 1e12, 1),
            "floor_ms": {"hbm": round(hbm_ms, 4), "mfma": round(mfma_ms, 4)},
            "avg_launch_us": round(per_ms * 1e3, 1),
            "hbm_GB/s": round(per_bytes / (per_ms * 1e-3) / 1e9, 1),
-           "hbm_frac": round(per_bytes / (per_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "flops_per_launch": int(per_flops),
            "flops_formula": "2*N*K*H (K = sum of the input segments)",
            "bytes_per_launch": int(per_bytes),
            "bytes_formula": "4*N*(K+H) (inputs read once, output written once; + 4*N*H for an added "
                             "row block, + 16*N for the ReLU mask bits)"}
     if x6:
+        out["bf16_mfma_frac"] = round(6 * tfs / BF16_MFMA_PEAK_TFS, 4)
         out["method"] = ("bf16x6: fp32-exact 3-piece bf16 split, 6 v_mfma_f32_16x16x32_bf16 "
                          "products per fp32 product, f32 accumulate"
                          + (" (K > 256: two column-block launches, the second adding the "
                             "first's rows)" if k > 256 else ""))
+        out["peak_note"] = (f"peak = the dense bf16 MFMA peak {BF16_MFMA_PEAK_TFS:g} TF/s / 6 "
+                            "bf16 products per fp32 product; frac = bf16_mfma_frac = 6 x achieved "
+                            "/ 2500")
         out["floor_note"] = (f"mfma floor = 6*(N/16)*(H/16)*(K/32) MFMAs x {BF16_MFMA_CYCLES} "
                              f"cycles / {N_SIMDS} SIMDs at {MFMA_CLOCK_GHZ} GHz (the launches "
                              "measured ~1.85 GHz under load, DESIGN §5); hbm floor = bytes / "
                              "8 TB/s")
     else:
         out["method"] = "f32-input MFMA (v_mfma_f32_16x16x4_f32)"
+        out["peak_note"] = "peak = the dense fp32 MFMA peak"
     return out
 
 
@@ -988,9 +1148,10 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     kern = _pool_shapes(kern)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(cfg, args.cpu_threads, args.cpu_sample_scale)
-        cpu["sample"] = "full-batch " + cpu["sample"] + " (the oracle has no sampler: the " \
-                        "per-edge rate of the full-batch step is the CPU comparison)"
+        lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
+        if ev is not None:
+            ev.synchronize()
+        cpu = cpu_baseline_sampled(lb, g.x_dict, rels, cfg, args.cpu_threads)
     return {
         "metric": "edges/s (fwd+bwd) hetero message-passing",
         "value": round(edges / elapsed, 1), "unit": "edges/s", "n_gpus": world,
@@ -1020,7 +1181,8 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                                    "static-capacity blocks ") + "(sampler eager)")
                                  if captured is not None else "eager")
                    + (", next batch sampled on a side stream" if side is not None else "")},
-        "roofline": _roofline(kern, cfg, world, pooled=True), "projection": _projection(kern),
+        "roofline": _roofline(kern, cfg, world, pooled=True),
+        "projection": _projection(kern, cfg.name),
         "cpu_baseline": cpu,
         "kernels": _kernel_rows(kern, args.timer_steps, cfg.name, world),
         "loss": float(loss.detach()), "setup_s": round(setup_s, 1),

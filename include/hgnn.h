@@ -32,9 +32,6 @@ extern "C" {
 
 #define HGNN_MEAN 1        /* multiply each row sum by 1/deg (deg 0 -> 0) */
 #define HGNN_ACCUMULATE 2  /* out += result instead of out = result */
-#define HGNN_CACHED_LOADS 4 /* hgnn_score_gather2_ex: default-policy row loads even from a table
-                               above 1 GiB (a source-block pass reads a slice that L2 / the
-                               Infinity Cache reuse; nt loads are for one pass over the table) */
 
 #define HGNN_MAX_SEG 6     /* input segments of one fused linear */
 
@@ -156,7 +153,10 @@ int hgnn_scatter_mean_bwd(const float* grad_aggr, int64_t n_dst, const float* in
  * Replaces SAGEConv's lin_l/lin_r addmm plus WeightedRGCN's weighted sum + ReLU
  * (train_gnn.py:187-198):
  *   out[n, h] = act( sum_s xs[s][n, ks[s]] @ w[:, off_s:off_s+ks[s]]^T + bias )
- * w is [h, sum(ks)] row-major (torch Linear layout), act = ReLU when relu != 0. */
+ * w is [h, sum(ks)] row-major (torch Linear layout), act = ReLU when relu != 0.
+ * `out` should not alias an input segment: at h = 128 and sum(ks) = 384 / 512 the split kernels
+ * run as two column blocks that pass partial rows through `out`, and a call whose `out` overlaps
+ * an xs[s] (or `add`) range is routed to the general f32-input kernels instead. */
 int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* bias, int32_t relu, float* out,
                     hgnn_stream_t stream);
@@ -254,27 +254,6 @@ int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t
                        const int32_t* heavy_rows, const int32_t* heavy_first, int64_t n_heavy,
                        int64_t n_chunks, int32_t chunk, float* slab, float* out,
                        hgnn_stream_t stream);
-
-/* hgnn_score_gather2 as one pass of a source-blocked dP gather (the K1 source blocking of
- * hgnn_gather_reduce_scaled applied to the loss's dP, train_gnn.py:262,273): the positives are
- * block b's CSR (RelationCSR.blocks), the negatives' segment of row r is [rowbeg_n[r],
- * rowend_n[r]) (rowend_n NULL: up to rowbeg_n[r + 1]); flags HGNN_ACCUMULATE (out +=, passes
- * after the first) and HGNN_CACHED_LOADS. */
-int hgnn_score_gather2_ex(const float* x, int64_t n_x, const float* rowvec, int32_t d,
-                          const int32_t* rowptr, const int32_t* col, const int32_t* rowbeg_n,
-                          const int32_t* rowend_n, const int32_t* col_n, int64_t n_rows,
-                          const float* cscale, float inv_e, const int32_t* heavy_rows,
-                          const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
-                          int32_t chunk, float* slab, float* out, int32_t flags,
-                          hgnn_stream_t stream);
-
-/* bounds[t * n_rows + r] = the first position p of row r (rowptr/col, col ascending within each
- * row) with col[p] >= thresholds[t]: every row's sub-segment per source block, for the negatives
- * of a source-blocked dP gather (grouped by post with their users ascending: the stable sort of
- * user-grouped positions). */
-int hgnn_segment_bounds(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
-                        const int32_t* thresholds, int32_t n_thr, int32_t* bounds,
-                        hgnn_stream_t stream);
 
 /* ---- edge scoring + weighted BCE (train_gnn.py:259-281), fused with its gradient --------------
  * Positive edges grouped by user (rowptr_u/col_u = post ids); neg_u_order[k] = the negative post

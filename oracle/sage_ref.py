@@ -123,6 +123,29 @@ def hetero_sage(params: Mapping[str, torch.Tensor], x_dict: Mapping[str, torch.T
     return h
 
 
+def hetero_sage_blocks(params: Mapping[str, torch.Tensor], x_in: Mapping[str, torch.Tensor],
+                       blocks: Sequence[Tuple[Mapping[EdgeType, torch.Tensor], Mapping[str, int]]],
+                       relations: Sequence[Tuple[EdgeType, float]]) -> Dict[str, torch.Tensor]:
+    """``hetero_sage`` on sampled blocks (PyG NeighborLoader's layer-wise bipartite graphs):
+    block l is (local ``edge_index_dict``, ``n_dst`` per type); its destinations are the first
+    ``n_dst[t]`` of its source nodes of type ``t``, so the root term reads that prefix.  Types with
+    no relation into them keep that prefix unchanged."""
+    h = dict(x_in)
+    for layer, (eid, n_dst) in enumerate(blocks):
+        nxt = {}
+        for dst_t, nd in n_dst.items():
+            acc = None
+            for et, w in relations:
+                if et[2] != dst_t or et not in eid:
+                    continue
+                name = f"layers.{layer}.{'__'.join(et)}"
+                m = sage_conv(h[et[0]], h[dst_t][:nd], eid[et], *_conv_params(params, name))
+                acc = w * m if acc is None else acc + w * m
+            nxt[dst_t] = F.relu(acc) if acc is not None else h[dst_t][:nd]
+        h = nxt
+    return h
+
+
 def link_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,
               neg_p: torch.Tensor, pos_weights: torch.Tensor) -> torch.Tensor:
     """train_gnn.py:259-281.  ``pos_weights`` is the per-positive-edge interaction weight

@@ -4,6 +4,7 @@ with HGNN_LIB=libhgnn_<name>.so).  Objects of sources the flags do not touch are
 default build's.
 
   python scripts/build_variant.py NAME -DHGNN_FOO=1 [...] [--only linear_xs]"""
+import json
 import os
 import pathlib
 import subprocess
@@ -40,6 +41,11 @@ def main():
                         *map(str, objs)], capture_output=True, text=True)
     if r.returncode:
         raise SystemExit(r.stderr)
+    # the stamp _native checks before it loads this library through HGNN_LIB: the digest of the
+    # current sources with these flags, and the flags themselves
+    only_l = sorted(only) if only else None
+    B.stamp_path(out).write_text(B._digest(tuple(rest), only_l) + "\n" +
+                                 json.dumps({"extra": rest, "only": only_l}) + "\n")
     print(f"built {out}")
 
 

@@ -193,7 +193,6 @@ def main():
                       "cover_over_7links": None if cover is None else round(cover / t7, 2) if t7 else None})
     env.log = None
     print(json.dumps({"world": args.world, "rank": args.rank, "config": gcfg.name,
-                      "chunked_last_gather": parallel.CHUNKED_LAST_GATHER,
                       "chunk_group": parallel.CHUNK_GROUP, "chunk_first": parallel.CHUNK_FIRST,
                       "collectives": colls,
                       "link_timeline": timeline,

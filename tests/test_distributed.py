@@ -105,13 +105,13 @@ def test_sharded_step_with_other_partial_sum_splits(world, kind, split, monkeypa
     _run_and_check(world, kind, False)
 
 
-@pytest.mark.parametrize("mode,group", [("1", "2"), ("2", "2"), ("3", "3"), ("0", "2")])
-def test_sharded_step_with_other_last_gather_chunkings(mode, group, monkeypatch):
-    """The loss's post table as one all-gather (0), one dP launch per broadcast block (1), own /
-    below / above (2, round 3-4), or landing-order groups of 3 blocks (the default mode 3 takes
-    groups of 2): the same oracle step at world 4 (blocks split around the own one)."""
-    monkeypatch.setenv("HGNN_CHUNKED_GATHER", mode)      # read at import by the spawned ranks
-    monkeypatch.setenv("HGNN_CHUNK_GROUP", group)
+@pytest.mark.parametrize("group,first", [("1", "1"), ("3", "2")])
+def test_sharded_step_with_other_last_gather_chunkings(group, first, monkeypatch):
+    """The loss's dP gather over the broadcast blocks of the post table in landing-order groups
+    of other sizes (the default takes the own block, then groups of 2): the same oracle step at
+    world 4 (blocks split around the own one)."""
+    monkeypatch.setenv("HGNN_CHUNK_GROUP", group)        # read at import by the spawned ranks
+    monkeypatch.setenv("HGNN_CHUNK_FIRST", first)
     _run_and_check(4, "engage2", True)
 
 

@@ -787,61 +787,6 @@ def test_loss_dp_gather_in_row_blocks_is_bitwise_one_pass(neg_kind):
             assert torch.equal(x, y)
 
 
-def test_segment_bounds_matches_searchsorted():
-    """hgnn_segment_bounds: per row of a column-sorted CSR, the first position at or above each
-    threshold — numpy's searchsorted per row (empty rows, thresholds past every column)."""
-    from truth_recommendation_gnn_amd import _native as Nn
-    rng = np.random.default_rng(8)
-    n_rows, n_col = 777, 5000
-    deg = rng.integers(0, 40, n_rows)
-    deg[::50] = 0
-    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
-    col = np.concatenate([np.sort(rng.integers(0, n_col, k)) for k in deg]).astype(np.int32)
-    thr = np.array([1, 700, 2500, 2501, 4999, 5000, 9000], dtype=np.int32)
-    out = torch.full((len(thr) * n_rows,), -1, dtype=torch.int32, device=DEV)
-    d_rp, d_col, d_thr = (torch.from_numpy(v).to(DEV) for v in (rowptr, col, thr))
-    Nn.check(Nn.lib().hgnn_segment_bounds(Nn.ptr(d_rp), Nn.ptr(d_col), n_rows, Nn.ptr(d_thr),
-                                          len(thr), Nn.ptr(out), Nn.stream_ptr(torch.device(DEV))),
-             "hgnn_segment_bounds")
-    want = np.array([[rowptr[r] + np.searchsorted(col[rowptr[r]:rowptr[r + 1]], t)
-                      for r in range(n_rows)] for t in thr]).reshape(-1)
-    assert np.array_equal(out.cpu().numpy(), want)
-
-
-@pytest.mark.parametrize("B,cached", [(2, True), (5, True), (8, False), (64, True)])
-def test_loss_dp_gather_in_source_blocks_matches_one_pass(B, cached):
-    """The dP gather as B source-block passes over the user table (VERDICT r4 #3;
-    ops._score_gather2_blocked): the positives from the K1 blocks of the same relation, the
-    negatives per block by hgnn_segment_bounds, passes 2.. accumulating — dP equals the one-pass
-    gather up to fp32 reassociation (the sums are split by user block), and the loss and dU are
-    untouched.  Heavy (chunked) positive rows, blocks with no edge of a row, more blocks than
-    rows of some posts; nt and default-policy loads."""
-    rng = np.random.default_rng(23)
-    nu, npost, E, d = 6000, 2500, 300_000, 128
-    pos = torch.from_numpy(np.stack([rng.integers(0, nu, E),
-                                     synth._zipf_sample_np(rng, npost, E, 1.0)]).astype(np.int64)
-                           ).to(DEV)
-    U = torch.from_numpy(rng.standard_normal((nu, d)).astype(np.float32) * 0.3).to(DEV)
-    P = torch.from_numpy(rng.standard_normal((npost, d)).astype(np.float32) * 0.3).to(DEV)
-    cscale = torch.tensor(1.25, device=DEV)
-    neg = ops.draw_negatives(pos, npost, generator=torch.Generator(device=DEV).manual_seed(4))
-    csr = ops.relation_csr_for_loss(pos, nu, npost)
-    assert csr.fwd.plan.n_heavy >= 3
-    ref = ops.edge_bce_loss_raw(U, P, pos, neg, E, cscale)
-    keep = (ops.DP_BLOCKS, ops.DP_CACHED)
-    ops.DP_BLOCKS, ops.DP_CACHED = str(B), cached
-    try:
-        got = ops.edge_bce_loss_raw(U, P, pos, neg, E, cscale)
-    finally:
-        ops.DP_BLOCKS, ops.DP_CACHED = keep
-    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])   # loss, dU: same kernels
-    dp, dp_ref = got[2], ref[2]
-    scale = float(dp_ref.abs().max())
-    err = float((dp - dp_ref).abs().max()) / scale
-    assert err < 1e-5, err
-    assert not torch.equal(dp, dp_ref) or B == 1      # it really ran blocked (reassociated)
-
-
 @pytest.mark.parametrize("nu,npost,E,d", [(3000, 1 << 20, 70_001, 128), (500, 37, 9_000, 64),
                                            (10, 5, 0, 16)])
 def test_edge_score_draw_entry_equals_materialised_draws(nu, npost, E, d):

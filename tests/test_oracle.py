@@ -135,3 +135,35 @@ def test_synth_schema_and_determinism():
     c = synth.make_graph(synth.scaled("cfg2", 0.001))
     deg = torch.bincount(c.edge_index_dict[synth.ENGAGES][1], minlength=c.num_posts)
     assert int(deg.max()) > 5 * float(deg.float().mean()) and int(deg.sum()) == 20000
+
+
+def test_hetero_sage_blocks_full_fanout_equals_full_graph():
+    """oracle.sage_ref.hetero_sage_blocks (the cfg5 CPU baseline's step on sampled blocks): with
+    every node a destination and every edge in the block — what full fan-out sampling gives —
+    each layer is hetero_sage's layer on the whole graph; with the destinations a prefix of the
+    sources, the rows past the prefix do not reach the output."""
+    g = torch.Generator().manual_seed(5)
+    nu, npo, d = 40, 15, 8
+    x = {"user": torch.randn(nu, d, generator=g), "post": torch.randn(npo, d, generator=g)}
+    e = torch.stack([torch.randint(0, nu, (120,), generator=g),
+                     torch.randint(0, npo, (120,), generator=g)])
+    eid = {("user", "engages", "post"): e, ("post", "rev_engages", "user"): e.flip(0)}
+    rels = [(("post", "rev_engages", "user"), 1.0), (("user", "engages", "post"), 1.0)]
+    names = []
+    for l in range(2):
+        for et, _ in rels:
+            p = f"layers.{l}.{'__'.join(et)}"
+            names += [(f"{p}.lin_l.weight", (d, d)), (f"{p}.lin_l.bias", (d,)),
+                      (f"{p}.lin_r.weight", (d, d))]
+    params = sage_ref.init_params(names)
+    ref = sage_ref.hetero_sage(params, x, eid, rels, 2)
+    n_all = {"user": nu, "post": npo}
+    got = sage_ref.hetero_sage_blocks(params, x, [(eid, n_all), (eid, n_all)], rels)
+    for t in ref:
+        assert torch.allclose(got[t], ref[t], atol=1e-6)
+    # destinations a prefix: the last block keeps only the first rows, whose values are the same
+    keep = {"user": 7, "post": 3}
+    sub = {et: ei[:, ei[1] < keep[et[2]]] for et, ei in eid.items()}
+    got2 = sage_ref.hetero_sage_blocks(params, x, [(eid, n_all), (sub, keep)], rels)
+    for t in ref:
+        assert torch.allclose(got2[t], ref[t][:keep[t]], atol=1e-6)

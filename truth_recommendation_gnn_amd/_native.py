@@ -14,14 +14,14 @@ from typing import Optional, Sequence
 import torch
 
 LIB_PATH = pathlib.Path(__file__).resolve().parent / "lib" / "libhgnn.so"
-# A/B measurement of two builds of the same library (scripts/*_bench.py): HGNN_LIB names another
-# in-tree build under lib/ (e.g. libhgnn_old.so); never a path outside the package.
+# A/B measurement of two builds of the same sources (scripts/build_variant.py): HGNN_LIB names
+# another in-tree build under lib/ (libhgnn_<name>.so); never a path outside the package, and
+# never a library whose build stamp does not match this tree's sources (build.check_library).
 if os.environ.get("HGNN_LIB"):
     LIB_PATH = LIB_PATH.parent / pathlib.Path(os.environ["HGNN_LIB"]).name
 
 HGNN_MEAN = 1
 HGNN_ACCUMULATE = 2
-HGNN_CACHED_LOADS = 4
 MAX_SEG = 6
 
 _c_i32, _c_i64, _c_sz, _p = ctypes.c_int32, ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p
@@ -70,10 +70,6 @@ _SIGS = {
                                    _c_i32, _p]),
     "hgnn_score_gather2": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _c_i64, _p,
                                     ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
-    "hgnn_score_gather2_ex": (_c_i32, [_p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _c_i64, _p,
-                                       ctypes.c_float, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p,
-                                       _c_i32, _p]),
-    "hgnn_segment_bounds": (_c_i32, [_p, _p, _c_i64, _p, _c_i32, _p, _p]),
     "hgnn_sample_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_hop_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_sample_hop_count": (_c_i32, [_c_i32, _p, _p, _p, _p, _c_i32, _p, _p, _p, _c_sz, _p]),
@@ -141,6 +137,11 @@ def lib() -> ctypes.CDLL:
         if not LIB_PATH.exists():
             raise NativeError(f"hgnn native library not found at {LIB_PATH}; build it with "
                               "`python -m truth_recommendation_gnn_amd.build` (no CPU fallback)")
+        from . import build as _build
+        try:
+            _build.check_library(LIB_PATH)
+        except RuntimeError as e:
+            raise NativeError(str(e)) from None
         l = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in _SIGS.items():
             fn = getattr(l, name, None)

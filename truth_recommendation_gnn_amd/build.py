@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import hashlib
+import json
 import os
 import pathlib
 import subprocess
@@ -32,7 +33,9 @@ def _sources():
     return sorted(CSRC.glob("*.hip"))
 
 
-def _digest() -> str:
+def _digest(extra=(), only=None) -> str:
+    """Hash of the sources and the flags they are built with.  ``extra`` / ``only``: the added
+    flags of an A/B variant build (scripts/build_variant.py) and the sources they apply to."""
     h = hashlib.sha256()
     for p in _sources() + sorted(CSRC.glob("*.h")) + [INCLUDE / "hgnn.h"]:
         h.update(p.name.encode())
@@ -41,7 +44,32 @@ def _digest() -> str:
     # must hash the same, or the shipped library would be rebuilt there
     h.update(" ".join(f for f in FLAGS if not f.startswith("-I")).encode())
     h.update(repr(sorted(FILE_FLAGS.items())).encode())
+    if extra:
+        h.update(repr((list(extra), sorted(only) if only else None)).encode())
     return h.hexdigest()[:16]
+
+
+def stamp_path(lib: pathlib.Path) -> pathlib.Path:
+    return lib.with_name(lib.name[:-len(".so")] + ".digest")
+
+
+def check_library(lib: pathlib.Path) -> None:
+    """Refuse a library not built from the sources in this tree: its stamp (written by
+    ``build()`` or scripts/build_variant.py beside it) must hold the digest of the current
+    sources and of the flags it records."""
+    st = stamp_path(lib)
+    if not st.exists():
+        raise RuntimeError(f"{lib.name}: no build stamp {st.name}; rebuild with "
+                           "`python -m truth_recommendation_gnn_amd.build`")
+    lines = st.read_text().splitlines()
+    extra, only = (), None
+    if len(lines) > 1 and lines[1].strip():
+        rec = json.loads(lines[1])
+        extra, only = tuple(rec["extra"]), rec.get("only")
+    want = _digest(extra, only)
+    if not lines or lines[0].strip() != want:
+        raise RuntimeError(f"{lib.name} was built from other sources (stamp "
+                           f"{lines[0].strip() if lines else '?'}, tree {want}); rebuild it")
 
 
 def build(force: bool = False, verbose: bool = True) -> pathlib.Path:
@@ -50,7 +78,7 @@ def build(force: bool = False, verbose: bool = True) -> pathlib.Path:
     Skips the work when the sources' digest matches the one recorded beside the library.
     """
     LIBDIR.mkdir(exist_ok=True)
-    stamp = LIBDIR / "libhgnn.digest"
+    stamp = stamp_path(LIB)
     dig = _digest()
     if not force and LIB.exists() and stamp.exists() and stamp.read_text().strip() == dig:
         return LIB

@@ -160,12 +160,6 @@ constexpr int kSortThreads = HGNN_SORT_THREADS;
 constexpr int kSortRounds = HGNN_SORT_ROUNDS;             // one item per thread per round
 constexpr int kSortTile = kSortThreads * kSortRounds;     // 8192 items per block
 constexpr int kMaxRadix = 1024;
-#ifndef HGNN_SORT_KV64
-#define HGNN_SORT_KV64 0
-#endif
-#ifndef HGNN_SORT_LANE_HIST
-#define HGNN_SORT_LANE_HIST 0
-#endif
 
 // key32 = key if both endpoints valid, else n_keys (sentinel sorts last); counts invalid edges.
 __global__ void __launch_bounds__(256) k_prepare_keys(const int64_t* key, const int64_t* other,
@@ -194,24 +188,16 @@ struct KeyGen {
 
 __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb);
 
-// The tile histogram is one counter per (digit, lane mod 32): lane l of a wave adds to word
-// digit * 32 + (l & 31), so the 32 lanes of an LDS lane group always hit 32 different banks
-// (a plain hist[digit] put every lane with the same digit on one address: 5-8 conflict cycles
-// per atomic in round 4's PMC census).  Each digit's 32 counters are summed at the end, thread d
-// reading them rotated by d so that a wave's reads spread over the banks too.
+// One LDS counter per digit.  (Measured and not kept, round 5: one counter per (digit, lane
+// mod 32), conflict-free — count conflicts 4.7 -> 0 per LDS instruction, the cfg4 draw + sort
+// 2.862 -> 2.888 ms; the conflicts are ~1 % of the kernel's wave-cycles)
 template <int BITS, int RR = kSortRounds, bool GEN = false>
 __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* keys, int64_t E,
                                                                int shift, int32_t* counts,
                                                                KeyGen gen = KeyGen{nullptr, 0}) {
   constexpr int R = 1 << BITS;
-#if HGNN_SORT_LANE_HIST
-  __shared__ int hist[R * 32];
-  for (int dd = threadIdx.x; dd < R * 32; dd += kSortThreads) hist[dd] = 0;
-  const int slot = threadIdx.x & 31;
-#else
   __shared__ int hist[R];
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads) hist[dd] = 0;
-#endif
   // XCD-aware tile order as in k_digit_scatter: neighbouring tiles' count words (one line holds
   // 16 tiles' counts of a digit) are written from one XCD's L2 instead of eight
   const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -224,25 +210,12 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_counts(const int32_t* ke
     k[r] = i < E ? (GEN ? uniform_draw(seed, i, gen.hi) : keys[i]) : -1;
   }
   __syncthreads();
-#if HGNN_SORT_LANE_HIST
-#pragma unroll
-  for (int r = 0; r < RR; ++r)
-    if (k[r] >= 0) atomicAdd(&hist[((k[r] >> shift) & (R - 1)) * 32 + slot], 1);
-  __syncthreads();
-  for (int dd = threadIdx.x; dd < R; dd += kSortThreads) {
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) c += hist[dd * 32 + ((j + dd) & 31)];
-    counts[(int64_t)dd * gridDim.x + tile] = c;
-  }
-#else
 #pragma unroll
   for (int r = 0; r < RR; ++r)
     if (k[r] >= 0) atomicAdd(&hist[(k[r] >> shift) & (R - 1)], 1);
   __syncthreads();
   for (int dd = threadIdx.x; dd < R; dd += kSortThreads)
     counts[(int64_t)dd * gridDim.x + tile] = hist[dd];
-#endif
 }
 
 // Stable scatter, block-local sort first.  Tile = kSortTile items; wave w owns the contiguous
@@ -276,13 +249,10 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
   __shared__ int wcount[NW][R];                  // running count -> wave offset within tile
   __shared__ int gbase[R];                       // global start of this tile's digit run, then
                                                  // minus its tile-local start
-#if HGNN_SORT_KV64
-  // key and payload a side by side: one ds_write_b64 / ds_read_b64 per item instead of two b32
-  __shared__ int2 skv[TILE];
-#else
+  // (Measured and not kept, round 5: key and payload as one 8-B LDS word — reorder conflicts
+  // 2.32 -> 2.12 per instruction, the cfg4 draw + sort 2.862 -> 2.866 ms.)
   __shared__ int skey[TILE];
   __shared__ int sa[TILE];
-#endif
   __shared__ int sb[HAS_B ? TILE : 1];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = xcd_tile(blockIdx.x, gridDim.x);
@@ -382,32 +352,19 @@ __global__ void __launch_bounds__(kSortThreads) k_digit_scatter(
     if (rank[r] >= 0) {
       const int digit = (key[r] >> shift) & (R - 1);
       const int pos = wcount[wid][digit] + rank[r];
-#if HGNN_SORT_KV64
-      skv[pos] = make_int2(key[r], va[r]);
-#else
       skey[pos] = key[r];
       sa[pos] = va[r];
-#endif
       if (HAS_B) sb[pos] = vb[r];
     }
   }
   __syncthreads();
   const int n_tile = (int)min<int64_t>(TILE, E - tile0);
   for (int j = threadIdx.x; j < n_tile; j += kSortThreads) {
-#if HGNN_SORT_KV64
-    const int2 kv = skv[j];
-    const int k = kv.x;
-#else
     const int k = skey[j];
-#endif
     const int digit = (k >> shift) & (R - 1);
     const int64_t pos = (int64_t)gbase[digit] + j;
     keys_out[pos] = k;
-#if HGNN_SORT_KV64
-    a_out[pos] = kv.y;
-#else
     a_out[pos] = sa[j];
-#endif
     if (HAS_B) b_out[pos] = sb[j];
   }
 }

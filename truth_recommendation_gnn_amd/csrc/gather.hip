@@ -49,10 +49,6 @@ struct GatherArgs {
   int32_t nt_load;             // rows gathered with nt loads (score gathers over multi-GB tables)
   int32_t nt_store;            // output rows stored with nt stores
   const int32_t* col2;
-  // hgnn_score_gather2_ex: the second list's segment of row r is [rowptr2[r], rowend2[r]) when
-  // set (one source-block pass of a list sorted by column within each row), else up to
-  // rowptr2[r + 1]
-  const int32_t* rowend2;
 };
 
 // Sum of row segment [beg, end) of `col` into acc (per lane: VPL vectors of width W; each slot of
@@ -181,8 +177,7 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
   }
   if (own) segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, a.col, a.score, beg, end, rv, acc);
   if (two && !partial)
-    segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, a.col2, 2, a.rowptr2[row],
-                                                a.rowend2 ? a.rowend2[row] : a.rowptr2[row + 1],
+    segment_sum<LPR, VPL, W, UNROLL, HAS_W, SC>(a, a.col2, 2, a.rowptr2[row], a.rowptr2[row + 1],
                                                 rv, acc);
   slot_combine<LPR, VPL, W>(acc);
   if (!writer) return;
@@ -257,22 +252,15 @@ __global__ void __launch_bounds__(256) k_fixup(const GatherArgs a) {
   }
 }
 
-// HGNN_GATHER_LDS (a measurement build, scripts/fuse_occupancy_probe.py): dynamic LDS per block
-// that caps the waves per CU, to time the gather at the occupancy a kernel fused with K3 would have
-#ifndef HGNN_GATHER_LDS
-#define HGNN_GATHER_LDS 0
-#endif
-
 template <int LPR, int VPL, int W, int UNROLL>
 static int launch_gather(const GatherArgs& a, bool has_w, hipStream_t stream) {
   const dim3 grid((unsigned)cdiv(a.n_items, 4)), block(256);
-  constexpr unsigned lds = HGNN_GATHER_LDS;
   if (a.score)
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false, true>), grid, block, lds, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false, true>), grid, block, 0, stream, a);
   else if (has_w)
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, lds, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, true>), grid, block, 0, stream, a);
   else
-    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, lds, stream, a);
+    hipLaunchKernelGGL((k_gather<LPR, VPL, W, UNROLL, false>), grid, block, 0, stream, a);
   return check_launch("k_gather");
 }
 
@@ -344,25 +332,6 @@ static int run_gather(GatherArgs a, hipStream_t stream) {
   return HGNN_OK;
 }
 
-// bounds[t * n_rows + r] = first position p in [rowptr[r], rowptr[r+1]) with col[p] >= thr[t]
-// (col ascending within every row): row r's sub-segments between consecutive thresholds.  One
-// thread per (row, threshold), a binary search over the row.
-__global__ void __launch_bounds__(256) k_segment_bounds(const int32_t* rowptr, const int32_t* col,
-                                                        int64_t n_rows, const int32_t* thr,
-                                                        int32_t n_thr, int32_t* bounds) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_rows * n_thr) return;
-  const int64_t t = i / n_rows, r = i % n_rows;
-  const int32_t v = thr[t];
-  int64_t lo = rowptr[r], hi = rowptr[r + 1];
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (col[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  bounds[i] = (int32_t)lo;
-}
-
 }  // namespace hgnn
 
 using namespace hgnn;
@@ -422,17 +391,6 @@ int hgnn_scatter_mean_bwd(const float* grad_aggr, int64_t n_dst, const float* in
                             n_chunks, chunk, slab, grad_x_src, stream);
 }
 
-int hgnn_segment_bounds(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
-                        const int32_t* thresholds, int32_t n_thr, int32_t* bounds,
-                        hgnn_stream_t stream) {
-  if (n_rows < 0 || n_thr < 0) return fail(HGNN_E_ARG, "segment_bounds: bad sizes");
-  if (n_rows == 0 || n_thr == 0) return HGNN_OK;
-  if (!rowptr || !thresholds || !bounds) return fail(HGNN_E_ARG, "segment_bounds: null pointer");
-  hipLaunchKernelGGL(k_segment_bounds, dim3((unsigned)cdiv(n_rows * n_thr, 256)), dim3(256), 0,
-                     as_stream(stream), rowptr, col, n_rows, thresholds, n_thr, bounds);
-  return check_launch("k_segment_bounds");
-}
-
 int hgnn_score_gather(const float* x, int64_t n_x, const float* rowvec, int32_t d,
                       const int32_t* rowptr, const int32_t* col, int64_t n_rows, int32_t mode,
                       const float* cscale, float inv_e, const int32_t* heavy_rows,
@@ -456,30 +414,15 @@ int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t
                        const int32_t* heavy_rows, const int32_t* heavy_first, int64_t n_heavy,
                        int64_t n_chunks, int32_t chunk, float* slab, float* out,
                        hgnn_stream_t stream) {
-  return hgnn_score_gather2_ex(x, n_x, rowvec, d, rowptr, col, rowptr_n, nullptr, col_n, n_rows,
-                               cscale, inv_e, heavy_rows, heavy_first, n_heavy, n_chunks, chunk,
-                               slab, out, 0, stream);
-}
-
-int hgnn_score_gather2_ex(const float* x, int64_t n_x, const float* rowvec, int32_t d,
-                          const int32_t* rowptr, const int32_t* col, const int32_t* rowbeg_n,
-                          const int32_t* rowend_n, const int32_t* col_n, int64_t n_rows,
-                          const float* cscale, float inv_e, const int32_t* heavy_rows,
-                          const int32_t* heavy_first, int64_t n_heavy, int64_t n_chunks,
-                          int32_t chunk, float* slab, float* out, int32_t flags,
-                          hgnn_stream_t stream) {
-  if (!rowbeg_n && n_rows > 0) return fail(HGNN_E_ARG, "score_gather2: rowptr_n is null");
-  if (flags & ~(HGNN_ACCUMULATE | HGNN_CACHED_LOADS))
-    return fail(HGNN_E_ARG, "score_gather2_ex: flags=%d", flags);
+  if (!rowptr_n && n_rows > 0) return fail(HGNN_E_ARG, "score_gather2: rowptr_n is null");
   GatherArgs a{};
   a.x = x; a.rowptr = rowptr; a.col = col;
   a.heavy_rows = heavy_rows; a.heavy_first = heavy_first; a.slab = slab; a.out = out;
   a.n_rows = n_rows; a.n_heavy = n_heavy; a.n_items = n_rows + (n_heavy > 0 ? n_chunks : 0);
-  a.d = d; a.chunk = chunk; a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+  a.d = d; a.chunk = chunk;
   a.rowvec = rowvec; a.cscale = cscale; a.inv_e = inv_e; a.score = 1;
-  a.rowptr2 = rowbeg_n; a.rowend2 = rowend_n; a.col2 = col_n;
+  a.rowptr2 = rowptr_n; a.col2 = col_n;
   nt_policy(a, n_x);
-  if (flags & HGNN_CACHED_LOADS) a.nt_load = 0;
   return run_gather(a, as_stream(stream));
 }
 

@@ -1281,6 +1281,21 @@ static bool xs_wide_ok(const LinArgs& a, bool vec) {
   return x6_enabled();
 }
 
+// The two column blocks pass the first one's partial rows through `out`, so out must not alias
+// an input segment (or `add`) on this path; such a call goes to the general kernels instead
+// (ADVICE r5).  Byte ranges of n rows each.
+static bool out_overlaps_inputs(const LinArgs& a) {
+  const uintptr_t o0 = reinterpret_cast<uintptr_t>(a.out);
+  const uintptr_t o1 = o0 + (uintptr_t)a.n * a.h * 4;
+  auto hit = [&](const void* p, int64_t row_floats) {
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(p), p1 = p0 + (uintptr_t)a.n * row_floats * 4;
+    return p && p0 < o1 && o0 < p1;
+  };
+  for (int s = 0; s < a.n_seg; ++s)
+    if (hit(a.seg[s].x, a.seg[s].k)) return true;
+  return hit(a.add, a.h);
+}
+
 static int xs_fwd_wide(const LinArgs& a, hipStream_t stream) {
   LinArgs A = a;
   A.k_total = 256;
@@ -1399,7 +1414,8 @@ int hgnn_linear_fwd_mask(int32_t n_seg, const float* const* xs, const int32_t* k
     a.out = out;
     a.relu = relu;
     a.mask_out = mask;
-    return xs_fwd_wide(a, stream);
+    if (!out_overlaps_inputs(a)) return xs_fwd_wide(a, stream);
+    a.bias = nullptr; a.add = nullptr; a.out = nullptr; a.relu = 0; a.mask_out = nullptr;
   }
   if (mask && !(fwd4_ok(a, vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
                         reinterpret_cast<uintptr_t>(bias) % 16 == 0 &&

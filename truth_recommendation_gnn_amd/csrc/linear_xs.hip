@@ -31,53 +31,8 @@
 #ifndef HGNN_XS_LDSPF_DXWG
 #define HGNN_XS_LDSPF_DXWG 1
 #endif
-#ifndef HGNN_XS_STAGGER
-#define HGNN_XS_STAGGER 1
-#endif
-#ifndef HGNN_XS_SPLITILP
-#define HGNN_XS_SPLITILP 0
-#endif
-#ifndef HGNN_XS_MASKMED
-#define HGNN_XS_MASKMED 1
-#endif
-// HGNN_XS_PROBE (timing probes only, wrong results): 1 = no HBM traffic in the forward (every
-// tile's loads hit the first R rows, no output stores); 2 = no MFMA sweep in the forward; 3 = as 1
-// with the stores kept; 4 = the loads kept, no stores
-#ifndef HGNN_XS_PROBE
-#define HGNN_XS_PROBE 0
-#endif
 
 namespace hgnn {
-
-// HGNN_XS_STAMPS (a diagnostic build only, scripts/k3_stamps.py): lane 0 of every wave of the
-// first 64 blocks records s_memtime at the phase boundaries of 8 loop iterations into a buffer
-// of its own, read back by hgnn_debug_xs_stamps; no output and no other code reads them.
-#ifndef HGNN_XS_STAMPS
-#define HGNN_XS_STAMPS 0
-#endif
-#if HGNN_XS_STAMPS
-constexpr int kStampBlocks = 64, kStampIters = 8, kStampFirst = 40, kStampPts = 12;
-__device__ unsigned long long g_xs_stamps[kStampBlocks * 8 * kStampIters * kStampPts];
-#define XS_STAMP(it, k)                                                                          \
-  do {                                                                                           \
-    if (blockIdx.x < kStampBlocks && (it) >= kStampFirst && (it) < kStampFirst + kStampIters) {   \
-      const unsigned long long ts_ = __builtin_amdgcn_s_memtime();                               \
-      if ((threadIdx.x & 63) == 0)                                                               \
-        g_xs_stamps[(((int)blockIdx.x * 8 + (int)(threadIdx.x >> 6)) * kStampIters +            \
-                     ((it) - kStampFirst)) * kStampPts + (k)] = ts_;                            \
-    }                                                                                            \
-  } while (0)
-// points 8 / 9: after an explicit wait for every outstanding memory operation right before the
-// late / early waves' split — how much of a split phase is waiting for its loads
-#define XS_WAIT_STAMP(it, k)                                                                     \
-  do {                                                                                           \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                            \
-    XS_STAMP(it, k);                                                                             \
-  } while (0)
-#else
-#define XS_STAMP(it, k) do { } while (0)
-#define XS_WAIT_STAMP(it, k) do { } while (0)
-#endif
 
 namespace {
 
@@ -92,30 +47,6 @@ __device__ __forceinline__ uint32_t clamp_row(int64_t row, int32_t last) {
 }
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
-// The three-piece split of N float4 at once, level by level (HGNN_XS_SPLITILP): every level's
-// converts, extracts and subtractions are independent across the 2N value pairs, where the
-// per-pair order chains ~11 dependent instructions (in-kernel stamps: a wave's split of 16
-// values took ~900 cycles for ~90 VALU).  pc[level][j][h]: the packed bf16 pair of level
-// `level` for values 2h, 2h+1 of float4 j — the words x6_split4 produces.
-template <int N>
-__device__ __forceinline__ void x6_split_levels(float (&v)[N][4], uint32_t (&pc)[3][N][2]) {
-#pragma unroll
-  for (int lv = 0; lv < 3; ++lv) {
-#pragma unroll
-    for (int j = 0; j < N; ++j)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) pc[lv][j][h] = x6_cvt_pk(v[j][2 * h], v[j][2 * h + 1]);
-    if (lv < 2) {
-#pragma unroll
-      for (int j = 0; j < N; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          v[j][2 * h] -= __uint_as_float(pc[lv][j][h] << 16);
-          v[j][2 * h + 1] -= __uint_as_float(pc[lv][j][h] & 0xffff0000u);
-        }
-    }
-  }
-}
 typedef uint32_t xs_u32x2 __attribute__((ext_vector_type(2)));
 
 // One [R x K] fp32 tile of the concatenated input, staged by all 512 threads: float4 j of thread
@@ -143,15 +74,13 @@ struct XStage {
   // kept: a uniform in-range test per tile taking one v_mad_u64_u32 and 64-bit adds for the row
   // addresses — fewer VALU, but 3.42 -> 3.46 ms at K = 256 forward, 3.55 -> 3.64 backward.)
   __device__ __forceinline__ void issue_one(Regs& x, int64_t r0, int32_t last, int j) const {
-    const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(row0 + j * RSTEP)
-                                                                    : clamp_row(r0 + row0 + j * RSTEP, last);
+    const uint32_t row = clamp_row(r0 + row0 + j * RSTEP, last);
     x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
   }
   __device__ __forceinline__ void issue(Regs& x, int64_t r0, int32_t last) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(row0 + j * RSTEP)
-                                              : clamp_row(r0 + row0 + j * RSTEP, last);
+      const uint32_t row = clamp_row(r0 + row0 + j * RSTEP, last);
       x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
     }
   }
@@ -161,29 +90,6 @@ struct XStage {
   template <int LDP, int PS, bool ZERO = false>
   __device__ __forceinline__ void put(const Regs& x, unsigned short* pl, int64_t r0,
                                       int64_t n = 0) const {
-#if HGNN_XS_SPLITILP
-    // the split level by level across all NL float4 (2 NL value pairs): each level's converts,
-    // extracts and subtractions are independent, where the per-pair order chained ~11
-    // dependent instructions (stamps: a wave's split took ~900 cycles for ~90 VALU)
-    float v[NL][4];
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      float4 u = x.v[j];
-      if (ZERO && r0 + row0 + j * RSTEP >= n) u = make_float4(0.f, 0.f, 0.f, 0.f);
-      v[j][0] = u.x; v[j][1] = u.y; v[j][2] = u.z; v[j][3] = u.w;
-    }
-    uint32_t pc[3][NL][2];
-    x6_split_levels<NL>(v, pc);
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      unsigned short* d = pl + (row0 + j * RSTEP) * LDP + col;
-#pragma unroll
-      for (int lv = 0; lv < 3; ++lv)
-        *reinterpret_cast<bf16x4_t*>(d + lv * PS) =
-            __builtin_bit_cast(bf16x4_t, (xs_u32x2){pc[lv][j][0], pc[lv][j][1]});
-    }
-    return;
-#endif
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       float4 v = x.v[j];
@@ -227,51 +133,31 @@ __device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int la
 // MFMA: A = W pieces (rows = output columns 16 w + i), B = X^T from the planes, so lane (i, g)
 // ends with columns 16 w + 4 g .. +3 of tile row 16 r + i: float4 stores; the ReLU mask words
 // (bit 4 c + e of word row * 4 + g) collect each wave's nibble through an LDS OR.
-// Per tile: [the previous tile's output stores] [this tile's added rows, the next tile's X]
-// [MFMA sweep] [epilogue into registers] [split of the next tile into the other buffer] [barrier].
+// Per tile: [MFMA sweep, with the iteration's memory instructions one or two per sweep step]
+// [epilogue into registers] [split of the next tile into the other buffer] [barrier].
 // Memory order matters because vmcnt is one in-order counter: a wait on an operation also waits
-// for everything issued before it.  The outputs are stored at the top of the NEXT iteration,
-// before its loads, and their registers are held until after that iteration's sweep: the
-// compiler waits for a store to read its data before it lets anything overwrite those registers,
-// and with the stores issued last (before the barrier) that wait landed at the loop head and
-// drained the prefetch with them.  The prefetch is unconditional (past the last tile the rows
-// clamp and the split goes to an unread buffer): a conditional issue made the waitcnt pass
-// assume loads in flight at the loop head and wait for everything there.  (Measured and not
-// kept: loads two tiles ahead in a second register set, the split interleaved into the sweep
-// — 3.84 vs 3.69 ms at 9M rows, K = 256; the kernel runs at a power-limited ~1.75 GHz, so
-// what counts is the instruction count, not the overlap.)
-// HGNN_XS_VMEM_STEP: the sweep step after which the iteration's memory instructions are issued
-// (-1: before the sweep).  In-kernel stamps (scripts/k3_stamps.py) showed each wave spending
-// ~600 cycles at the top of every iteration issuing them — all 8 waves queue ~48 KB of requests
-// on the CU's memory pipe right after the barrier — while its partner split: the matrix pipe sat
-// idle ~670 cycles per iteration.
-#ifndef HGNN_XS_VMEM_STEP
-#define HGNN_XS_VMEM_STEP -1
-#endif
-constexpr int kVmemStep = HGNN_XS_VMEM_STEP;
-#ifndef HGNN_XS_BIASINIT
-#define HGNN_XS_BIASINIT 0
-#endif
-constexpr bool kBiasInit = HGNN_XS_BIASINIT != 0;
-// HGNN_XS_VMEM_SPREAD (default on, round 5): the iteration's memory instructions one or two per
-// sweep step (the added rows first, then the previous tile's stores and mask words, then the
-// prefetch) instead of one burst after the barrier.  Probes (HGNN_XS_PROBE) put ~1 ms of the
-// K = 256 forward's 3.45 ms in its loads and stores (no HBM traffic: 2.52 ms; stores only 2.96;
-// loads only 3.12), and the stamps showed all 8 waves stalled ~600 cycles issuing them at once.
-// A/B at the cfg4 shapes: K = 128 + add 2.589 -> 2.512 ms, K = 128 (preprojection, 1M rows)
-// 0.219 -> 0.198, K = 256 unchanged (3.433 / 3.436).
-#ifndef HGNN_XS_VMEM_SPREAD
-#define HGNN_XS_VMEM_SPREAD 1
-#endif
-constexpr bool kSpread = HGNN_XS_VMEM_SPREAD != 0;
-// (Measured and not kept: the output tile staged in LDS and stored as whole rows, 1 KiB of
-// contiguous output per wave store instead of 16 rows x 64 B — K = 256 forward 3.46 -> 3.56 ms
-// with the spread, 3.50 in one burst.)
-
+// for everything issued before it.  The outputs are stored during the NEXT iteration's sweep, and
+// their registers are held until after it: the compiler waits for a store to read its data before
+// it lets anything overwrite those registers, and with the stores issued last (before the
+// barrier) that wait landed at the loop head and drained the prefetch with them.  The prefetch is
+// unconditional (past the last tile the rows clamp and the split goes to an unread buffer): a
+// conditional issue made the waitcnt pass assume loads in flight at the loop head and wait for
+// everything there.  For the same reason the stores inside the loop are unconditional: a tile
+// before a block's last is full (only tile n_tiles - 1 is partial, and it is some block's last),
+// and a store under a branch counts as maybe-not-issued, so the epilogue's wait for the added rows
+// had waited for every store as well (round 6).
+// The memory instructions spread over the sweep (round 5): in-kernel stamps (scripts/k3_stamps.py)
+// had shown all 8 waves queueing ~48 KB of requests on the CU's memory pipe right after the
+// barrier, ~600 cycles each, while the matrix pipe sat idle.  A/B at the cfg4 shapes: K = 128 +
+// add 2.589 -> 2.512 ms, K = 128 (preprojection, 1M rows) 0.219 -> 0.198, K = 256 unchanged.
+// Measured and not kept: a prefetch two tiles deep; the split interleaved into
+// the sweep; the burst issued at a later sweep step; the split level by level for ILP; the bias as
+// the accumulator's initial value; the output tile staged in LDS and stored as whole rows.
 template <int K, bool ADD>
 __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
                                                         int64_t n_tiles) {
   constexpr int R = K == 256 ? 32 : 64, KS = K / 32, RT = R / 16, LDP = K + 16, PS = R * LDP;
+  constexpr int NA = ADD ? RT : 0, NX = XStage<K, R>::NL;
   __shared__ __attribute__((aligned(16))) unsigned short pl[2][3 * PS];
   __shared__ uint32_t mk[2][R * 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -297,25 +183,17 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   float4 po[RT];   // the previous tile's output rows
 #pragma unroll
   for (int r = 0; r < RT; ++r) po[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto store_one = [&](int64_t tp, int r) {
+  // FULL: a tile before the block's last (every row < n), stored without a row test
+  auto store_one = [&](int64_t tp, int r, auto full_c) {
     const int64_t row = tp * R + 16 * r + i;
-    if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n)
+    if (decltype(full_c)::value || row < a.n)
       *reinterpret_cast<float4*>(a.out + row * kH + 16 * w + 4 * g) = po[r];
   };
-  auto mask_one = [&](int64_t tp, int bp) {
-    if (mask_out && threadIdx.x < R * 4) {
-      const int64_t row = tp * R + (threadIdx.x >> 2);
-      if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n)
-        a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
-      mk[bp][threadIdx.x] = 0u;
-    }
-  };
-  auto store_prev = [&](int64_t tp, int bp) {
-#pragma unroll
-    for (int r = 0; r < RT; ++r) store_one(tp, r);
+  auto mask_one = [&](int64_t tp, int bp, auto full_c) {
     if (mask_out && threadIdx.x < R * 4) {   // its mask words are complete (last barrier)
       const int64_t row = tp * R + (threadIdx.x >> 2);
-      if (HGNN_XS_PROBE != 1 && HGNN_XS_PROBE != 4 && row < a.n) a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
+      if (decltype(full_c)::value || row < a.n)
+        a.mask_out[tp * R * 4 + threadIdx.x] = mk[bp][threadIdx.x];
       mk[bp][threadIdx.x] = 0u;
     }
   };
@@ -337,66 +215,42 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   // SIMD (spills at K = 256 + add): too little for a second forward kernel.  Larger tiles (48
   // rows at K = 256, 80 at K = 128: fewer barriers and epilogue phases per MFMA) measured the
   // same (3.52 / 3.49 ms, 2.68 / 2.69 ms).
-  // (Measured and not kept: a prefetch two tiles deep in a second register set, with the added
-  // rows one tile ahead too — the 9M-row launches unchanged, 3.63 vs 3.66 ms at K = 256; round 5
-  // again for the early waves only, the loop unrolled by two so the sets alternate at compile
-  // time: 3.575 / 3.574 ms at K = 256, 2.614 / 2.613 at K = 128 + add.)
   auto loop = [&](auto late_c) {
     constexpr bool LATE = decltype(late_c)::value;
     if constexpr (LATE) xs.issue(xr, (t + G) * R, last);
     __syncthreads();
     int it = 0;
-    for (; t < n_tiles; t += G, ++it) {
+    // the first iteration peeled (FIRST: no previous tile to store), so the stores of every
+    // other iteration are unconditional and the compiler's waits count them
+    auto iter = [&](auto first_c) {
+      constexpr bool FIRST = decltype(first_c)::value;
       const int b = it & 1;
-      XS_STAMP(it, 0);
-      if constexpr (LATE) XS_WAIT_STAMP(it, 8);
       if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
-      XS_STAMP(it, 1);
-      // the iteration's memory instructions: the previous tile's output stores, this tile's
-      // added rows, the prefetch
-      auto vmem = [&]() {
-        if (it > 0) store_prev(t - G, b ^ 1);
-        if constexpr (ADD) {
-#pragma unroll
-          for (int r = 0; r < RT; ++r) {
-            const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3) ? (uint32_t)(16 * r + i)
-                                                    : clamp_row(t * R + 16 * r + i, last);
-            ad[r] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
-          }
-          __builtin_amdgcn_sched_barrier(0);   // issued before the prefetch: waited for alone
-        }
-        xs.issue(xr, (t + (LATE ? 2 : 1) * G) * R, last);
-        __builtin_amdgcn_sched_barrier(0);   // keep the loads ahead of what follows
-      };
-      // the same instructions spread over the sweep (HGNN_XS_VMEM_SPREAD): piece k at step
-      // k * NQ / NP — the added rows, the stores, the mask words, the prefetch
+      // the iteration's memory instructions, piece k at sweep step k * NQ / NP: the previous
+      // tile's mask words, this tile's added rows, the prefetch, the previous tile's stores
+      // (youngest: the waits for the added rows and the prefetch leave them in flight)
       auto vmem_step = [&](int q) {
-        constexpr int NA = ADD ? RT : 0, NX = XStage<K, R>::NL, NP = NA + RT + 1 + NX;
-        constexpr int NQ = RT * (K / 32);
+        constexpr int NP = 1 + NA + NX + RT, NQ = RT * KS;
 #pragma unroll
         for (int k = 0; k < NP; ++k) {
           if (k * NQ / NP != q) continue;
-          if (k < NA) {
+          if (k == 0) {
+            if constexpr (!FIRST) mask_one(t - G, b ^ 1, std::true_type{});
+          } else if (k < 1 + NA) {
             if constexpr (ADD) {
-              const uint32_t row = (HGNN_XS_PROBE == 1 || HGNN_XS_PROBE == 3)
-                                       ? (uint32_t)(16 * k + i)
-                                       : clamp_row(t * R + 16 * k + i, last);
-              ad[k] = *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
+              const uint32_t row = clamp_row(t * R + 16 * (k - 1) + i, last);
+              ad[k - 1] =
+                  *reinterpret_cast<const float4*>(a.add + (uint64_t)row * kH + 16 * w + 4 * g);
             }
-          } else if (k < NA + RT) {
-            if (it > 0) store_one(t - G, k - NA);
-          } else if (k == NA + RT) {
-            if (it > 0) mask_one(t - G, b ^ 1);
+          } else if (k < 1 + NA + NX) {
+            xs.issue_one(xr, (t + (LATE ? 2 : 1) * G) * R, last, k - 1 - NA);
           } else {
-            xs.issue_one(xr, (t + (LATE ? 2 : 1) * G) * R, last, k - NA - RT - 1);
+            if constexpr (!FIRST) store_one(t - G, k - 1 - NA - NX, std::true_type{});
           }
         }
       };
-      if constexpr (kVmemStep < 0 && !kSpread) vmem();
-      XS_STAMP(it, 2);
       const unsigned short* p = pl[b];
       f32x4 hi[RT], lo[RT];
-#if HGNN_XS_LDSPF
       // software-pipelined sweep: step q = (r, s) reads its three fragments LDSPF steps ahead,
       // pinned as [3 ds_read (step q + LDSPF)] [6 MFMA (step q)] by scheduling barriers (the
       // compiler otherwise issues each step's reads right before its MFMAs and waits on them)
@@ -411,9 +265,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         };
 #pragma unroll
         for (int r = 0; r < RT; ++r) {
-          // HGNN_XS_BIASINIT: the bias as the large-term accumulator's initial value (a GEMM
-          // with C = bias), not an add per element in the epilogue
-          hi[r] = kBiasInit ? f32x4{bb.x, bb.y, bb.z, bb.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+          hi[r] = f32x4{0.f, 0.f, 0.f, 0.f};
           lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
@@ -421,77 +273,47 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          if constexpr (kVmemStep >= 0) {
-            if (q == kVmemStep) vmem();   // after the sweep has the matrix pipe going
-          }
-          if constexpr (kSpread) vmem_step(q);
+          vmem_step(q);
           if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (HGNN_XS_PROBE != 2)
-            x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
-                   hi[q / KS], lo[q / KS]);
+          x6_mma(wa[q % KS], fr[q % (PF + 1)][0], fr[q % (PF + 1)][1], fr[q % (PF + 1)][2],
+                 hi[q / KS], lo[q / KS]);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else
-      static_assert(!kSpread, "HGNN_XS_VMEM_SPREAD needs HGNN_XS_LDSPF");
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        hi[r] = kBiasInit ? f32x4{bb.x, bb.y, bb.z, bb.w} : f32x4{0.f, 0.f, 0.f, 0.f};
-        lo[r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const bf16x8_t x1 = row8<LDP>(p, 16 * r, 32 * s, i, g);
-          const bf16x8_t x2 = row8<LDP>(p + PS, 16 * r, 32 * s, i, g);
-          const bf16x8_t x3 = row8<LDP>(p + 2 * PS, 16 * r, 32 * s, i, g);
-          x6_mma(wa[s], x1, x2, x3, hi[r], lo[r]);
-        }
-      }
-#endif
-      XS_STAMP(it, 3);
       // the stored rows' registers are reserved until here (see above)
 #pragma unroll
       for (int r = 0; r < RT; ++r)
         asm volatile("" ::"v"(po[r].x), "v"(po[r].y), "v"(po[r].z), "v"(po[r].w));
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
-        float4 v;
-        if constexpr (kBiasInit) {
-          v = make_float4(x6_out(hi[r][0], lo[r][0]), x6_out(hi[r][1], lo[r][1]),
-                          x6_out(hi[r][2], lo[r][2]), x6_out(hi[r][3], lo[r][3]));
-        } else {
-          v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
-                          x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
-        }
+        float4 v = make_float4(x6_out(hi[r][0], lo[r][0]) + bb.x, x6_out(hi[r][1], lo[r][1]) + bb.y,
+                               x6_out(hi[r][2], lo[r][2]) + bb.z, x6_out(hi[r][3], lo[r][3]) + bb.w);
         if constexpr (ADD) {
           v.x += ad[r].x; v.y += ad[r].y; v.z += ad[r].z; v.w += ad[r].w;
         }
         if (a.relu) v = relu4(v);
         po[r] = v;
-#if HGNN_XS_MASKMED
         if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_out_bits(v, 4 * w));
-#else
-        if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_bits(v, 4 * w));
-#endif
       }
-      XS_STAMP(it, 4);
-      if constexpr (!LATE) XS_WAIT_STAMP(it, 9);
       if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
-      XS_STAMP(it, 5);
       __syncthreads();
-      XS_STAMP(it, 6);
+    };
+    if (t < n_tiles) {
+      iter(std::true_type{});
+      t += G;
+      ++it;
     }
-    store_prev(t - G, (it - 1) & 1);
+    for (; t < n_tiles; t += G, ++it) iter(std::false_type{});
+#pragma unroll
+    for (int r = 0; r < RT; ++r) store_one(t - G, r, std::false_type{});
+    mask_one(t - G, (it - 1) & 1, std::false_type{});
   };
-#if HGNN_XS_STAGGER
   if (w >= 4) {
     loop(std::true_type{});
   } else {
     loop(std::false_type{});
   }
-#else
-  loop(std::false_type{});
-#endif
 }
 
 // ---------------------------------------------------------------- backward
@@ -554,10 +376,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     if constexpr (WG) xs.issue(xr, tt * R, last32);
   };
   float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto put = [&](int64_t tt, int b, int sit) {   // sit: the iteration for stamp 10 / 11, or -1
-#if HGNN_XS_SPLITILP
-    float zs[ZL][4];
-#endif
+  auto put = [&](int64_t tt, int b) {
 #pragma unroll
     for (int j = 0; j < ZL; ++j) {
       const int64_t row = tt * R + zr + 16 * j;
@@ -571,32 +390,14 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       if (row >= a.n) z = make_float4(0.f, 0.f, 0.f, 0.f);
       else if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + row * kH + zc) = z;
       dbacc.x += z.x; dbacc.y += z.y; dbacc.z += z.z; dbacc.w += z.w;
-#if HGNN_XS_SPLITILP
-      zs[j][0] = z.x; zs[j][1] = z.y; zs[j][2] = z.z; zs[j][3] = z.w;
-    }
-    {
-      uint32_t pc[3][ZL][2];
-      x6_split_levels<ZL>(zs, pc);
-#pragma unroll
-      for (int j = 0; j < ZL; ++j) {
-        unsigned short* d = zp[b] + (zr + 16 * j) * LDZ + zc;
-#pragma unroll
-        for (int lv = 0; lv < 3; ++lv)
-          *reinterpret_cast<bf16x4_t*>(d + lv * ZS) =
-              __builtin_bit_cast(bf16x4_t, (xs_u32x2){pc[lv][j][0], pc[lv][j][1]});
-      }
-#else
       bf16x4_t p1, p2, p3;
       x6_split4(z, p1, p2, p3);
       unsigned short* d = zp[b] + (zr + 16 * j) * LDZ + zc;
       *reinterpret_cast<bf16x4_t*>(d) = p1;
       *reinterpret_cast<bf16x4_t*>(d + ZS) = p2;
       *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
-#endif
     }
-    XS_STAMP(sit, 10);
     if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
-    XS_STAMP(sit, 11);
   };
   // (Measured and not kept: a uniform branch to a copy of the put without the per-row zeroing
   // on every tile but the last — within noise at the cfg4 shapes, and the K = 256 wgrad kernel
@@ -619,7 +420,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   }
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   issue(t);
-  put(t, 0, -1);
+  put(t, 0);
   // staggered halves as in the forward: waves 4-7 put the next tile first, then sweep
   auto loop = [&](auto late_c) {
     constexpr bool LATE = decltype(late_c)::value;
@@ -627,39 +428,29 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     __syncthreads();
     for (int it = 0; t < n_tiles; t += G, ++it) {
       const int b = it & 1;
-      XS_STAMP(it, 0);
-      if constexpr (LATE) XS_WAIT_STAMP(it, 8);
-      if constexpr (LATE) put(t + G, b ^ 1, it);
-      XS_STAMP(it, 1);
+      if constexpr (LATE) put(t + G, b ^ 1);
       // an accumulating dX reads what the rows hold first: issued before the prefetch, so its
       // wait leaves the prefetch in flight
       float4 dxo[DT][ACC ? R / 16 : 1];
-      auto vmem = [&]() {
-        if constexpr (ACC) {
+      if constexpr (ACC) {
 #pragma unroll
-          for (int u = 0; u < DT; ++u) {
-            if (dxp[u]) {
+        for (int u = 0; u < DT; ++u) {
+          if (dxp[u]) {
 #pragma unroll
-              for (int r = 0; r < R / 16; ++r)
-                dxo[u][r] = *reinterpret_cast<const float4*>(
-                    dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
-            }
+            for (int r = 0; r < R / 16; ++r)
+              dxo[u][r] = *reinterpret_cast<const float4*>(
+                  dxp[u] + (uint64_t)clamp_row(t * R + 16 * r + i, last32) * dxld[u] + 4 * g);
           }
-          __builtin_amdgcn_sched_barrier(0);
         }
-        issue(t + (LATE ? 2 : 1) * G);   // consumed by the next put(), unconditionally (see forward)
-        __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of what follows
-      };
-      // the memory instructions before the first sweep, or inside it (HGNN_XS_VMEM_STEP, see the
-      // forward): in the dgrad sweep when there is one, else in the wgrad sweep
-      if constexpr (kVmemStep < 0) vmem();
-      XS_STAMP(it, 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      issue(t + (LATE ? 2 : 1) * G);   // consumed by the next put(), unconditionally (see forward)
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of what follows
       const unsigned short* z = zp[b];
       f32x4 dh[DT][DX ? R / 16 : 1], dl[DT][DX ? R / 16 : 1];
-#if HGNN_XS_LDSPF
       // the sweeps software-pipelined as in the forward: each step's fragments are read PF
-      // steps ahead, pinned by scheduling barriers
-      // the fused dgrad + wgrad kernels are at the register limit: fewer fragments ahead there
+      // steps ahead, pinned by scheduling barriers; the fused dgrad + wgrad kernels are at the
+      // register limit: fewer fragments ahead there
       constexpr int PF = DX && WG ? (ACC ? 0 : HGNN_XS_LDSPF_DXWG) : HGNN_XS_LDSPF;
       if constexpr (DX) {
         constexpr int NQ = (R / 16) * HS;
@@ -679,9 +470,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-          if constexpr (kVmemStep >= 0) {
-            if (q == kVmemStep) vmem();
-          }
           if (q + PF < NQ) ld(q + PF, fr[(q + PF) % (PF + 1)]);
           __builtin_amdgcn_sched_barrier(0);
           const bf16x8_t(&f)[3] = fr[q % (PF + 1)];
@@ -691,7 +479,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-      XS_STAMP(it, 3);
       if constexpr (WG) {
         const unsigned short* x = xp[b];
         bf16x8_t xb[KT][3];
@@ -707,9 +494,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int h = 0; h < 8; ++h) {
-          if constexpr (kVmemStep >= 0 && !DX) {
-            if (h == (kVmemStep < 8 ? kVmemStep : 7)) vmem();
-          }
           if (h + PF < 8) {
 #pragma unroll
             for (int q = 0; q < 3; ++q)
@@ -722,40 +506,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
           __builtin_amdgcn_sched_barrier(0);
         }
       }
-#else
-      if constexpr (DX) {
-#pragma unroll
-        for (int r = 0; r < R / 16; ++r) {
-#pragma unroll
-          for (int u = 0; u < DT; ++u) dh[u][r] = dl[u][r] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < HS; ++s) {
-            const bf16x8_t x1 = row8<LDZ>(z, 16 * r, 32 * s, i, g);
-            const bf16x8_t x2 = row8<LDZ>(z + ZS, 16 * r, 32 * s, i, g);
-            const bf16x8_t x3 = row8<LDZ>(z + 2 * ZS, 16 * r, 32 * s, i, g);
-#pragma unroll
-            for (int u = 0; u < DT; ++u) x6_mma(wt[u][s], x1, x2, x3, dh[u][r], dl[u][r]);
-          }
-        }
-      }
-      if constexpr (WG) {
-        const unsigned short* x = xp[b];
-        bf16x8_t xb[KT][3];
-#pragma unroll
-        for (int u = 0; u < KT; ++u)
-#pragma unroll
-          for (int q = 0; q < 3; ++q) xb[u][q] = tr8<LDX>(x + q * XS, 16 * (KT * w + u), lane);
-#pragma unroll
-        for (int h = 0; h < 8; ++h) {
-          bf16x8_t za[3];
-#pragma unroll
-          for (int q = 0; q < 3; ++q) za[q] = tr8<LDZ>(z + q * ZS, 16 * h, lane);
-#pragma unroll
-          for (int u = 0; u < KT; ++u) x6_mma(za, xb[u][0], xb[u][1], xb[u][2], hw[h][u], lw[h][u]);
-        }
-      }
-#endif
-      XS_STAMP(it, 4);
       if constexpr (DX) {   // after the wgrad sweep: an accumulating dX had it to arrive
 #pragma unroll
         for (int u = 0; u < DT; ++u)
@@ -775,23 +525,15 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
             }
           }
       }
-      XS_STAMP(it, 5);
-      if constexpr (!LATE) XS_WAIT_STAMP(it, 9);
-      if constexpr (!LATE) put(t + G, b ^ 1, -1);
-      XS_STAMP(it, 6);
+      if constexpr (!LATE) put(t + G, b ^ 1);
       __syncthreads();
-      XS_STAMP(it, 7);
     }
   };
-#if HGNN_XS_STAGGER
   if (w >= 4) {
     loop(std::true_type{});
   } else {
     loop(std::false_type{});
   }
-#else
-  loop(std::false_type{});
-#endif
   if constexpr (WG) {
     // the slab row: [h][K + 1] of its own, or a column block of a shared [h][slab_ld] (the
     // K = 384 / 512 column blocks, one reduce for both)
@@ -830,15 +572,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
 }
 
 }  // namespace
-
-#if HGNN_XS_STAMPS
-extern "C" int hgnn_debug_xs_stamps(unsigned long long* host, size_t n) {
-  const size_t have = sizeof(g_xs_stamps) / sizeof(g_xs_stamps[0]);
-  if (n > have) n = have;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_xs_stamps), n * sizeof(unsigned long long)) ==
-                 hipSuccess ? (int)n : -1;
-}
-#endif
 
 int64_t xs_bwd_grid(int64_t n_rows) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_rows, 32), 256));

@@ -235,6 +235,14 @@ class CapturedStep:
         self.model, self.x_dict, self.loss_fn, self.opt = model, x_dict, loss_fn, optimizer
         self.between = between
         self.capture_between = bool(capture_between) and between is not None
+        if self.capture_between:
+            # a collective recorded into the graph must be a device-side one (RCCL); gloo runs
+            # its collectives on the host and cannot be captured
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized() and dist.get_backend() != "nccl":
+                raise ValueError("CapturedStep(capture_between=True) needs the nccl (RCCL) "
+                                 f"backend; got {dist.get_backend()!r} — leave capture_between "
+                                 "off to replay around an eager all-reduce")
         if partial_seeds is None:
             partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
         self.blocks = StaticBlocks(smp, n_seeds, slack, partial_seeds=partial_seeds)

@@ -230,58 +230,6 @@ def _score_gather2(U, P, pos, negs, cscale, inv_e, out):
             N.stream_ptr(dev)), "hgnn_score_gather2")
 
 
-_SCORE2 = os.environ.get("HGNN_SCORE2", "1") == "1"   # 0: the two separate dP gathers (A/B)
-
-# The dP gather over the user table in source-block passes, as K1: pass b sums
-# the positives and negatives whose user lies in block b, accumulating into dP; every pass
-# re-reads its rows' P vectors and dP.  HGNN_DP_BLOCKS: 1 one pass, N passes, "auto" the K1
-# rule (ops.gather_blocks); HGNN_DP_CACHED=1: default-policy user-row loads in the passes.
-DP_BLOCKS = os.environ.get("HGNN_DP_BLOCKS", "1")
-DP_CACHED = os.environ.get("HGNN_DP_CACHED", "1") == "1"
-
-
-def dp_blocks(U: torch.Tensor, n_edges: int) -> int:
-    if DP_BLOCKS == "auto":
-        return gather_blocks(U, n_edges)
-    return max(1, int(DP_BLOCKS))
-
-
-def _score_gather2_blocked(U, P, csr: RelationCSR, rowptr_n, nu_s, cscale, inv_e, out, B: int,
-                           cached: bool = True):
-    """``_score_gather2`` as ``B`` source-block passes over the user table: the positives from
-    ``csr.blocks("fwd", B)`` (the K1 passes of the same relation: built once, shared), the
-    negatives as each post's sub-segment per block (their users ascend within a post: the
-    stable sort of user-grouped positions), found by one ``hgnn_segment_bounds`` launch.  Sums
-    per row in block order (fp32 reassociation against the one pass, like the blocked K1)."""
-    dev = out.device
-    d = int(out.shape[1])
-    n = csr.n_dst
-    nu = int(U.shape[0])
-    passes, _ = csr.blocks("fwd", B)
-    bs = -(-nu // B)
-    lib, s = N.lib(), N.stream_ptr(dev)
-    E = csr.num_edges + int(nu_s.numel())
-    nb = gather_bytes(E, n, d, False) + 4 * (n + 1) + 4 * n * d
-    cb = gather_compulsory_bytes(E, n, nu, d, False) + 4 * (n + 1) + 4 * n * d
-    thr = torch.tensor([b * bs for b in range(1, B)], dtype=torch.int32, device=dev)
-    bounds = torch.empty(max((B - 1) * n, 1), dtype=torch.int32, device=dev)
-    with _timed(f"score_gather[{n}<-{nu}]x{d}", nb, cb):
-        N.check(lib.hgnn_segment_bounds(N.ptr(rowptr_n), N.ptr(nu_s), n, N.ptr(thr), B - 1,
-                                        N.ptr(bounds), s), "hgnn_segment_bounds")
-        for b, g in enumerate(passes):
-            p = g.plan
-            slab = (torch.empty(p.n_chunks * d, dtype=torch.float32, device=dev)
-                    if p.n_heavy else None)
-            beg = rowptr_n if b == 0 else bounds[(b - 1) * n:b * n]
-            end = bounds[b * n:(b + 1) * n] if b < B - 1 else rowptr_n[1:]
-            flags = (N.HGNN_ACCUMULATE if b > 0 else 0) | (N.HGNN_CACHED_LOADS if cached else 0)
-            N.check(lib.hgnn_score_gather2_ex(
-                N.ptr(U), nu, N.ptr(P), d, N.ptr(g.rowptr), N.ptr(g.col), N.ptr(beg), N.ptr(end),
-                N.ptr(nu_s), n, N.ptr(cscale), inv_e, N.ptr(p.heavy_rows), N.ptr(p.heavy_first),
-                p.n_heavy, p.n_chunks, p.chunk, N.ptr(slab), N.ptr(out), flags, s),
-                "hgnn_score_gather2_ex")
-
-
 def scatter_mean_bwd(grad_aggr: torch.Tensor, csr: RelationCSR,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K2: ``grad_x_src[j] (+)= sum_{(j->i)} grad_aggr[i] / deg_i`` over the CSC."""
@@ -1077,14 +1025,10 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
                     ng = GroupedEdges(rowptr_n[lo:hi + 1], nu_s, None,
                                       Plan(NO_SPLIT, 0, 0, None, None), hi - lo)
                     _score_gather2(U, P[lo:hi], _row_range(pf, lo, hi), ng, c, inv_e, dP[lo:hi])
-        elif _SCORE2 and dp_blocks(U, E) > 1:
-            _score_gather2_blocked(U, P, csr, rowptr_n, nu_s, c, inv_e, dP, dp_blocks(U, E),
-                                   DP_CACHED)
-        elif _SCORE2:
-            _score_gather2(U, P, pf, negs, c, inv_e, dP)
         else:
-            _score_gather(U, P, pf, 1, c, inv_e, dP, False, "pos")
-            _score_gather(U, P, negs, 2, c, inv_e, dP, True, "neg")
+            # (Measured and not kept, round 5: this gather in 8 source-block passes like K1,
+            # 32.83 vs 31.32 ms at cfg4 — each pass re-reads its rows' P vectors and dP.)
+            _score_gather2(U, P, pf, negs, c, inv_e, dP)
         if on_dP is not None:
             on_dP(dP)
     if ready is not None and p_chunks is not None:

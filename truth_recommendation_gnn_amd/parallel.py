@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import time
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -45,6 +46,92 @@ from .synth import ENGAGES, REV_ENGAGES
 EdgeType = Tuple[str, str, str]
 
 RELATIONS = [(REV_ENGAGES, 1.0), (ENGAGES, 1.0)]
+
+
+class CollectiveTrace:
+    """Per-collective timing of the sharded step (bench.py's per-kernel timer run at N > 1,
+    VERDICT r5 #2): a mark on the issuing stream when a collective is issued, and on the
+    consumer's stream just before and just after the consumer's ``wait()``.
+      * issue -> after: the collective's latency as its consumer sees it (cover + stall);
+      * before -> after: the stall it caused (the consumer's stream waited that long for it);
+      * issue -> before: the compute issued under it (its cover).
+    With RCCL the marks are HIP events (``wait()`` is a stream wait, no host sync); on the CPU
+    (the gloo rehearsal) host clock readings.  ``begin_step()`` starts a step's list, so the
+    collectives line up by their position in the step across steps and ranks."""
+
+    def __init__(self, device: torch.device):
+        self.cuda = device.type == "cuda"
+        self.steps: List[List[dict]] = []
+
+    def begin_step(self):
+        self.steps.append([])
+
+    def _mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def issue(self, op: str, nbytes: int) -> dict:
+        if not self.steps:
+            self.begin_step()
+        rec = {"op": op, "bytes": int(nbytes), "issue": self._mark()}
+        self.steps[-1].append(rec)
+        return rec
+
+    def before_wait(self, rec: dict):
+        if "pre" not in rec:
+            rec["pre"] = self._mark()
+
+    def after_wait(self, rec: dict):
+        if "post" not in rec:
+            rec["post"] = self._mark()
+
+    def _ms(self, a, b) -> float:
+        return float(a.elapsed_time(b)) if self.cuda else (b - a) * 1e3
+
+    def per_position(self) -> List[dict]:
+        """Means over the recorded steps, per collective position: op, bytes, wait_ms (issue ->
+        after), stall_ms (before -> after), cover_ms (issue -> before).  Call after a device
+        synchronise.  A position some step did not wait for is left out of that step's mean."""
+        if not self.steps:
+            return []
+        M = min(len(st) for st in self.steps)
+        out = []
+        for j in range(M):
+            recs = [st[j] for st in self.steps if "pre" in st[j] and "post" in st[j]]
+            r0 = self.steps[0][j]
+            row = {"op": r0["op"], "bytes": r0["bytes"], "n": len(recs)}
+            if recs:
+                row["wait_ms"] = sum(self._ms(r["issue"], r["post"]) for r in recs) / len(recs)
+                row["stall_ms"] = sum(max(0.0, self._ms(r["pre"], r["post"]))
+                                      for r in recs) / len(recs)
+                row["cover_ms"] = sum(self._ms(r["issue"], r["pre"]) for r in recs) / len(recs)
+            out.append(row)
+        return out
+
+
+_TRACE: Optional[CollectiveTrace] = None
+
+
+def set_collective_trace(trace: Optional[CollectiveTrace]) -> None:
+    """Record every collective DistEnv issues into ``trace`` (None: stop)."""
+    global _TRACE
+    _TRACE = trace
+
+
+def _issue(op: str, t: torch.Tensor):
+    return _TRACE.issue(op, t.numel() * t.element_size()) if _TRACE is not None else None
+
+
+def _sync_done(rec):
+    """A collective that completed in its call (gloo over device tensors, the blocking all-reduce):
+    the consumer waited from the issue on (no cover), until the mark taken after the call (with
+    RCCL recorded behind the stream wait the call enqueued)."""
+    if rec is not None and _TRACE is not None:
+        rec.setdefault("pre", rec["issue"])
+        _TRACE.after_wait(rec)
 
 
 @dataclasses.dataclass
@@ -69,7 +156,9 @@ class DistEnv:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
+            rec = _issue("all_reduce", t)
             dist.all_reduce(t, group=self.group)
+            _sync_done(rec)
         return t
 
     def post_slice(self, n: int) -> Tuple[int, int, int]:
@@ -88,22 +177,26 @@ class DistEnv:
         S = full.shape[0] // self.world
         if out is None:
             out = torch.empty((S,) + tuple(full.shape[1:]), dtype=full.dtype, device=full.device)
+        rec = _issue("reduce_scatter", full)
         if self._direct(full):
             work = dist.reduce_scatter_tensor(out, full, group=self.group, async_op=True)
-            return out, _Held(work, full, out)
+            return out, _Held(work, full, out, rec=rec)
         t = full.clone()
         dist.all_reduce(t, group=self.group)
         out.copy_(t[self.rank * S:(self.rank + 1) * S])
+        _sync_done(rec)
         return out, _Done()
 
     def all_gather_async(self, own: torch.Tensor):
         """Concatenation over ranks of ``own`` [S, ...]; returns (full [world*S, ...], work)."""
         full = torch.empty((own.shape[0] * self.world,) + tuple(own.shape[1:]), dtype=own.dtype,
                            device=own.device)
+        rec = _issue("all_gather", full)
         if self._direct(own):
             work = dist.all_gather_into_tensor(full, own, group=self.group, async_op=True)
-            return full, _Held(work, own, full)
+            return full, _Held(work, own, full, rec=rec)
         dist.all_gather(list(full.chunk(self.world)), own, group=self.group)
+        _sync_done(rec)
         return full, _Done()
 
     def broadcast_slices_async(self, own: torch.Tensor):
@@ -116,36 +209,43 @@ class DistEnv:
         full = torch.empty((S * self.world,) + tuple(own.shape[1:]), dtype=own.dtype,
                            device=own.device)
         if not self._direct(own):
+            rec = _issue("all_gather", full)
             dist.all_gather(list(full.chunk(self.world)), own, group=self.group)
+            _sync_done(rec)
             return full, [_Done() for _ in range(self.world)]
         full[self.rank * S:(self.rank + 1) * S].copy_(own)
         works = []
         for q in range(self.world):
             blk = full[q * S:(q + 1) * S]
+            rec = _issue(f"broadcast[src={q}]", blk)
             w = dist.broadcast(blk, src=q, group=self.group, async_op=True)
-            works.append(_Done() if q == self.rank and w is None else _Held(w, own, full))
+            works.append(_Done() if q == self.rank and w is None else
+                         _Held(w, own, full, rec=rec))
         return full, works
 
     def all_to_all_async(self, inp: torch.Tensor, send_splits, recv_splits):
         """Rows ``inp[sum(send_splits[:q]) : ...]`` go to rank q; returns (received rows, in rank
         order, work).  Split lists are host ints (static per graph: no size exchange per call)."""
         out = inp.new_empty((int(sum(recv_splits)),) + tuple(inp.shape[1:]))
+        rec = _issue("all_to_all", inp)
         if self._direct(inp):
             work = dist.all_to_all_single(out, inp, list(recv_splits), list(send_splits),
                                           group=self.group, async_op=True)
-            return out, _Held(work, inp, out)
+            return out, _Held(work, inp, out, rec=rec)
         # gloo over device tensors (one-GPU rehearsal): the exchange goes through host memory
         host = torch.empty(out.shape, dtype=out.dtype)
         dist.all_to_all_single(host, inp.cpu(), list(recv_splits), list(send_splits),
                                group=self.group)
         out.copy_(host)
+        _sync_done(rec)
         return out, _Done()
 
     def all_reduce_async(self, t: torch.Tensor):
         """Start an in-place all-reduce; ``.wait()`` on the result before reading ``t`` (with
         NCCL/RCCL that is a stream wait, so kernels enqueued in between overlap the collective)."""
         if self.world > 1:
-            return _Held(dist.all_reduce(t, group=self.group, async_op=True), t)
+            rec = _issue("all_reduce", t)
+            return _Held(dist.all_reduce(t, group=self.group, async_op=True), t, rec=rec)
         return _Done()
 
 
@@ -158,14 +258,19 @@ class _Held:
     """An async collective's Work plus references to its buffers until ``wait()`` (gloo's async
     ops do not keep a temporary input alive on their own)."""
 
-    def __init__(self, work, *refs):
+    def __init__(self, work, *refs, rec: Optional[dict] = None):
         self.work, self.refs = work, refs
+        self.rec, self.trace = rec, _TRACE if rec is not None else None
 
     def wait(self):
+        if self.trace is not None:
+            self.trace.before_wait(self.rec)
         # gloo finishes an async collective by copying into the output at wait(); outside no_grad
         # autograd would record that copy on an output it already tracks and cut its graph
         with torch.no_grad():
             self.work.wait()
+        if self.trace is not None:
+            self.trace.after_wait(self.rec)
         self.refs = None
         return True
 
@@ -183,14 +288,13 @@ class _AllOf:
 
 
 # The last forward gather of the post table (the loss's input) as per-source broadcasts whose
-# row blocks the loss's dP gather consumes as they land (DistEnv.broadcast_slices_async):
-# HGNN_CHUNKED_GATHER=1 one dP launch per block, 2 three launches (own block, the blocks below,
-# the blocks above), 3 the own block and then the others in landing order in groups of
-# HGNN_CHUNK_GROUP (2) blocks, 0 one all-gather and one dP launch.  The broadcasts land one by one
-# (one link: ~0.42 ms per 64 MB block at N = 8) and the dP gather of a block takes ~0.49 ms, so
-# groups of two keep the gather just behind the link where mode 2's "blocks above" waited for all
-# seven (rank 0: 2.3 ms stalled on the one-link replay, round 4).
-CHUNKED_LAST_GATHER = int(os.environ.get("HGNN_CHUNKED_GATHER", "3"))
+# row blocks the loss's dP gather consumes as they land (DistEnv.broadcast_slices_async): the own
+# block first, then the others in landing order in groups of HGNN_CHUNK_GROUP (2) blocks.  The
+# broadcasts land one by one (one link: ~0.42 ms per 64 MB block at N = 8) and the dP gather of a
+# block takes ~0.49 ms, so groups of two keep the gather just behind the link.  (Measured and
+# not kept, DESIGN.md §7: one all-gather and one dP launch; one launch per block; own block /
+# blocks below / blocks above, whose "blocks above" waited for all seven broadcasts — rank 0
+# stalled 2.3 ms on the one-link replay, round 4.)
 CHUNK_GROUP = int(os.environ.get("HGNN_CHUNK_GROUP", "2"))
 # the first group's size: the own block's dP gather (~0.66 ms at N = 8) covers one landed block,
 # not two (HGNN_CHUNK_FIRST)
@@ -1061,42 +1165,29 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
                     table = impl.linear_fwd_raw([y_p_own], block, None, False)
                     proj[nxt] = (block, (o, k))
             st["y_p_own"] = y_p_own
-            if multi and nxt == L and CHUNKED_LAST_GATHER:
+            if multi and nxt == L:
                 # the loss's post table: one broadcast per source rank, so the dP gather can run
                 # on each row block as it lands (own block first) instead of after all of them
                 st["y_p"], works = env.broadcast_slices_async(table)
                 S, r, W = shard.post_rows, env.rank, env.world
-                if CHUNKED_LAST_GATHER == 1:      # one dP launch per source block
-                    order = [r] + [q for q in range(W) if q != r]   # own, then as they land
-                    st["p_chunks"] = [(q * S, (q + 1) * S, None if q == r else works[q].wait)
-                                      for q in order]
-                elif CHUNKED_LAST_GATHER == 3:    # own block, then groups in landing order
-                    others = [q for q in range(W) if q != r]
-                    first = max(1, CHUNK_FIRST)
-                    groups = [others[:first]] + [
-                        others[i:i + max(1, CHUNK_GROUP)]
-                        for i in range(first, len(others), max(1, CHUNK_GROUP))]
-                    groups = [grp for grp in groups if grp]
-                    st["p_chunks"] = [(r * S, (r + 1) * S, None)]
-                    for grp in groups:
-                        # a group of blocks contiguous in rows (the own block splits at most one)
-                        runs = []
-                        for q in grp:
-                            if runs and runs[-1][1] == q * S:
-                                runs[-1][1] = (q + 1) * S
-                            else:
-                                runs.append([q * S, (q + 1) * S])
-                        wait = (lambda qs: (lambda: [works[q].wait() for q in qs]))(grp)
-                        for k, (lo, hi) in enumerate(runs):
-                            st["p_chunks"].append((lo, hi, wait if k == 0 else None))
-                else:                             # own block, blocks below it, blocks above it
-                    # each range waits on every broadcast it reads (stream waits, free): no
-                    # reliance on the backend finishing them in issue order
-                    def wait_all(qs):
-                        return (lambda: [works[q].wait() for q in qs]) if qs else None
-                    st["p_chunks"] = [(r * S, (r + 1) * S, None),
-                                      (0, r * S, wait_all(range(0, r))),
-                                      ((r + 1) * S, W * S, wait_all(range(r + 1, W)))]
+                others = [q for q in range(W) if q != r]
+                first = max(1, CHUNK_FIRST)
+                groups = [others[:first]] + [
+                    others[i:i + max(1, CHUNK_GROUP)]
+                    for i in range(first, len(others), max(1, CHUNK_GROUP))]
+                groups = [grp for grp in groups if grp]
+                st["p_chunks"] = [(r * S, (r + 1) * S, None)]
+                for grp in groups:
+                    # a group of blocks contiguous in rows (the own block splits at most one)
+                    runs = []
+                    for q in grp:
+                        if runs and runs[-1][1] == q * S:
+                            runs[-1][1] = (q + 1) * S
+                        else:
+                            runs.append([q * S, (q + 1) * S])
+                    wait = (lambda qs: (lambda: [works[q].wait() for q in qs]))(grp)
+                    for k, (lo, hi) in enumerate(runs):
+                        st["p_chunks"].append((lo, hi, wait if k == 0 else None))
                 ag = _AllOf(works)
             else:
                 st["y_p"], ag = env.all_gather_async(table) if multi else (table, None)
@@ -1109,19 +1200,11 @@ def _step(shard: "UserShard", model, x_user_own, x_post, neg_local, neg_order, x
             user_gathers()
             user_projection()
         else:
+            # the loss's dP gather covers the last post table's broadcasts, so the user
+            # projection goes first, under the reduce-scatter
             user_gathers()
-            # the last layer's user projection waits until the post table's all-gather is
-            # issued: the loss needs that table at once, so the projection and the negatives
-            # sort both run under the collective (the reduce-scatter still has the user-side
-            # gathers under it).  With the chunked gather the loss's dP gather covers it, and the
-            # projection goes first, under the reduce-scatter.
-            late_u = (multi and bool(pm) and bool(um) and li == L - 1
-                      and not CHUNKED_LAST_GATHER)
-            if not late_u:
-                user_projection()
+            user_projection()
             post_side()
-            if late_u:
-                user_projection()
         x_ext, a_u, add, y_u = st["x_ext"], st["a_u"], st["add"], st["y_u"]
         p_chunks = st["p_chunks"]
         a_p, y_p_own, y_p = st["a_p"], st["y_p_own"], st["y_p"]
