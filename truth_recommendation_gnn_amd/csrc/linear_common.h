@@ -147,40 +147,12 @@ __device__ __forceinline__ uint32_t x6_cvt_pk(float a, float b) {
   asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
-// The residuals a - lo(p), b - hi(p) as one v_dot2c_f32_bf16 each (round 6): the packed pair p
-// dotted with the bf16 pair (-1, 0) or (0, -1), accumulated onto a or b.  Both products are
-// exact and so is the difference (a minus its own bf16 rounding), so the pieces are bit for bit
-// the shift/mask + subtract form's (scripts/x6_split_probe.hip, 2^25 pairs over the finite range,
-// denormals and rounding ties) in 7 VALU per pair instead of 11.  One difference, for non-finite
-// inputs only: the other half's inf or NaN times 0 makes this half's residual NaN too — both
-// values of a pair then feed the same output row (forward, dgrad), which the inf already makes
-// non-finite; only the wgrad's column of the pair's finite partner differs from the f32 kernels.
-#ifndef HGNN_X6_DOT2
-#define HGNN_X6_DOT2 1
-#endif
-typedef __bf16 x6_bf16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ float x6_res_lo(uint32_t p, float a) {
-#if HGNN_X6_DOT2
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(x6_bf16x2, p),
-                                         __builtin_bit_cast(x6_bf16x2, 0x0000BF80u), a, false);
-#else
-  return a - __uint_as_float(p << 16);
-#endif
-}
-__device__ __forceinline__ float x6_res_hi(uint32_t p, float b) {
-#if HGNN_X6_DOT2
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(x6_bf16x2, p),
-                                         __builtin_bit_cast(x6_bf16x2, 0xBF800000u), b, false);
-#else
-  return b - __uint_as_float(p & 0xffff0000u);
-#endif
-}
 __device__ __forceinline__ void x6_split2(float a, float b, uint32_t& p1, uint32_t& p2,
                                           uint32_t& p3) {
   p1 = x6_cvt_pk(a, b);
-  const float ra = x6_res_lo(p1, a), rb = x6_res_hi(p1, b);
+  const float ra = a - __uint_as_float(p1 << 16), rb = b - __uint_as_float(p1 & 0xffff0000u);
   p2 = x6_cvt_pk(ra, rb);
-  const float sa = x6_res_lo(p2, ra), sb = x6_res_hi(p2, rb);
+  const float sa = ra - __uint_as_float(p2 << 16), sb = rb - __uint_as_float(p2 & 0xffff0000u);
   p3 = x6_cvt_pk(sa, sb);
 }
 __device__ __forceinline__ void x6_split4(const float4& u, bf16x4_t& p1, bf16x4_t& p2,

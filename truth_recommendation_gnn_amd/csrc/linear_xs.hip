@@ -28,6 +28,9 @@
 #ifndef HGNN_XS_LDSPF
 #define HGNN_XS_LDSPF 2
 #endif
+#ifndef HGNN_XS_XZERO
+#define HGNN_XS_XZERO 0
+#endif
 #ifndef HGNN_XS_LDSPF_DXWG
 #define HGNN_XS_LDSPF_DXWG 1
 #endif
@@ -397,7 +400,11 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
       *reinterpret_cast<bf16x4_t*>(d + ZS) = p2;
       *reinterpret_cast<bf16x4_t*>(d + 2 * ZS) = p3;
     }
-    if constexpr (WG) xs.template put<LDX, XS, true>(xr, xp[b], tt * R, a.n);
+    // X's rows past n are NOT zeroed (round 6): they are clamped copies of row n - 1 and meet
+    // only the zeroed dz rows above, so their products are exact zeros — unless row n - 1 holds
+    // an inf or NaN, where 0 x inf adds NaN to the columns the f32 kernels would make +-inf.
+    // Saves a compare and four selects per float4 on every tile.
+    if constexpr (WG) xs.template put<LDX, XS, HGNN_XS_XZERO != 0>(xr, xp[b], tt * R, a.n);
   };
   // (Measured and not kept: a uniform branch to a copy of the put without the per-row zeroing
   // on every tile but the last — within noise at the cfg4 shapes, and the K = 256 wgrad kernel
