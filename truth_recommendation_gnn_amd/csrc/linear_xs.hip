@@ -28,9 +28,6 @@
 #ifndef HGNN_XS_LDSPF
 #define HGNN_XS_LDSPF 2
 #endif
-#ifndef HGNN_XS_XZERO
-#define HGNN_XS_XZERO 0
-#endif
 #ifndef HGNN_XS_LDSPF_DXWG
 #define HGNN_XS_LDSPF_DXWG 1
 #endif
@@ -87,18 +84,15 @@ struct XStage {
       x.v[j] = *reinterpret_cast<const float4*>(base + (uint64_t)row * ld);
     }
   }
-  // split into the three planes (plane stride PS halfwords, row stride LDP).  ZERO: rows past n
-  // (clamped copies of the last row) become zeros — the backward's reductions over rows need
-  // that (0 x inf would be NaN); a forward row only reaches its own output, never stored
-  template <int LDP, int PS, bool ZERO = false>
-  __device__ __forceinline__ void put(const Regs& x, unsigned short* pl, int64_t r0,
-                                      int64_t n = 0) const {
+  // split into the three planes (plane stride PS halfwords, row stride LDP).  Rows past the end
+  // are clamped copies of the last row: a forward row only reaches its own (unstored) output,
+  // and the backward pairs them with zeroed dz rows
+  template <int LDP, int PS>
+  __device__ __forceinline__ void put(const Regs& x, unsigned short* pl) const {
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      float4 v = x.v[j];
-      if (ZERO && r0 + row0 + j * RSTEP >= n) v = make_float4(0.f, 0.f, 0.f, 0.f);
       bf16x4_t p1, p2, p3;
-      x6_split4(v, p1, p2, p3);
+      x6_split4(x.v[j], p1, p2, p3);
       unsigned short* d = pl + (row0 + j * RSTEP) * LDP + col;
       *reinterpret_cast<bf16x4_t*>(d) = p1;
       *reinterpret_cast<bf16x4_t*>(d + PS) = p2;
@@ -202,7 +196,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   };
   int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
   xs.issue(xr, t * R, last);
-  xs.template put<LDP, PS>(xr, pl[0], t * R);
+  xs.template put<LDP, PS>(xr, pl[0]);
   // Staggered halves (HGNN_XS_STAGGER): the two waves sharing a SIMD (w and w + 4) run the same
   // program in lockstep, so both sweep (matrix pipe busy, VALU idle) and then both split (VALU
   // busy, matrix pipe idle).  Waves 4-7 instead split the next tile FIRST — from loads issued an
@@ -228,7 +222,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
     auto iter = [&](auto first_c) {
       constexpr bool FIRST = decltype(first_c)::value;
       const int b = it & 1;
-      if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
+      if constexpr (LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1]);
       // the iteration's memory instructions, piece k at sweep step k * NQ / NP: the previous
       // tile's mask words, this tile's added rows, the prefetch, the previous tile's stores
       // (youngest: the waits for the added rows and the prefetch leave them in flight)
@@ -299,7 +293,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
         po[r] = v;
         if (mask_out) atomicOr(&mk[b][(16 * r + i) * 4 + g], relu_out_bits(v, 4 * w));
       }
-      if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1], (t + G) * R);
+      if constexpr (!LATE) xs.template put<LDP, PS>(xr, pl[b ^ 1]);
       __syncthreads();
     };
     if (t < n_tiles) {
@@ -404,7 +398,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     // only the zeroed dz rows above, so their products are exact zeros — unless row n - 1 holds
     // an inf or NaN, where 0 x inf adds NaN to the columns the f32 kernels would make +-inf.
     // Saves a compare and four selects per float4 on every tile.
-    if constexpr (WG) xs.template put<LDX, XS, HGNN_XS_XZERO != 0>(xr, xp[b], tt * R, a.n);
+    if constexpr (WG) xs.template put<LDX, XS>(xr, xp[b]);
   };
   // (Measured and not kept: a uniform branch to a copy of the put without the per-row zeroing
   // on every tile but the last — within noise at the cfg4 shapes, and the K = 256 wgrad kernel
