@@ -36,6 +36,7 @@ sample of the same graph family (same degree distributions, so per-edge work is 
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -103,6 +104,9 @@ def parse(argv=None):
                    help="cfg5 mini-batch: no side-stream sampling of the next batch")
     p.add_argument("--prefetch", action="store_true",
                    help="cfg5 mini-batch: sample the next batch on a side stream under this one")
+    p.add_argument("--prepare-on-main", action="store_true",
+                   help="cfg5 mini-batch: stage the batch's block / loss structures on the main "
+                        "stream right before the replay, not on the side stream after sampling")
     p.add_argument("--scale", type=float, default=1.0, help="shrink the config (debug only)")
     p.add_argument("--timer-steps", type=int, default=5,
                    help="steps of the separate per-kernel-event run (0: none)")
@@ -1041,13 +1045,31 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     prefetch = args.prefetch or (use_graph and not args.no_prefetch)
     side = torch.cuda.Stream(dev) if prefetch else None
 
-    def sample(b):
+    ph = _Phases() if os.environ.get("HGNN_CFG5_PHASES") else None
+
+    def sample(b, prep=True):
         gb = (b % max(per_epoch, 1)) * world + rank            # this rank's slice of the order
         ids = order[gb * nb:(gb + 1) * nb].long()
 
         def make():
-            lb = minibatch.link_batch(pos_ei, ids, cfg.num_posts, generator=gen_neg)
-            lb.mb = s.sample(lb.seeds, seed=gb)
+            if ph:
+                ph.mark(b, "smp0")
+            with _Phases.host(ph, "link_batch"):
+                lb = minibatch.link_batch(pos_ei, ids, cfg.num_posts, generator=gen_neg)
+            with _Phases.host(ph, "sample"):
+                lb.mb = s.sample(lb.seeds, seed=gb)
+            if ph:
+                ph.mark(b, "smp1")
+            if prep and not args.prepare_on_main:
+                # the batch's block / loss structures into the staging buffers, on the same
+                # stream as the sampler (the side stream under the running replay)
+                with _Phases.host(ph, "prepare"):
+                    if captured is not None:
+                        captured.prepare(lb.mb, lb.pu, lb.pp, lb.pn)
+                    else:
+                        link_loss.prepare(lb.pu, lb.pp, lb.pn)
+                if ph:
+                    ph.mark(b, "prep1")
             return lb
         if side is None:
             return make(), None
@@ -1074,6 +1096,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         return link_loss(out)
 
     loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
+    loss_of.prepare, loss_of.commit = link_loss.prepare, link_loss.commit
     loss_of.partial_seeds = True                 # both forms read the seed rows by local id
 
     # over RCCL the gradient all-reduce is recorded inside the step's graph (one replay per
@@ -1092,7 +1115,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         captured = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_of, opt,
                                           between=sync if (world > 1 or capture_ar) else None,
                                           capture_between=capture_ar)
-        lb0 = sample(0)[0]
+        lb0 = sample(0, prep=False)[0]
         link_loss.load(lb0.pu, lb0.pp, lb0.pn)
         captured.capture(lb0.mb, warmup=2)
 
@@ -1110,16 +1133,37 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     def step(graph=True):
         lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
         state["b"] += 1
+        main = torch.cuda.current_stream(dev)
         if ev is not None:
-            main = torch.cuda.current_stream(dev)
             main.wait_event(ev)
-            lb.mb.record_stream(main)
-            for t in (lb.pu, lb.pp, lb.pn):
-                t.record_stream(main)
         mb = lb.mb
         state["edges"] += sum(blk.csr[et].num_edges for blk in mb.blocks for et in blk.csr)
-        link_loss.load(lb.pu, lb.pp, lb.pn)     # on this stream: the running step reads them
-        loss = captured.step(mb) if (graph and captured is not None) else eager(lb)
+        if args.prepare_on_main:
+            if ev is not None:                   # read on this stream
+                lb.mb.record_stream(main)
+                for t in (lb.pu, lb.pp, lb.pn):
+                    t.record_stream(main)
+            with _Phases.host(ph, "prepare"):
+                if captured is not None:
+                    captured.prepare(lb.mb, lb.pu, lb.pp, lb.pn)
+                else:
+                    link_loss.prepare(lb.pu, lb.pp, lb.pn)
+            if ph:
+                ph.mark(state["b"] - 1, "prep1")
+        if graph and captured is not None:
+            if ph:
+                ph.mark(state["b"] - 1, "rep0")
+            with _Phases.host(ph, "step"):
+                loss = captured.step()           # commit the staged batch, replay
+            if ph:
+                ph.mark(state["b"] - 1, "rep1")
+        else:
+            if ev is not None:                   # the eager step reads the batch on this stream
+                lb.mb.record_stream(main)
+                for t in (lb.pu, lb.pp, lb.pn):
+                    t.record_stream(main)
+            link_loss.commit()
+            loss = eager(lb)
         if side is not None:
             nxt[0] = sample(state["b"])          # under this step's GPU work
         return loss
@@ -1129,11 +1173,14 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     setup_s = time.perf_counter() - t_setup
     clock = _Clock(dev, sharded, args, local)
     state["edges"] = 0
+    if ph:
+        ph.h.clear()
     elapsed, loss = clock.time(step, args.steps)
     edges = torch.tensor([float(state["edges"])], dtype=torch.float64, device=dev)
     if sharded:
         dist.all_reduce(edges)
     edges = float(edges)
+    phases = ph.summary(args.steps) if ph else None
     kern = {}
     if not args.profile_steps and args.timer_steps > 0:
         # per-kernel events need the eager launches: the timer steps run the same kernels
@@ -1186,7 +1233,51 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         "cpu_baseline": cpu,
         "kernels": _kernel_rows(kern, args.timer_steps, cfg.name, world),
         "loss": float(loss.detach()), "setup_s": round(setup_s, 1),
+        **({"phases": phases} if phases else {}),
     }
+
+
+class _Phases:
+    """HGNN_CFG5_PHASES=1: where a cfg5 step's time goes — host seconds per phase of the loop
+    (link batch, sampler, prepare, step issue) and, from events on the stream each phase runs
+    on, the GPU spans per batch: sampling and prepare on the side stream, the replay on the
+    main one, and the main stream's idle gap between two replays."""
+
+    def __init__(self):
+        self.h = {}
+        self.ev = {}
+
+    @staticmethod
+    @contextlib.contextmanager
+    def host(ph, name):
+        if ph is None:
+            yield
+            return
+        t = time.perf_counter()
+        yield
+        ph.h[name] = ph.h.get(name, 0.0) + time.perf_counter() - t
+
+    def mark(self, b, name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.ev.setdefault(b, {})[name] = e
+
+    def summary(self, steps):
+        torch.cuda.synchronize()
+        spans = {"sample": ("smp0", "smp1"), "prepare": ("smp1", "prep1"),
+                 "replay": ("rep0", "rep1"), "prep_to_replay": ("prep1", "rep0")}
+        out = {k: [] for k in list(spans) + ["main_idle"]}
+        bs = sorted(b for b, e in self.ev.items() if {"smp0", "prep1", "rep0", "rep1"} <= set(e))
+        for b in bs[-steps:]:
+            e = self.ev[b]
+            for k, (a, z) in spans.items():
+                out[k].append(e[a].elapsed_time(e[z]))
+            if b - 1 in self.ev and "rep1" in self.ev[b - 1]:
+                out["main_idle"].append(self.ev[b - 1]["rep1"].elapsed_time(e["rep0"]))
+        n = max(len(bs[-steps:]), 1)
+        return {"host_ms_per_step": {k: round(v / n * 1e3, 4) for k, v in self.h.items()},
+                "gpu_ms_mean": {k: round(sum(v) / max(len(v), 1), 4) for k, v in out.items()},
+                "batches": n}
 
 
 if __name__ == "__main__":

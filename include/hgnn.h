@@ -410,6 +410,29 @@ int hgnn_pad_csr_multi(int32_t n_items, const int32_t* const* rowptr, const int3
                        const int64_t* e_cap, const int32_t* dummy, const int32_t* spread,
                        hgnn_stream_t stream);
 
+/* The outermost block's destination rows of a static step (minibatch.StaticBlocks.prepare),
+ * gathered with the staged batch in one launch: item i (n_items <= 8) writes
+ * out[i][r][0..d) = src[i][ids[i][r]][0..d) for r < n_rows[i]; d % 4 == 0, 16-byte aligned rows,
+ * ids in range (not validated).  Replaces the per-type x.index_select of the captured step. */
+int hgnn_gather_rows_multi(int32_t n_items, const float* const* src, const int32_t* const* ids,
+                           const int64_t* n_rows, int64_t d, float* const* out,
+                           hgnn_stream_t stream);
+
+/* A link mini-batch's loss structures in one call (minibatch.LinkLoss.prepare; the reference's
+ * loss, train_gnn.py:259-281, over a batch's positive pairs and their negatives): the E pairs
+ * (pu[i], pp[i]) with negative pn[i] — local ids, users < n_users, posts < n_posts, not
+ * validated — grouped by user, stable: rowptr_u[n_users+1], col_p / neg / uop[E] (post, negative,
+ * user per position); the same pairs by post (hgnn_csr_transpose of rowptr_u / col_p: p_rowptr
+ * [n_posts+1], p_users / p_perm[E]); the negatives by post (hgnn_sort_pairs_i32(neg, uop):
+ * n_rowptr[n_posts+1], n_users_sorted[E]) — the dP gather's order.  Exactly the three calls it
+ * replaces.  ws: hgnn_link_group_ws_bytes(E). */
+size_t hgnn_link_group_ws_bytes(int64_t E);
+int hgnn_link_group(const int32_t* pu, const int32_t* pp, const int32_t* pn, int64_t E,
+                    int64_t n_users, int64_t n_posts, int32_t* rowptr_u, int32_t* col_p,
+                    int32_t* neg, int32_t* uop, int32_t* p_rowptr, int32_t* p_users,
+                    int32_t* p_perm, int32_t* n_rowptr, int32_t* n_users_sorted, void* ws,
+                    size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of
  * user and candidate embeddings, computed by the caller).  Per row:

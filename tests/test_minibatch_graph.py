@@ -244,7 +244,7 @@ def _ref_link_loss(out, lb):
 
 def test_captured_link_step_matches_reference_loss():
     """The captured link-prediction step (static capacities: B users, 2B posts; the fused loss
-    over the pairs, its post grouping built inside the graph) against the eager block forward
+    over the pairs, its groupings staged before the replay) against the eager block forward
     with the reference loss as torch ops, on new batches: loss and every gradient."""
     from truth_recommendation_gnn_amd import minibatch, sampler
     g, s, batch, make_model, _, _, n_seeds = _link_setup()
@@ -361,3 +361,42 @@ def test_captured_link_step_with_rccl_allreduce_in_the_graph():
         assert all(np.isfinite(losses))
     finally:
         dist.destroy_process_group()
+
+
+def test_captured_link_step_prepared_on_a_side_stream():
+    """The bench's pipeline (round 6): each batch is sampled and prepared — padded blocks, root
+    rows, the inner blocks' CSCs, the loss's groupings — into the staging buffers on a side
+    stream while the previous replay runs, then committed (one copy) and replayed: loss and
+    every gradient as the eager step with the reference loss on the same batch."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, batch, make_model, _, _, n_seeds = _link_setup()
+    B = n_seeds["user"]
+    model = make_model()
+    ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, None, slack=16)
+    lb0 = batch(0)
+    ll.load(lb0.pu, lb0.pp, lb0.pn)
+    step.capture(lb0.mb)
+    main, side = torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)
+    lbs = {}
+
+    def prep(b):
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            lbs[b] = lb = batch(b)
+            step.prepare(lb.mb, lb.pu, lb.pp, lb.pn)
+    prep(1)
+    for b in (1, 2, 3):
+        main.wait_stream(side)
+        loss = step.step()                  # commits what prep(b) staged
+        prep(b + 1)                         # the next batch, under this replay
+        got_loss = float(loss)
+        got = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+        torch.cuda.synchronize()
+        ref_model = make_model()
+        ref_model.load_state_dict(model.state_dict())
+        ref = _ref_link_loss(sampler.forward_blocks(ref_model, lbs[b].mb, g.x_dict), lbs[b])
+        ref.backward()
+        assert abs(got_loss - float(ref)) <= 2e-6 * abs(float(ref)), (b, got_loss, float(ref))
+        for n, p in ref_model.named_parameters():
+            _close(got[n], p.grad, n)

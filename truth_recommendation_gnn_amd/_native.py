@@ -91,6 +91,10 @@ _SIGS = {
     "hgnn_relabel_multi_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
     "hgnn_set_k3_split": (_c_i32, [_c_i32]),
     "hgnn_pad_csr_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "hgnn_gather_rows_multi": (_c_i32, [_c_i32, _p, _p, _p, _c_i64, _p, _p]),
+    "hgnn_link_group_ws_bytes": (_c_sz, [_c_i64]),
+    "hgnn_link_group": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _p, _p,
+                                 _p, _p, _p, _c_sz, _p]),
     "hgnn_relabel_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _c_i32, _p, _c_sz,
                                     _p]),
     "hgnn_topk_metrics": (_c_i32, [_p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _c_i32, _p, _p, _p,

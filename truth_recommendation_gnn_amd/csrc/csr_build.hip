@@ -708,6 +708,52 @@ int hgnn_csr_transpose(const int32_t* rowptr, const int32_t* col, int64_t n_rows
 }  // extern "C"
 
 namespace hgnn {
+// the row owning each CSR position (binary search in rowptr)
+__global__ void k_row_of_position(const int32_t* rowptr, int64_t n_rows, int64_t E,
+                                  int32_t* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= E) return;
+  int64_t lo = 0, hi = n_rows;   // rowptr[lo] <= i < rowptr[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rowptr[mid] <= i) lo = mid; else hi = mid;
+  }
+  out[i] = (int32_t)lo;
+}
+}  // namespace hgnn
+
+extern "C" {
+
+size_t hgnn_link_group_ws_bytes(int64_t E) { return sort_ws_bytes(E < 1 ? 1 : E); }
+
+int hgnn_link_group(const int32_t* pu, const int32_t* pp, const int32_t* pn, int64_t E,
+                    int64_t n_users, int64_t n_posts, int32_t* rowptr_u, int32_t* col_p,
+                    int32_t* neg, int32_t* uop, int32_t* p_rowptr, int32_t* p_users,
+                    int32_t* p_perm, int32_t* n_rowptr, int32_t* n_users_sorted, void* ws,
+                    size_t ws_bytes, hgnn_stream_t stream_) {
+  if (E < 0 || n_users < 1 || n_posts < 1 || !uop || (E > 0 && (!pu || !pp || !pn)))
+    return fail(HGNN_E_ARG, "link_group: E=%lld n_users=%lld n_posts=%lld", (long long)E,
+                (long long)n_users, (long long)n_posts);
+  // the pairs by user (stable: positive order within a user), their posts and negatives along
+  if (int rc = hgnn_sort_pairs_i32(pu, pp, pn, E, n_users, rowptr_u, col_p, neg, nullptr, ws,
+                                   ws_bytes, stream_))
+    return rc;
+  if (E > 0) {
+    hipLaunchKernelGGL(k_row_of_position, dim3(cdiv(E, 256)), dim3(256), 0, as_stream(stream_),
+                       rowptr_u, n_users, E, uop);
+    if (int rc = check_launch("k_row_of_position")) return rc;
+  }
+  // the same pairs by post (the dU scoring pass's transpose), and the negatives by post
+  if (int rc = hgnn_csr_transpose(rowptr_u, col_p, n_users, E, n_posts, p_rowptr, p_users, p_perm,
+                                  nullptr, ws, ws_bytes, stream_))
+    return rc;
+  return hgnn_sort_pairs_i32(neg, uop, nullptr, E, n_posts, n_rowptr, n_users_sorted, nullptr,
+                             nullptr, ws, ws_bytes, stream_);
+}
+
+}  // extern "C"
+
+namespace hgnn {
 // The CSCs of several destination-grouped CSRs in one sort: relation r's columns are keyed
 // col + cbase[r] and its positions numbered from ebase[r], so one stable sort over the combined
 // key range groups every relation's entries by (relation, column); each output then takes its

@@ -532,6 +532,57 @@ int hgnn_pad_csr_multi(int32_t n_items, const int32_t* const* rowptr, const int3
   return check_launch("k_pad_csr");
 }
 
+// hgnn_gather_rows_multi: item i's rows out[i][r] = src[i][ids[i][r]] (d floats, r < n_rows[i])
+// in one launch — the static step's root rows, gathered from the feature tables with the staged
+// batch (minibatch.StaticBlocks.prepare).  One float4 per thread over the items' rows numbered
+// consecutively; ids are not validated (the sampler's global ids, padded with 0).
+constexpr int kGatherRowsMax = 8;
+struct RowGather {
+  const float4* src[kGatherRowsMax];
+  const int32_t* ids[kGatherRowsMax];
+  float4* out[kGatherRowsMax];
+  int64_t base[kGatherRowsMax + 1];
+  int32_t n_items, d4;
+};
+
+__global__ void __launch_bounds__(256) k_gather_rows(const RowGather g) {
+  const int64_t total = g.base[g.n_items] * g.d4;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * 256) {
+    const int64_t row = idx / g.d4;
+    const int64_t c = idx - row * g.d4;
+    int it = 0;
+    while (it + 1 < g.n_items && row >= g.base[it + 1]) ++it;
+    const int64_t r = row - g.base[it];
+    g.out[it][r * g.d4 + c] = g.src[it][(int64_t)g.ids[it][r] * g.d4 + c];
+  }
+}
+
+int hgnn_gather_rows_multi(int32_t n_items, const float* const* src, const int32_t* const* ids,
+                           const int64_t* n_rows, int64_t d, float* const* out,
+                           hgnn_stream_t stream_) {
+  if (n_items < 1 || n_items > kGatherRowsMax || d < 4 || d % 4 || d / 4 > INT32_MAX)
+    return fail(HGNN_E_ARG, "gather_rows_multi: n_items=%d (1..%d), d=%lld (a multiple of 4)",
+                n_items, kGatherRowsMax, (long long)d);
+  RowGather g{};
+  g.n_items = n_items;
+  g.d4 = (int32_t)(d / 4);
+  for (int i = 0; i < n_items; ++i) {
+    if (n_rows[i] < 0 || (n_rows[i] > 0 && (!src[i] || !ids[i] || !out[i])) ||
+        ((uintptr_t)src[i] | (uintptr_t)out[i]) % 16)
+      return fail(HGNN_E_ARG, "gather_rows_multi: item %d: null or unaligned rows", i);
+    g.src[i] = reinterpret_cast<const float4*>(src[i]);
+    g.ids[i] = ids[i];
+    g.out[i] = reinterpret_cast<float4*>(out[i]);
+    g.base[i + 1] = g.base[i] + n_rows[i];
+  }
+  const int64_t total = g.base[n_items] * g.d4;
+  if (total == 0) return HGNN_OK;
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(total, 256), 8192);
+  hipLaunchKernelGGL(k_gather_rows, dim3(gx), dim3(256), 0, as_stream(stream_), g);
+  return check_launch("k_gather_rows");
+}
+
 }  // extern "C"
 
 static int relabel(int32_t T, const int32_t* const* prefix, const int64_t* n_prefix,

@@ -9,34 +9,35 @@ node and edge counts, so this module runs the model on STATIC-CAPACITY blocks:
   most level h plus fanout x level-h destinations per relation out of each source type; every
   level gets ``slack`` padded rows on top (>= 1 padded destination row for the padding edges,
   and a padded source row for them to read);
-* ``load(batch)`` copies the batch's block CSRs into the fixed buffers in ONE launch
-  (``hgnn_pad_csr_multi``): real rows first and unchanged, the padding entries spread over the
-  padded rows and pointing at a padded source row, so every buffer is a valid CSR of exactly its
-  capacity; the outermost block's column ids are mapped to GLOBAL ids on the way, so its
-  gathers read the feature tables directly (no ``index_select`` of the input nodes), and its
-  destinations' own rows come as a separate root input (``DstGroup.root_src``);
+* every per-batch input the graph reads lives in one byte arena (``_Arena``), held twice: the
+  LIVE copy the graph was recorded on and a STAGE copy a batch is prepared into.
+  ``prepare(batch)`` fills the stage — the block CSRs padded to capacity in ONE launch
+  (``hgnn_pad_csr_multi``: real rows first and unchanged, the padding entries spread over the
+  padded rows and pointing at a padded source row; the outermost block's column ids mapped to
+  GLOBAL ids on the way, so its gathers read the feature tables directly), the outermost
+  destinations' own rows (``DstGroup.root_src``) gathered from the feature tables, and the CSCs
+  + per-position 1/deg of the inner blocks (one ``hgnn_csr_transpose_multi``) that the backward
+  needs; ``commit()`` is ONE device copy stage -> live.  So the structure builds run on whatever
+  stream ``prepare`` is called on — a side stream under the previous replay, next to the
+  sampler — and the replay itself is the model's kernels only (round 6: 28 fewer graph nodes);
 * ``capture(loss_fn, optimizer)`` records forward + loss + backward (+ the optimizer step) once;
-  ``step(batch)`` = ``load`` + ``replay``.
+  ``step(batch)`` = ``prepare`` + ``commit`` + replay (``step()`` after a ``prepare`` elsewhere).
 
 Padded rows carry finite junk (means of padded source rows) that never reaches a seed: a padded
 destination row is never a source of a real row, and the loss reads the seed rows only, so the
-padded rows' gradients are exactly 0 and add nothing to the weight gradients.  The block CSCs
-and 1/deg the backward needs are built INSIDE the graph (the relation objects used for capture
-are fresh, so nothing cached from the warm-up stands in for the next batch's structures).
-Tested against the eager ``forward_blocks`` step on the same batches (outputs, loss, every
-parameter gradient).
+padded rows' gradients are exactly 0 and add nothing to the weight gradients.  Tested against
+the eager ``forward_blocks`` step on the same batches (outputs, loss, every parameter gradient).
 """
 from __future__ import annotations
 
 import dataclasses
-import weakref
 from typing import Callable, Dict, List, Mapping, Optional, Tuple
 
 import torch
 
 from . import _native as N
 from . import ops
-from .graph import RelationCSR
+from .graph import NO_SPLIT, GroupedEdges, Plan, RelationCSR
 from .nn import HeteroSAGE, _fused_weights
 from .sampler import EdgeType, MiniBatch, NeighborSampler
 
@@ -65,17 +66,66 @@ def capacities(relations, n_seeds: Mapping[str, int], fanouts, slack: int = SLAC
     return cap, ecap
 
 
+class _Arena:
+    """Named per-batch buffers in one byte arena, held twice with one layout: ``live`` (what a
+    recorded graph reads) and ``stage`` (where the next batch is written, on any stream).
+    ``commit()`` = one device copy stage -> live on the current stream; ``prepare`` callers wait
+    for the last commit first (``wait_committed``), so a stage write never races the copy that
+    reads it.  Offsets are 256-byte aligned; both copies start zeroed (a valid empty CSR)."""
+
+    ALIGN = 256
+
+    def __init__(self, specs: Mapping[str, Tuple[int, torch.dtype]], device):
+        self.layout, off = {}, 0
+        for k, (n, dt) in specs.items():
+            nb = int(n) * torch.empty((), dtype=dt).element_size()
+            self.layout[k] = (off, int(n), dt, nb)
+            off += -(-max(nb, 1) // self.ALIGN) * self.ALIGN
+        self.nbytes = off
+        self._bytes = {w: torch.zeros(max(off, self.ALIGN), dtype=torch.uint8, device=device)
+                       for w in ("live", "stage")}
+        self.live = self._views("live")
+        self.stage = self._views("stage")
+        self._committed: Optional[torch.cuda.Event] = None
+        self._dirty = False
+
+    def _views(self, which):
+        buf = self._bytes[which]
+        return {k: buf[o:o + nb].view(dt) for k, (o, n, dt, nb) in self.layout.items()}
+
+    def wait_committed(self) -> None:
+        """Called by a writer of the stage before it writes (on its stream)."""
+        if self._committed is not None:
+            torch.cuda.current_stream(self._bytes["stage"].device).wait_event(self._committed)
+        self._dirty = True
+
+    def commit(self) -> None:
+        """No-op when nothing was prepared since the last commit."""
+        if not self._dirty:
+            return
+        self._dirty = False
+        self._bytes["live"].copy_(self._bytes["stage"])
+        if self._bytes["live"].is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._committed = ev
+
+
 class StaticBlocks:
     """Fixed-capacity buffers for the blocks of one sampler configuration (see module doc).
 
-    ``partial_seeds``: a batch may hold FEWER seeds than ``n_seeds`` (the rest are padded level-0
-    rows).  Only a loss that reads the seed rows by their local ids may allow it (``LinkLoss``:
-    a link batch's distinct endpoints vary in number); a loss over all seed rows would be fed
-    the padding, so by default a batch must have exactly ``n_seeds`` seeds per type."""
+    ``x_dict``: the feature tables the outermost block reads (their rows per type give the
+    staged root rows' width).  ``partial_seeds``: a batch may hold FEWER seeds than ``n_seeds``
+    (the rest are padded level-0 rows).  Only a loss that reads the seed rows by their local ids
+    may allow it (``LinkLoss``: a link batch's distinct endpoints vary in number); a loss over
+    all seed rows would be fed the padding, so by default a batch must have exactly ``n_seeds``
+    seeds per type."""
 
-    def __init__(self, smp: NeighborSampler, n_seeds: Mapping[str, int], slack: int = SLACK,
+    def __init__(self, smp: NeighborSampler, n_seeds: Mapping[str, int],
+                 x_dict: Mapping[str, torch.Tensor], slack: int = SLACK,
                  partial_seeds: bool = False):
         self.smp = smp
+        self.x_dict = x_dict
         self.n_seeds = {t: int(n) for t, n in n_seeds.items()}
         self.partial_seeds = bool(partial_seeds)
         if slack < 1:
@@ -85,19 +135,96 @@ class StaticBlocks:
         self.cap, self.ecap = capacities(smp.relations, self.n_seeds, smp.fanouts, slack)
         if max(max(c.values()) for c in self.cap) >= 2**31 - 1:
             raise ValueError("static block capacities exceed int32")
-        dev = smp.device
-        i32 = dict(dtype=torch.int32, device=dev)
-        self.rowptr = [{et: torch.empty(self.cap[h][et[2]] + 1, **i32) for et in self.ecap[h]}
-                       for h in range(self.L)]
-        self.col = [{et: torch.empty(max(self.ecap[h][et], 1), **i32) for et in self.ecap[h]}
-                    for h in range(self.L)]
-        # the outermost block's destinations (level L - 1) as global ids: its root rows
-        self.root_ids = {t: torch.zeros(n, **i32) for t, n in self.cap[self.L - 1].items()}
+        L, i32, f32 = self.L, torch.int32, torch.float32
+        spec: Dict[str, Tuple[int, torch.dtype]] = {}
+        for h in range(L):
+            for et in self.ecap[h]:
+                E = max(self.ecap[h][et], 1)
+                spec[f"rp{h}{et}"] = (self.cap[h][et[2]] + 1, i32)
+                spec[f"col{h}{et}"] = (E, i32)
+                if h < L - 1:
+                    # the inner blocks' CSC + K2 weights (the outermost block reads the feature
+                    # tables, which take no gradient: it has no backward gather)
+                    spec[f"crp{h}{et}"] = (self.cap[h + 1][et[0]] + 1, i32)
+                    spec[f"ccol{h}{et}"] = (E, i32)
+                    spec[f"cperm{h}{et}"] = (E, i32)
+                    spec[f"cw{h}{et}"] = (E, f32)
+        # the outermost block's destinations (level L - 1): global ids and their feature rows
+        for t, n in self.cap[L - 1].items():
+            spec[f"root_ids{t}"] = (n, i32)
+            spec[f"root_x{t}"] = (n * int(x_dict[t].shape[1]), x_dict[t].dtype)
+        self.arena = _Arena(spec, smp.device)
         self.csrs: Optional[List[Dict[EdgeType, RelationCSR]]] = None
+        self._static_calls()
+
+    def _static_calls(self) -> None:
+        """The staging calls' arguments that do not change per batch (the stage buffers, the
+        capacities), built once: a batch then fills five small arrays (its CSR and id
+        pointers, row and entry counts) — prepare's host cost is three ctypes calls."""
+        L, st, dev = self.L, self.arena.stage, self.smp.device
+        lib = N.lib()
+        # pad items: every (hop, relation) in the static layout's order, then the root id lists
+        self._items = [(h, et) for h in range(L) for et in self.ecap[h]]
+        roots = list(self.cap[L - 1])
+        n = len(self._items) + len(roots)
+        if n > 16:
+            raise ValueError(f"{n} padded items: hgnn_pad_csr_multi takes at most 16")
+        outer = [h == L - 1 for h, _ in self._items]
+        self._pad_var = [(N._p * n)(), (N._p * n)(), (N._p * n)(), (N._c_i64 * n)(),
+                         (N._c_i64 * n)()]                     # rowptr, col, map, n_dst, E
+        self._pad_static = (
+            N.ptr_array([st[f"rp{h}{et}"] for h, et in self._items] + [None] * len(roots)),
+            N.ptr_array([st[f"col{h}{et}"] for h, et in self._items]
+                        + [st[f"root_ids{t}"] for t in roots]),
+            N.i64_array([self.cap[h][et[2]] for h, et in self._items] + [-1] * len(roots)),
+            N.i64_array([self.ecap[h][et] for h, et in self._items]
+                        + [self.cap[L - 1][t] for t in roots]),
+            # padding entries read source row 0 of the global table (outermost block: no
+            # transposed grouping is built for it) or, in turn, the `slack` padded rows at the
+            # end of the level-(h+1) table (its backward's CSC then has no long row)
+            N.int_array([0 if o else self.cap[h + 1][et[0]] - self.slack
+                         for (h, et), o in zip(self._items, outer)] + [0] * len(roots)),
+            N.int_array([1 if o else self.slack for o in outer] + [1] * len(roots)))
+        self._n_pad = n
+        # the root rows: one gather of every type's rows
+        dims = {int(self.x_dict[t].shape[1]) for t in roots}
+        if len(dims) != 1 or any(self.x_dict[t].dtype != torch.float32 for t in roots):
+            raise ValueError("static blocks: the feature tables must be fp32 of one width")
+        self._rows_args = (len(roots), N.ptr_array([self.x_dict[t] for t in roots]),
+                           N.ptr_array([st[f"root_ids{t}"] for t in roots]),
+                           N.i64_array([self.cap[L - 1][t] for t in roots]), dims.pop(),
+                           N.ptr_array([st[f"root_x{t}"] for t in roots]))
+        # the inner blocks' CSCs: one hgnn_csr_transpose_multi per inner hop, static workspace
+        self._csc_args = []
+        for h in range(L - 1):
+            ets = list(self.ecap[h])
+            Es = [self.ecap[h][et] for et in ets]
+            ncols = [self.cap[h + 1][et[0]] for et in ets]
+            ws = torch.empty(max(int(lib.hgnn_csr_transpose_multi_ws_bytes(sum(Es), sum(ncols))),
+                                 256), dtype=torch.uint8, device=dev)
+            self._csc_args.append((ws, (
+                len(ets), N.ptr_array([st[f"rp{h}{et}"] for et in ets]),
+                N.ptr_array([st[f"col{h}{et}"] for et in ets]),
+                N.i64_array([self.cap[h][et[2]] for et in ets]), N.i64_array(Es),
+                N.i64_array(ncols), N.ptr_array([st[f"crp{h}{et}"] for et in ets]),
+                N.ptr_array([st[f"ccol{h}{et}"] for et in ets]),
+                N.ptr_array([st[f"cperm{h}{et}"] for et in ets]),
+                N.ptr_array([st[f"cw{h}{et}"] for et in ets]), ws.data_ptr(), ws.numel())))
+
+    def rowptr(self, h: int, et: EdgeType, which: str = "live") -> torch.Tensor:
+        return getattr(self.arena, which)[f"rp{h}{et}"]
+
+    def col(self, h: int, et: EdgeType, which: str = "live") -> torch.Tensor:
+        return getattr(self.arena, which)[f"col{h}{et}"][:self.ecap[h][et]]
+
+    def root_rows(self, t: str, which: str = "live") -> torch.Tensor:
+        return getattr(self.arena, which)[f"root_x{t}"].view(self.cap[self.L - 1][t], -1)
 
     # -- per batch ---------------------------------------------------------------------------
-    def load(self, mb: MiniBatch) -> None:
-        """The batch's blocks into the fixed buffers: one launch, no sync."""
+    def prepare(self, mb: MiniBatch) -> None:
+        """The batch into the STAGE buffers on the current stream (no sync): the padded CSRs
+        and root ids (one launch), the root rows (one launch) and the inner blocks' CSCs (one
+        launch per inner hop).  ``commit()`` makes them the live ones."""
         if len(mb.blocks) != self.L:
             raise ValueError(f"{len(mb.blocks)} blocks for {self.L} static levels")
         seeds = mb.nodes[-1]
@@ -110,62 +237,61 @@ class StaticBlocks:
             raise ValueError(f"batch seeds {got} differ from the captured {self.n_seeds} "
                              "(partial_seeds=False)")
         L = self.L
-        rp, col, mp, nd, e, rpo, colo, dcap, ecap, dummy, spread = ([] for _ in range(11))
-        for h in range(L):
+        rp, col, mp, nd, e = self._pad_var
+        for i, (h, et) in enumerate(self._items):
             blk = mb.blocks[L - 1 - h]
-            if set(blk.csr) != set(self.ecap[h]):
+            c = blk.csr.get(et)
+            if c is None or len(blk.csr) != len(self.ecap[h]):
                 raise ValueError(f"hop {h}: relations {sorted(blk.csr)} differ from the static "
                                  f"layout {sorted(self.ecap[h])}")
-            for et, c in blk.csr.items():
-                rp.append(c.fwd.rowptr)
-                col.append(c.fwd.col if c.num_edges else None)
-                outer = h == L - 1
-                mp.append(mb.nodes[0][et[0]] if outer else None)   # local -> global ids
-                nd.append(c.n_dst)
-                e.append(c.num_edges)
-                rpo.append(self.rowptr[h][et])
-                colo.append(self.col[h][et])
-                dcap.append(self.cap[h][et[2]])
-                ecap.append(self.ecap[h][et])
-                # padding entries read source row 0 of the global table (outermost block: no
-                # transposed grouping is built for it) or, in turn, the `slack` padded rows at
-                # the end of the level-(h+1) table (its backward's CSC then has no long row)
-                dummy.append(0 if outer else self.cap[h + 1][et[0]] - self.slack)
-                spread.append(1 if outer else self.slack)
-        for t, ids in self.root_ids.items():
+            rp[i] = c.fwd.rowptr.data_ptr()
+            col[i] = c.fwd.col.data_ptr() if c.num_edges else None
+            # the outermost block's local source ids -> global ids
+            mp[i] = mb.nodes[0][et[0]].data_ptr() if h == L - 1 else None
+            nd[i] = c.n_dst
+            e[i] = c.num_edges
+        for i, t in enumerate(self.cap[L - 1], len(self._items)):
             src = mb.nodes[1][t]                                   # level L - 1 (nodes reversed)
-            rp.append(None)
-            col.append(src if src.numel() else None)
-            mp.append(None)
-            nd.append(0)
-            e.append(int(src.numel()))
-            rpo.append(None)
-            colo.append(ids)
-            dcap.append(-1)
-            ecap.append(int(ids.numel()))
-            dummy.append(0)
-            spread.append(1)
-        n = len(rp)
-        N.check(N.lib().hgnn_pad_csr_multi(
-            n, N.ptr_array(rp), N.ptr_array(col), N.ptr_array(mp), N.i64_array(nd),
-            N.i64_array(e), N.ptr_array(rpo), N.ptr_array(colo), N.i64_array(dcap),
-            N.i64_array(ecap), N.int_array(dummy), N.int_array(spread),
-            N.stream_ptr(self.smp.device)),
-            "hgnn_pad_csr_multi")
+            rp[i] = mp[i] = None
+            col[i] = src.data_ptr() if src.numel() else None
+            nd[i] = 0
+            e[i] = int(src.numel())
+        self.arena.wait_committed()
+        lib, s = N.lib(), N.stream_ptr(self.smp.device)
+        rpo, colo, dcap, ecap, dummy, spread = self._pad_static
+        N.check(lib.hgnn_pad_csr_multi(self._n_pad, rp, col, mp, nd, e, rpo, colo, dcap, ecap,
+                                       dummy, spread, s), "hgnn_pad_csr_multi")
+        N.check(lib.hgnn_gather_rows_multi(*self._rows_args, s), "hgnn_gather_rows_multi")
+        for _, args in self._csc_args:
+            N.check(lib.hgnn_csr_transpose_multi(*args, s), "hgnn_csr_transpose_multi")
+
+    def commit(self) -> None:
+        """The prepared batch becomes the live one: one device copy on the current stream."""
+        self.arena.commit()
+
+    def load(self, mb: MiniBatch) -> None:
+        """``prepare`` + ``commit`` on the current stream."""
+        self.prepare(mb)
+        self.commit()
 
     def make_csrs(self) -> None:
-        """Fresh relation objects over the buffers (their CSC / 1/deg are built on first use:
-        inside the graph when this runs right before capture)."""
-        out = []
+        """Relation objects over the LIVE buffers, their CSCs and K2 weights set to the live
+        ones (nothing of them is built inside a recorded step)."""
+        out, lv = [], self.arena.live
         for h in range(self.L):
             outer = h == self.L - 1
-            csrs = {et: RelationCSR.from_csr(
-                self.rowptr[h][et], self.col[h][et][:self.ecap[h][et]],
-                self.smp.num_nodes[et[0]] if outer else self.cap[h + 1][et[0]],
-                self.cap[h][et[2]], may_have_heavy_rows=False) for et in self.ecap[h]}
-            group = [weakref.ref(c) for c in csrs.values()]
-            for c in csrs.values():
-                c._csc_group = group
+            csrs = {}
+            for et in self.ecap[h]:
+                n_src = self.smp.num_nodes[et[0]] if outer else self.cap[h + 1][et[0]]
+                E = self.ecap[h][et]
+                c = RelationCSR.from_csr(self.rowptr(h, et), self.col(h, et), n_src,
+                                         self.cap[h][et[2]], may_have_heavy_rows=False)
+                if not outer:
+                    c._bwd = GroupedEdges(lv[f"crp{h}{et}"], lv[f"ccol{h}{et}"][:E],
+                                          lv[f"cperm{h}{et}"][:E],
+                                          Plan(NO_SPLIT, 0, 0, None, None), n_src)
+                    c._bwd_w = lv[f"cw{h}{et}"][:E]
+                csrs[et] = c
             out.append(csrs)
         self.csrs = out
 
@@ -177,10 +303,13 @@ class StaticBlocks:
         if len(model.layers) != self.L:
             raise ValueError(f"{len(model.layers)}-layer model on {self.L} static levels")
         L = self.L
+        if any(x_dict[t] is not v for t, v in self.x_dict.items()):
+            raise ValueError("StaticBlocks.forward: other feature tables than the staged root "
+                             "rows were gathered from")
         # outermost block: relations gather the global tables; roots are their own input
         h_in = {t: x_dict[t] for t in self.smp.num_nodes}
-        for t, ids in self.root_ids.items():
-            h_in[f"{t}@root"] = x_dict[t].index_select(0, ids)
+        for t in self.cap[L - 1]:
+            h_in[f"{t}@root"] = self.root_rows(t)
         h: Dict[str, torch.Tensor] = {}
         for li in range(L):
             hop = L - 1 - li
@@ -245,7 +374,7 @@ class CapturedStep:
                                  "off to replay around an eager all-reduce")
         if partial_seeds is None:
             partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
-        self.blocks = StaticBlocks(smp, n_seeds, slack, partial_seeds=partial_seeds)
+        self.blocks = StaticBlocks(smp, n_seeds, x_dict, slack, partial_seeds=partial_seeds)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
@@ -307,11 +436,25 @@ class CapturedStep:
         else:
             self.model.zero_grad(set_to_none=True)
 
-    def step(self, mb: MiniBatch) -> torch.Tensor:
-        """``mb`` through the recorded step (queued, no sync); returns the static loss tensor."""
+    def prepare(self, mb: MiniBatch, *loss_args) -> None:
+        """The next batch into the staging buffers on the current stream (a side stream under
+        the running replay, say): the blocks, and ``loss_fn.prepare(*loss_args)`` if given."""
+        self.blocks.prepare(mb)
+        if loss_args:
+            self.loss_fn.prepare(*loss_args)
+
+    def step(self, mb: Optional[MiniBatch] = None) -> torch.Tensor:
+        """One recorded step (queued, no sync) on ``mb`` — or, with no argument, on the batch
+        last ``prepare``d: the staged inputs committed (one copy each for the blocks and a
+        loss with a ``commit``), then the replay.  Returns the static loss tensor."""
         if self.graph is None:
             raise RuntimeError("CapturedStep.step before capture()")
-        self.blocks.load(mb)
+        if mb is not None:
+            self.blocks.prepare(mb)
+        self.blocks.commit()
+        commit = getattr(self.loss_fn, "commit", None)
+        if commit is not None:
+            commit()
         self.graph.replay()
         if self.graph_opt is not None:
             self.between()
@@ -321,16 +464,19 @@ class CapturedStep:
 
 # ----------------------------------------------------------------------------- link batches
 class _LossCSR:
-    """The grouping ``ops._edge_bce`` reads for a link batch: ``bwd`` = the positive pairs by
-    user (built outside the step), ``fwd`` = the same pairs by post (the transposed grouping of
-    a ``from_csr`` relation: one ``hgnn_csr_transpose`` on first use, no host sync)."""
+    """The groupings ``ops._edge_bce`` reads for a link batch, over a ``LinkLoss``'s live
+    buffers: ``bwd`` = the positive pairs by user, ``fwd`` = the same pairs by post (the staged
+    transpose; nothing is built inside a recorded step)."""
 
-    def __init__(self, rowptr_u, col_p, uop, n_users: int, n_posts: int):
-        self._rel = RelationCSR.from_csr(rowptr_u, col_p, n_posts, n_users,
+    def __init__(self, lv, n_users: int, n_posts: int):
+        E = int(lv["col"].numel())
+        self._rel = RelationCSR.from_csr(lv["rowptr"], lv["col"], n_posts, n_users,
                                          may_have_heavy_rows=False)
+        self._rel._bwd = GroupedEdges(lv["p_rowptr"], lv["p_users"], lv["p_perm"],
+                                      Plan(NO_SPLIT, 0, 0, None, None), n_posts)
         self.n_src, self.n_dst = int(n_users), int(n_posts)
-        self.num_edges = int(col_p.numel())
-        self._uop = uop
+        self.num_edges = E
+        self._uop = lv["uop"]
 
     @property
     def fwd(self):
@@ -345,39 +491,67 @@ class LinkLoss:
     """The reference's loss (train_gnn.py:259-281: BCE-with-logits means over the positive
     edges and over one uniform negative post per positive, unit edge weights) on a link
     mini-batch, through the library's fused loss kernels (``ops._EdgeBCELoss``) over fixed-size
-    buffers: ``load(pu, pp, pn)`` (local user / post ids of the positives, local post ids of the
-    negatives; no sync) groups the pairs by user into them, ``make_csr()`` makes fresh
-    structures over them (their post grouping is built on first use: inside a capture, per
-    replay).  ``n_total`` = the positives of ALL ranks, so per-rank losses add up to the global
-    batch's mean (data-parallel gradients are summed).  It reads the seed rows by local id, so
-    a batch with fewer distinct endpoints than the capacity is fine (``partial_seeds``)."""
+    buffers (an ``_Arena``, live + stage, as ``StaticBlocks``).  ``prepare(pu, pp, pn)`` (local
+    user / post ids of the positives, local post ids of the negatives; no sync) writes the
+    stage in one call (``hgnn_link_group``): the pairs grouped by user, the same pairs grouped
+    by post and the negatives grouped by post (the dP gather's order) — every structure the
+    loss needs, so none is built inside a recorded step; ``commit()`` makes them live (one
+    copy); ``load`` = both.  ``n_total`` = the positives of ALL ranks, so per-rank
+    losses add up to the global batch's mean (data-parallel gradients are summed).  It reads the
+    seed rows by local id, so a batch with fewer distinct endpoints than the capacity is fine
+    (``partial_seeds``)."""
 
     partial_seeds = True
 
     def __init__(self, n_edges: int, n_users: int, n_posts: int, device, n_total: int = 0):
-        i32 = dict(dtype=torch.int32, device=device)
         self.E, self.n_users, self.n_posts = int(n_edges), int(n_users), int(n_posts)
         self.n_total = int(n_total) if n_total else self.E
-        self.rowptr = torch.zeros(self.n_users + 1, **i32)
-        self.col = torch.zeros(self.E, **i32)
-        self.neg = torch.zeros(self.E, **i32)
-        self.uop = torch.zeros(self.E, **i32)
-        self.cscale = torch.ones((), dtype=torch.float32, device=device)
+        self.device = torch.device(device)
+        i32, E = torch.int32, self.E
+        self.arena = _Arena({"rowptr": (self.n_users + 1, i32), "col": (E, i32),
+                             "neg": (E, i32), "uop": (E, i32),
+                             "p_rowptr": (self.n_posts + 1, i32), "p_users": (E, i32),
+                             "p_perm": (E, i32), "n_rowptr": (self.n_posts + 1, i32),
+                             "n_users": (E, i32)}, self.device)
+        self.cscale = torch.ones((), dtype=torch.float32, device=self.device)
         self.csr: Optional[_LossCSR] = None
+        self.presorted = None
+        st = self.arena.stage
+        self._stage_ptrs = tuple(st[k].data_ptr() for k in (
+            "rowptr", "col", "neg", "uop", "p_rowptr", "p_users", "p_perm", "n_rowptr",
+            "n_users"))
+        self._ws = torch.empty(max(int(N.lib().hgnn_link_group_ws_bytes(self.E)), 256),
+                               dtype=torch.uint8, device=self.device)
 
-    def load(self, pu: torch.Tensor, pp: torch.Tensor, pn: torch.Tensor) -> None:
+    # the live buffers under their round-5 names
+    rowptr = property(lambda self: self.arena.live["rowptr"])
+    col = property(lambda self: self.arena.live["col"])
+    neg = property(lambda self: self.arena.live["neg"])
+    uop = property(lambda self: self.arena.live["uop"])
+
+    def prepare(self, pu: torch.Tensor, pp: torch.Tensor, pn: torch.Tensor) -> None:
         if int(pu.numel()) != self.E:
             raise ValueError(f"{int(pu.numel())} positives for a {self.E}-edge link loss")
-        order = torch.argsort(pu, stable=True)
-        cnt = torch.zeros(self.n_users + 1, dtype=torch.int64, device=pu.device)
-        cnt.scatter_add_(0, pu.to(torch.int64) + 1, torch.ones_like(pu, dtype=torch.int64))
-        self.rowptr.copy_(torch.cumsum(cnt, 0))
-        self.col.copy_(pp[order])
-        self.neg.copy_(pn[order])
-        self.uop.copy_(pu[order])
+        pu, pp, pn = (t.to(torch.int32).contiguous() for t in (pu, pp, pn))
+        st = self.arena.stage
+        self.arena.wait_committed()
+        N.check(N.lib().hgnn_link_group(
+            N.ptr(pu), N.ptr(pp), N.ptr(pn), self.E, self.n_users, self.n_posts,
+            *self._stage_ptrs, self._ws.data_ptr(), self._ws.numel(),
+            N.stream_ptr(self.device)), "hgnn_link_group")
+
+    def commit(self) -> None:
+        self.arena.commit()
+
+    def load(self, pu: torch.Tensor, pp: torch.Tensor, pn: torch.Tensor) -> None:
+        self.prepare(pu, pp, pn)
+        self.commit()
 
     def make_csr(self) -> None:
-        self.csr = _LossCSR(self.rowptr, self.col, self.uop, self.n_users, self.n_posts)
+        lv = self.arena.live
+        self.csr = _LossCSR(lv, self.n_users, self.n_posts)
+        self.presorted = ops.PresortedNegatives(self.csr, lv["neg"], "user", self.n_posts,
+                                                lv["n_rowptr"], lv["n_users"])
 
     def __call__(self, out: Mapping[str, torch.Tensor]) -> torch.Tensor:
         U, P = out["user"], out["post"]
@@ -386,7 +560,9 @@ class LinkLoss:
                              f"{tuple(U.shape)} / {tuple(P.shape)}")
         if self.csr is None:
             self.make_csr()
-        return ops._EdgeBCELoss.apply(U, P, self.csr, self.neg, self.cscale, False, self.n_total)
+        return ops._EdgeBCELoss.apply(U, P, self.csr, self.arena.live["neg"], self.cscale,
+                                      False, self.n_total, None,
+                                      self.presorted if self.E else None)
 
 
 @dataclasses.dataclass
@@ -399,7 +575,7 @@ class LinkBatch:
     pos_p: torch.Tensor
     neg_p: torch.Tensor
     seeds: Dict[str, torch.Tensor]
-    pu: torch.Tensor         # local ids [B]
+    pu: torch.Tensor         # local ids [B] (int32)
     pp: torch.Tensor
     pn: torch.Tensor
     mb: Optional[MiniBatch] = None
