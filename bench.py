@@ -104,9 +104,10 @@ def parse(argv=None):
                    help="cfg5 mini-batch: no side-stream sampling of the next batch")
     p.add_argument("--prefetch", action="store_true",
                    help="cfg5 mini-batch: sample the next batch on a side stream under this one")
-    p.add_argument("--prepare-on-main", action="store_true",
-                   help="cfg5 mini-batch: stage the batch's block / loss structures on the main "
-                        "stream right before the replay, not on the side stream after sampling")
+    p.add_argument("--eager-sampler", action="store_true",
+                   help="cfg5 mini-batch: sample with the eager NeighborSampler (host-sized "
+                        "launches, read-backs) and stage its batches, instead of the sync-free "
+                        "LinkSampler")
     p.add_argument("--scale", type=float, default=1.0, help="shrink the config (debug only)")
     p.add_argument("--timer-steps", type=int, default=5,
                    help="steps of the separate per-kernel-event run (0: none)")
@@ -1047,20 +1048,30 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
     ph = _Phases() if os.environ.get("HGNN_CFG5_PHASES") else None
 
-    def sample(b, prep=True):
+    def sample(b, prep=True, eager=False):
+        """Batch b on the side stream (when prefetching): staged by the sync-free LinkSampler
+        (returns lb None), or — eager, before capture, ``--eager-sampler`` — a LinkBatch from
+        link_batch + NeighborSampler.sample, staged by CapturedStep.prepare when ``prep``."""
         gb = (b % max(per_epoch, 1)) * world + rank            # this rank's slice of the order
         ids = order[gb * nb:(gb + 1) * nb].long()
 
         def make():
             if ph:
                 ph.mark(b, "smp0")
+            if static is not None and not eager:
+                with _Phases.host(ph, "sample"):
+                    static.prepare(ids, gb, gen_neg)
+                if ph:
+                    ph.mark(b, "smp1")
+                    ph.mark(b, "prep1")
+                return None
             with _Phases.host(ph, "link_batch"):
                 lb = minibatch.link_batch(pos_ei, ids, cfg.num_posts, generator=gen_neg)
             with _Phases.host(ph, "sample"):
                 lb.mb = s.sample(lb.seeds, seed=gb)
             if ph:
                 ph.mark(b, "smp1")
-            if prep and not args.prepare_on_main:
+            if prep:
                 # the batch's block / loss structures into the staging buffers, on the same
                 # stream as the sampler (the side stream under the running replay)
                 with _Phases.host(ph, "prepare"):
@@ -1109,7 +1120,8 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     def sync():
         parallel.sync_grads(model, env, force=capture_ar)   # no-op at world size 1 otherwise
 
-    captured = None
+    captured = static = None
+    edges_dev = torch.zeros((), dtype=torch.int64, device=dev)   # the LinkSampler's counts
     if use_graph:
         # the capture's two warm-up passes are training steps on batch 0 (then recorded once)
         captured = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_of, opt,
@@ -1118,6 +1130,9 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         lb0 = sample(0, prep=False)[0]
         link_loss.load(lb0.pu, lb0.pp, lb0.pn)
         captured.capture(lb0.mb, warmup=2)
+        if not args.eager_sampler:
+            # every later batch: sampled straight into the staging buffers, no host sync
+            static = minibatch.LinkSampler(captured, pos_ei, cfg.num_posts, link_loss)
 
     def eager(lb):
         link_loss.make_csr()
@@ -1131,25 +1146,18 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         return loss
 
     def step(graph=True):
-        lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
+        staged = graph and static is not None
+        if nxt[0] is not None and (nxt[0][0] is None) != staged:
+            nxt[0] = None                        # a prefetched batch of the other kind
+        lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"], eager=not staged)
         state["b"] += 1
         main = torch.cuda.current_stream(dev)
         if ev is not None:
             main.wait_event(ev)
-        mb = lb.mb
-        state["edges"] += sum(blk.csr[et].num_edges for blk in mb.blocks for et in blk.csr)
-        if args.prepare_on_main:
-            if ev is not None:                   # read on this stream
-                lb.mb.record_stream(main)
-                for t in (lb.pu, lb.pp, lb.pn):
-                    t.record_stream(main)
-            with _Phases.host(ph, "prepare"):
-                if captured is not None:
-                    captured.prepare(lb.mb, lb.pu, lb.pp, lb.pn)
-                else:
-                    link_loss.prepare(lb.pu, lb.pp, lb.pn)
-            if ph:
-                ph.mark(state["b"] - 1, "prep1")
+        if staged:
+            edges_dev.add_(static.edge_count())  # before the commit the next prepare waits on
+        else:
+            state["edges"] += sum(c.num_edges for blk in lb.mb.blocks for c in blk.csr.values())
         if graph and captured is not None:
             if ph:
                 ph.mark(state["b"] - 1, "rep0")
@@ -1165,7 +1173,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
             link_loss.commit()
             loss = eager(lb)
         if side is not None:
-            nxt[0] = sample(state["b"])          # under this step's GPU work
+            nxt[0] = sample(state["b"], eager=not staged)   # under this step's GPU work
         return loss
 
     for _ in range(args.warmup):
@@ -1173,10 +1181,12 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     setup_s = time.perf_counter() - t_setup
     clock = _Clock(dev, sharded, args, local)
     state["edges"] = 0
+    edges_dev.zero_()
     if ph:
         ph.h.clear()
     elapsed, loss = clock.time(step, args.steps)
-    edges = torch.tensor([float(state["edges"])], dtype=torch.float64, device=dev)
+    edges = torch.tensor([float(state["edges"]) + float(edges_dev)], dtype=torch.float64,
+                         device=dev)
     if sharded:
         dist.all_reduce(edges)
     edges = float(edges)
@@ -1195,7 +1205,9 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     kern = _pool_shapes(kern)
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"])
+        lb, ev = nxt[0] if nxt[0] is not None else (None, None)
+        if lb is None:                           # a LinkBatch of the next batch's edges
+            lb, ev = sample(state["b"], prep=False, eager=True)
         if ev is not None:
             ev.synchronize()
         cpu = cpu_baseline_sampled(lb, g.x_dict, rels, cfg, args.cpu_threads)
@@ -1218,6 +1230,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    "batches_per_s": round(world * args.steps / elapsed, 1),
                    "graph_replays_per_step": (None if captured is None else
                                               1 if captured.graph_opt is None else 2),
+                   "graph_nodes": None if captured is None else captured.graph_nodes(),
                    "parallelism": f"data-parallel x{world}" if world > 1 else "single",
                    "execution": ((("one HIP graph replay per step (forward + loss + backward + "
                                    "RCCL gradient all-reduce + Adam) over static-capacity blocks "
@@ -1225,9 +1238,12 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                                    "one HIP graph replay per step over static-capacity blocks "
                                    if world == 1 else "HIP graph replays per step (forward + loss "
                                    "+ backward; eager gradient all-reduce; Adam) over "
-                                   "static-capacity blocks ") + "(sampler eager)")
+                                   "static-capacity blocks ")
+                                  + ("" if static is not None else "(sampler eager)"))
                                  if captured is not None else "eager")
-                   + (", next batch sampled on a side stream" if side is not None else "")},
+                   + (", next batch sampled on a side stream" if side is not None else "")
+                   + (" by the sync-free LinkSampler straight into the staging buffers"
+                      if static is not None else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True),
         "projection": _projection(kern, cfg.name),
         "cpu_baseline": cpu,

@@ -433,6 +433,51 @@ int hgnn_link_group(const int32_t* pu, const int32_t* pp, const int32_t* pn, int
                     int32_t* p_perm, int32_t* n_rowptr, int32_t* n_users_sorted, void* ws,
                     size_t ws_bytes, hgnn_stream_t stream);
 
+/* ---- sync-free static sampling (minibatch.StaticSampler; csrc/sampler_static.hip) ------------
+ * The eager sampler's results (hgnn_sample_hop_count / _fill, hgnn_relabel_multi) followed by
+ * hgnn_pad_csr_multi, written straight into static-capacity buffers with every count kept on
+ * the device, so a batch is queued without a host read-back.  Not in the reference (it trains
+ * full-batch, train_gnn.py:254); it feeds the captured cfg5 step.
+ *
+ * hgnn_link_seeds: a link batch (minibatch.link_batch): the B <= 2048 positives edge_ids into the
+ * (src, dst) rows of the positive relation and their negatives neg[B] (int64 ids < 2^31 - 1);
+ * seeds_u[B] / seeds_p[2B] = the distinct users / posts (positives' posts and negatives)
+ * ascending, d_counts[2] = their numbers, pu / pp / pn[B] = each pair's local ids (ranks). */
+int hgnn_link_seeds(const int64_t* src, const int64_t* dst, const int64_t* edge_ids,
+                    const int64_t* neg, int64_t B, int32_t* seeds_u, int32_t* seeds_p,
+                    int32_t* pu, int32_t* pp, int32_t* pn, int32_t* d_counts,
+                    hgnn_stream_t stream);
+
+/* One hop of n_rel (<= 8) relations, fanout 1..64: relation r samples the first *d_n_dst[r] ids
+ * of dst_ids[r] (global CSR rowptrs[r] / cols[r] over n_rows[r] destinations; the count lives on
+ * the device, caps[r] bounds it and leaves >= 1 padded row) exactly as hgnn_sample_hop_fill with
+ * `seed`: out_rowptrs[r][caps[r] + 1] = the real rows then padded rows spread as
+ * hgnn_pad_csr_multi does, fill_outs[r] = the sampled global source ids in CSR order,
+ * tail_outs[r][E .. ecaps[r]) = padding entries dummy[r] + (k mod spread[r]), d_E[r] = E.
+ * ws: hgnn_sample_hop_ws_bytes(sum of caps). */
+int hgnn_sample_hop_static(int32_t n_rel, const int32_t* const* rowptrs,
+                           const int32_t* const* cols, const int64_t* n_rows,
+                           const int32_t* const* dst_ids, const int32_t* const* d_n_dst,
+                           const int64_t* caps, const int64_t* ecaps, int32_t fanout,
+                           uint64_t seed, int32_t* const* out_rowptrs, int32_t* const* fill_outs,
+                           int32_t* const* tail_outs, const int32_t* dummy,
+                           const int32_t* spread, int32_t* d_E, void* ws, size_t ws_bytes,
+                           hgnn_stream_t stream);
+
+/* hgnn_relabel_multi over capacity layouts: type ty's prefix = the first *d_n_prefix[ty] ids of
+ * prefix[ty]; the items are n_irel (<= 8) relations' runs, relation q in slots item_caps[q] long
+ * (consecutive, grouped by source type irel_type[q] ascending), its first d_E[q] valid.  Writes
+ * nodes_out[ty] (zeroed past the count up to nodes_caps[ty]), each valid item's local id into
+ * local_out[q], d_count[ty] = the node counts.  ws: hgnn_relabel_static_ws_bytes(sum of
+ * prefix_caps, sum of item_caps). */
+size_t hgnn_relabel_static_ws_bytes(int64_t prefix_cap_total, int64_t item_cap_total);
+int hgnn_relabel_static(int32_t n_types, const int32_t* const* prefix,
+                        const int32_t* const* d_n_prefix, const int64_t* prefix_caps,
+                        int32_t* const* nodes_out, const int64_t* nodes_caps, int32_t n_irel,
+                        const int32_t* items, const int64_t* item_caps, const int32_t* irel_type,
+                        const int32_t* d_E, int32_t* const* local_out, int32_t* d_count,
+                        void* ws, size_t ws_bytes, hgnn_stream_t stream);
+
 /* ---- ranking metrics of the evaluation (train_gnn.py:289-367), batched ----------------------
  * scores [n_rows][ld]: one row per test user over the n_cand sorted test candidates (a GEMM of
  * user and candidate embeddings, computed by the caller).  Per row:

@@ -256,6 +256,9 @@ def test_captured_link_step_matches_reference_loss():
     lb0 = batch(0)
     ll.load(lb0.pu, lb0.pp, lb0.pn)
     step.capture(lb0.mb)
+    nodes = step.graph_nodes()                    # the recorded step, by node kind
+    assert nodes["kernel"] >= 20 and nodes["total"] == sum(
+        nodes[k] for k in ("kernel", "memcpy", "memset", "other"))
     for b in (1, 2, 6):
         lb = batch(b)
         ll.load(lb.pu, lb.pp, lb.pn)
@@ -400,3 +403,50 @@ def test_captured_link_step_prepared_on_a_side_stream():
         assert abs(got_loss - float(ref)) <= 2e-6 * abs(float(ref)), (b, got_loss, float(ref))
         for n, p in ref_model.named_parameters():
             _close(got[n], p.grad, n)
+
+
+def test_link_sampler_stages_what_the_eager_sampler_stages():
+    """The sync-free LinkSampler (round 6: device-side counts, no read-back) against link_batch
+    + NeighborSampler.sample + CapturedStep.prepare on the same edges, draws and seed: every
+    staged byte — padded block CSRs, root ids and rows, the inner CSCs and 1/deg, the loss
+    groupings — equal, and the sampled edge count equal; then a replay on it gives the reference
+    loss."""
+    from truth_recommendation_gnn_amd import minibatch, sampler
+    g, s, _, make_model, ei, P, n_seeds = _link_setup()
+    B = n_seeds["user"]
+    model = make_model()
+    ll = minibatch.LinkLoss(B, n_seeds["user"], n_seeds["post"], DEV)
+    step = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, ll, None, slack=16)
+    ls = minibatch.LinkSampler(step, ei, P)
+    order = torch.randperm(int(ei.shape[1]), device=DEV,
+                           generator=torch.Generator(device=DEV).manual_seed(7))
+    barena, larena = step.blocks.arena._bytes["stage"], ll.arena._bytes["stage"]
+    for b in range(4):
+        ids = order[b * B:(b + 1) * B]
+        lb = minibatch.link_batch(ei, ids, P,
+                                  generator=torch.Generator(device=DEV).manual_seed(100 + b))
+        lb.mb = s.sample(lb.seeds, seed=b)
+        step.prepare(lb.mb, lb.pu, lb.pp, lb.pn)
+        want_b, want_l = barena.clone(), larena.clone()
+        barena.fill_(0x5A)
+        larena.fill_(0x5A)
+        ls.prepare(ids, b, torch.Generator(device=DEV).manual_seed(100 + b))
+        torch.cuda.synchronize()
+        for name, (o, n, dt, nb) in step.blocks.arena.layout.items():
+            assert torch.equal(barena[o:o + nb], want_b[o:o + nb]), (b, name)
+        for name, (o, n, dt, nb) in ll.arena.layout.items():
+            assert torch.equal(larena[o:o + nb], want_l[o:o + nb]), (b, name)
+        assert int(ls.edge_count()) == sum(c.num_edges for blk in lb.mb.blocks
+                                           for c in blk.csr.values())
+    # one captured step over LinkSampler-staged batches
+    lb0 = minibatch.link_batch(ei, order[:B], P)
+    lb0.mb = s.sample(lb0.seeds, seed=0)
+    ll.load(lb0.pu, lb0.pp, lb0.pn)
+    step.capture(lb0.mb)
+    ids = order[5 * B:6 * B]
+    ls.prepare(ids, 5, torch.Generator(device=DEV).manual_seed(9))
+    got = float(step.step())
+    lb = minibatch.link_batch(ei, ids, P, generator=torch.Generator(device=DEV).manual_seed(9))
+    lb.mb = s.sample(lb.seeds, seed=5)
+    ref = _ref_link_loss(sampler.forward_blocks(model, lb.mb, g.x_dict), lb)
+    assert abs(got - float(ref)) <= 2e-6 * abs(float(ref)), (got, float(ref))

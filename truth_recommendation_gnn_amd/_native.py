@@ -92,6 +92,12 @@ _SIGS = {
     "hgnn_set_k3_split": (_c_i32, [_c_i32]),
     "hgnn_pad_csr_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "hgnn_gather_rows_multi": (_c_i32, [_c_i32, _p, _p, _p, _c_i64, _p, _p]),
+    "hgnn_link_seeds": (_c_i32, [_p, _p, _p, _p, _c_i64, _p, _p, _p, _p, _p, _p, _p]),
+    "hgnn_sample_hop_static": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _c_i32,
+                                        ctypes.c_uint64, _p, _p, _p, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_relabel_static_ws_bytes": (_c_sz, [_c_i64, _c_i64]),
+    "hgnn_relabel_static": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _c_i32, _p, _p, _p, _p, _p, _p,
+                                     _p, _c_sz, _p]),
     "hgnn_link_group_ws_bytes": (_c_sz, [_c_i64]),
     "hgnn_link_group": (_c_i32, [_p, _p, _p, _c_i64, _c_i64, _c_i64, _p, _p, _p, _p, _p, _p, _p,
                                  _p, _p, _p, _c_sz, _p]),

@@ -18,62 +18,15 @@
 //                   over the ids of this call (O(items) work, independent of the graph's node
 //                   count), atomicMin for the first appearance and one exclusive scan, so the
 //                   result is deterministic.
-#include "hgnn_common.h"
+#include "sampler_common.h"
 
 namespace hgnn {
-
-constexpr int kHopMax = 8;   // relations per hop (hgnn_sample_hop_*)
-
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-// uniform integer in [0, m) from the draw (seed, node, r); Lemire's multiply-shift
-__device__ __forceinline__ uint32_t draw(uint64_t seed, int32_t node, int r, uint32_t m) {
-  const uint64_t h = splitmix64(seed * 0xD1B54A32D192ED03ull + ((uint64_t)(uint32_t)node << 8) +
-                                (uint64_t)r);
-  return (uint32_t)(((h >> 32) * (uint64_t)m) >> 32);
-}
-
-// A destination id outside [0, n_rows) has no neighbours (count 0): the caller validates the ids
-// it was given with the first read-back it makes anyway, and nothing is read out of bounds.
-__device__ __forceinline__ int32_t sample_count(const int32_t* rowptr, int64_t n_rows, int32_t d,
-                                                int32_t fanout) {
-  if (d < 0 || d >= n_rows) return 0;
-  const int32_t deg = rowptr[d + 1] - rowptr[d];
-  return (fanout < 0 || deg <= fanout) ? deg : fanout;
-}
 
 __global__ void k_sample_count(const int32_t* rowptr, int64_t n_rows, const int32_t* dst_ids,
                                int64_t n, int32_t fanout, int32_t* counts) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   counts[i] = sample_count(rowptr, n_rows, dst_ids[i], fanout);
-}
-
-// One wave: the sample of destination d into out[0 .. count).
-__device__ __forceinline__ void sample_fill(const int32_t* rowptr, const int32_t* col,
-                                            int64_t n_rows, int32_t d, int32_t fanout,
-                                            uint64_t seed, int32_t* out) {
-  const int lane = threadIdx.x & 63;
-  if (d < 0 || d >= n_rows) return;   // counted 0
-  const int32_t beg = rowptr[d], deg = rowptr[d + 1] - beg;
-  if (fanout < 0 || deg <= fanout) {   // keep every neighbour, in CSR order
-    for (int32_t j = lane; j < deg; j += 64) out[j] = col[beg + j];
-    return;
-  }
-  // Floyd: for jj = deg-k .. deg-1 draw t in [0, jj]; take t unless already taken, then jj
-  int32_t chosen = -1;
-  for (int r = 0; r < fanout; ++r) {
-    const int32_t jj = deg - fanout + r;
-    const int32_t t = (int32_t)draw(seed, d, r, (uint32_t)jj + 1u);
-    const bool taken = __ballot(lane < r && chosen == t) != 0ull;
-    if (lane == r) chosen = taken ? jj : t;
-  }
-  if (lane < fanout) out[lane] = col[beg + chosen];
 }
 
 __global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, const int32_t* col,
@@ -164,29 +117,6 @@ __device__ __forceinline__ int rl_type(const int64_t* off, int T, int64_t i) {
   return t;
 }
 
-// slot of `key`; *found = the key was already in the table (inserted by another thread)
-__device__ __forceinline__ uint32_t rl_find_or_insert(const RelabelTab& t, int32_t key,
-                                                      bool* found = nullptr) {
-  uint32_t s = (uint32_t)(((uint64_t)(uint32_t)key * 0x9E3779B97F4A7C15ull) >> t.shift);
-  for (uint32_t probe = 0; probe <= t.mask; ++probe) {   // ends: load factor <= 1/2
-    const int32_t k = __atomic_load_n(&t.key[s], __ATOMIC_RELAXED);
-    if (k == key) {
-      if (found) *found = true;
-      return s;
-    }
-    if (k == -1) {
-      const int32_t old = atomicCAS(&t.key[s], -1, key);
-      if (old == -1) return s;
-      if (old == key) {
-        if (found) *found = true;
-        return s;
-      }
-    }
-    s = (s + 1) & t.mask;
-  }
-  return 0;   // unreachable with the capacity the host sizes
-}
-
 // Prefix ids (the previous frontier, or the seeds) are expected distinct and in range: with the
 // check on, a repeated id (found already inserted) clears bit 0 of its type's nflags word, an id
 // outside [0, id_limit) bit 1 (that id is not inserted) — read back with the node counts.
@@ -202,7 +132,7 @@ __global__ void k_relabel_prefix(RelabelTab t) {
     return;
   }
   bool found = false;
-  const uint32_t s = rl_find_or_insert(t, id * t.T + ty, &found);
+  const uint32_t s = rl_find_or_insert(t.key, t.mask, t.shift, id * t.T + ty, &found);
   if (found && t.nflags) atomicAnd(&t.nflags[ty], ~1);
   t.ppos[s] = (int32_t)i;   // one writer per slot when the prefix ids are distinct
 }
@@ -211,7 +141,7 @@ __global__ void k_relabel_insert(RelabelTab t, const int32_t* items, int32_t* sl
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= t.i_off[t.T]) return;
   const int ty = rl_type(t.i_off, t.T, k);
-  const uint32_t s = rl_find_or_insert(t, items[k] * t.T + ty);
+  const uint32_t s = rl_find_or_insert(t.key, t.mask, t.shift, items[k] * t.T + ty);
   slot_of[k] = (int32_t)s;
   if (t.ppos[s] < 0) atomicMin(&t.first[s], (int32_t)k);
 }
@@ -249,12 +179,6 @@ __global__ void k_relabel_count(RelabelTab t, const int32_t* rank, int32_t* d_co
   const int stride = t.nflags ? 2 : 1;
   d_count2[stride * ty] = (int32_t)(t.p_off[ty + 1] - t.p_off[ty] + n_new);
   if (t.nflags) d_count2[2 * ty + 1] = ~t.nflags[ty];
-}
-
-static int64_t relabel_cap(int64_t n) {
-  int64_t c = 64;
-  while (c < 2 * n) c <<= 1;
-  return c;
 }
 
 static size_t relabel_ws(int64_t n_prefix, int64_t n_items, size_t* scan_b) {

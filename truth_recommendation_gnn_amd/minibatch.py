@@ -261,6 +261,10 @@ class StaticBlocks:
         rpo, colo, dcap, ecap, dummy, spread = self._pad_static
         N.check(lib.hgnn_pad_csr_multi(self._n_pad, rp, col, mp, nd, e, rpo, colo, dcap, ecap,
                                        dummy, spread, s), "hgnn_pad_csr_multi")
+        self._stage_derived(lib, s)
+
+    def _stage_derived(self, lib, s) -> None:
+        """What follows from the staged CSRs and root ids: the root rows and the CSCs."""
         N.check(lib.hgnn_gather_rows_multi(*self._rows_args, s), "hgnn_gather_rows_multi")
         for _, args in self._csc_args:
             N.check(lib.hgnn_csr_transpose_multi(*args, s), "hgnn_csr_transpose_multi")
@@ -413,11 +417,12 @@ class CapturedStep:
                     self.between()
                     self.opt.step()
         torch.cuda.current_stream(dev).wait_stream(side)
-        self._fresh()                      # fresh: their CSC and 1/deg builds are recorded
+        self._fresh()
         self._zero_grad()
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)   # kept: its nodes are counted (graph_nodes)
         with torch.cuda.graph(g):
             out, loss = self._body(with_opt=not split)
+        g.instantiate()
         # the static outputs without the recorded autograd graph (kept alive, its AccumulateGrad
         # nodes would tie later eager backwards of the same parameters to the capture stream)
         self.out = {t: v.detach() for t, v in out.items()}
@@ -425,10 +430,18 @@ class CapturedStep:
         del out, loss
         self.graph = g
         if split:
-            go = torch.cuda.CUDAGraph()
+            go = torch.cuda.CUDAGraph(keep_graph=True)
             with torch.cuda.graph(go):
                 self.opt.step()
+            go.instantiate()
             self.graph_opt = go
+
+    def graph_nodes(self) -> Optional[Dict[str, int]]:
+        """Nodes of the recorded step's graph(s) by kind (hipGraphGetNodes /
+        hipGraphNodeGetType): kernels, copies, memsets, other."""
+        if self.graph is None:
+            return None
+        return _graph_node_counts([g for g in (self.graph, self.graph_opt) if g is not None])
 
     def _zero_grad(self):
         if self.opt is not None:
@@ -460,6 +473,27 @@ class CapturedStep:
             self.between()
             self.graph_opt.replay()
         return self.loss
+
+
+def _graph_node_counts(graphs) -> Dict[str, int]:
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    kinds = {0: "kernel", 1: "memcpy", 2: "memset"}
+    out = {"total": 0, "kernel": 0, "memcpy": 0, "memset": 0, "other": 0}
+    for g in graphs:
+        raw = ctypes.c_void_p(g.raw_cuda_graph())
+        n = ctypes.c_size_t(0)
+        if hip.hipGraphGetNodes(raw, None, ctypes.byref(n)) != 0:
+            raise RuntimeError("hipGraphGetNodes failed")
+        nodes = (ctypes.c_void_p * max(n.value, 1))()
+        if hip.hipGraphGetNodes(raw, nodes, ctypes.byref(n)) != 0:
+            raise RuntimeError("hipGraphGetNodes failed")
+        for i in range(n.value):
+            kind = ctypes.c_int(-1)
+            hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(kind))
+            out[kinds.get(kind.value, "other")] += 1
+        out["total"] += n.value
+    return out
 
 
 # ----------------------------------------------------------------------------- link batches
@@ -594,3 +628,145 @@ def link_batch(edge_index: torch.Tensor, edge_ids: torch.Tensor, num_posts: int,
     return LinkBatch(pos_u, pos_p, neg_p, {"user": su, "post": sp},
                      torch.searchsorted(su, pos_u), torch.searchsorted(sp, pos_p),
                      torch.searchsorted(sp, neg_p))
+
+
+class LinkSampler:
+    """Link mini-batches sampled straight into a ``CapturedStep``'s staging buffers with no host
+    sync (``csrc/sampler_static.hip``): per batch the negatives (the draws ``link_batch`` makes),
+    the seeds and pair ids (``hgnn_link_seeds``), each hop over the static capacities with the
+    counts kept on the device (``hgnn_sample_hop_static``; the inner hops relabelled by
+    ``hgnn_relabel_static`` into the next frontier, the outermost hop's sources left as global
+    ids), then the root rows, CSCs and loss groupings as ``prepare`` makes them.  The staged
+    bytes equal ``link_batch`` + ``NeighborSampler.sample`` + ``CapturedStep.prepare`` on the
+    same edges, draws and seed (tested), so the replayed step is unchanged; the host only
+    queues ~10 calls (the eager sampler's read-backs made the host loop the
+    cfg5 bound).  ``edge_ids``: the batch's positive edges into ``edge_index`` (int64 [B])."""
+
+    def __init__(self, step: CapturedStep, edge_index: torch.Tensor, num_posts: int,
+                 loss: Optional["LinkLoss"] = None):
+        blocks = step.blocks
+        loss = step.loss_fn if loss is None else loss     # the LinkLoss the step's loss reads
+        smp = blocks.smp
+        if not isinstance(getattr(loss, "arena", None), _Arena) or not hasattr(loss, "n_users"):
+            raise ValueError("LinkSampler stages a LinkLoss (its loss_fn)")
+        if set(blocks.n_seeds) != {"user", "post"} or blocks.n_seeds["post"] != 2 * loss.E \
+                or blocks.n_seeds["user"] != loss.E:
+            raise ValueError("LinkSampler: seeds capacities must be B users and 2B posts")
+        if blocks.L < 2:
+            raise ValueError("LinkSampler: at least two layers (the outermost block's "
+                             "destinations are an inner hop's relabelled frontier)")
+        self.step, self.blocks, self.loss = step, blocks, loss
+        self.edge_index, self.num_posts, self.B = edge_index, int(num_posts), loss.E
+        dev, i32, L = smp.device, torch.int32, blocks.L
+        lib = N.lib()
+        B = self.B
+        self.seeds = {"user": torch.zeros(B, dtype=i32, device=dev),
+                      "post": torch.zeros(2 * B, dtype=i32, device=dev)}
+        self.pairs = torch.zeros(3, B, dtype=i32, device=dev)          # pu, pp, pn
+        self.zero = torch.zeros(2, dtype=i32, device=dev)
+        # per level: node counts per type (level 0: the seed kernel's [users, posts])
+        self.counts = [torch.zeros(max(len(blocks.cap[h]), 2), dtype=i32, device=dev)
+                       for h in range(L)]
+        self.d_E = torch.zeros(L, 8, dtype=i32, device=dev)
+        st = blocks.arena.stage
+        # level h's node buffers (h >= 1): the outermost block's destinations are the staged
+        # root ids; deeper inner levels a scratch buffer each
+        nodes = [dict(self.seeds)]
+        for h in range(1, L):
+            nodes.append({t: st[f"root_ids{t}"] if h == L - 1
+                          else torch.zeros(blocks.cap[h][t], dtype=i32, device=dev)
+                          for t in blocks.cap[h]})
+        self._nodes = nodes
+
+        def cnt(h, t):          # device address of level h's count of type t
+            if h == 0:
+                return self.counts[0][0 if t == "user" else 1]
+            return self.counts[h][sorted(blocks.cap[h]).index(t)]
+        self._hops = []
+        for h, fanout in enumerate(smp.fanouts):
+            lvl = set(blocks.cap[h])
+            types_h = sorted(lvl | {et[0] for et in smp.relations if et[2] in lvl})
+            ets = sorted((et for et in smp.relations if et[2] in lvl),
+                         key=lambda et: types_h.index(et[0]))
+            outer = h == L - 1
+            g = [smp.csr[et].fwd for et in ets]
+            caps = [blocks.cap[h][et[2]] for et in ets]
+            ecaps = [blocks.ecap[h][et] for et in ets]
+            items = None if outer else torch.zeros(max(sum(ecaps), 1), dtype=i32, device=dev)
+            fill = ([st[f"col{h}{et}"] for et in ets] if outer else
+                    [items[o:o + c] for o, c in zip(_offsets(ecaps), ecaps)])
+            ws = torch.empty(max(int(lib.hgnn_sample_hop_ws_bytes(sum(caps))), 256),
+                             dtype=torch.uint8, device=dev)
+            d_E = self.d_E[h]
+            hop = dict(ws=ws, items=items, fanout=fanout, args=(
+                len(ets), N.ptr_array([x.rowptr for x in g]), N.ptr_array([x.col for x in g]),
+                N.i64_array([x.n_rows for x in g]),
+                N.ptr_array([nodes[h][et[2]] for et in ets]),
+                N.ptr_array([cnt(h, et[2]) for et in ets]), N.i64_array(caps),
+                N.i64_array(ecaps)), outs=(
+                N.ptr_array([st[f"rp{h}{et}"] for et in ets]), N.ptr_array(fill),
+                N.ptr_array([st[f"col{h}{et}"] for et in ets]),
+                N.int_array([0 if outer else blocks.cap[h + 1][et[0]] - blocks.slack
+                             for et in ets]),
+                N.int_array([1 if outer else blocks.slack for et in ets]), d_E.data_ptr(),
+                ws.data_ptr(), ws.numel()))
+            if not outer:
+                nxt = sorted(blocks.cap[h + 1])
+                if nxt != types_h:
+                    raise ValueError(f"level {h + 1} types {nxt} differ from the hop's {types_h}")
+                pcaps = [int(nodes[h][t].numel()) if t in lvl else 0 for t in types_h]
+                rws = torch.empty(max(int(lib.hgnn_relabel_static_ws_bytes(sum(pcaps),
+                                                                           sum(ecaps))), 256),
+                                  dtype=torch.uint8, device=dev)
+                hop["rws"] = rws
+                hop["relabel"] = (
+                    len(types_h),
+                    N.ptr_array([nodes[h][t] if t in lvl else self.zero for t in types_h]),
+                    N.ptr_array([cnt(h, t) if t in lvl else self.zero for t in types_h]),
+                    N.i64_array(pcaps), N.ptr_array([nodes[h + 1][t] for t in types_h]),
+                    N.i64_array([blocks.cap[h + 1][t] for t in types_h]), len(ets),
+                    items.data_ptr(), N.i64_array(ecaps),
+                    N.int_array([types_h.index(et[0]) for et in ets]), d_E.data_ptr(),
+                    N.ptr_array([st[f"col{h}{et}"] for et in ets]),
+                    self.counts[h + 1].data_ptr(), rws.data_ptr(), rws.numel())
+            self._hops.append(hop)
+
+    def prepare(self, edge_ids: torch.Tensor, seed: int,
+                generator: Optional[torch.Generator] = None) -> None:
+        """Batch ``seed``'s positives ``edge_ids`` into the staging buffers on the current
+        stream (no sync); ``CapturedStep.step()`` then commits and replays it."""
+        if int(edge_ids.numel()) != self.B:
+            raise ValueError(f"{int(edge_ids.numel())} positives for a {self.B}-pair batch")
+        dev = self.blocks.smp.device
+        eid = edge_ids.to(torch.int64).contiguous()
+        # the negatives exactly as link_batch draws them (same generator, same call)
+        neg = torch.randint(0, self.num_posts, (self.B,), device=dev, generator=generator,
+                            dtype=self.edge_index.dtype)
+        self.blocks.arena.wait_committed()
+        lib, s = N.lib(), N.stream_ptr(dev)
+        ei = self.edge_index
+        pu, pp, pn = self.pairs
+        N.check(lib.hgnn_link_seeds(N.ptr(ei[0]), N.ptr(ei[1]), N.ptr(eid), N.ptr(neg), self.B,
+                                    N.ptr(self.seeds["user"]), N.ptr(self.seeds["post"]),
+                                    N.ptr(pu), N.ptr(pp), N.ptr(pn), N.ptr(self.counts[0]), s),
+                "hgnn_link_seeds")
+        for h, hop in enumerate(self._hops):
+            hop_seed = (int(seed) * 1_000_003 + h) & 0xFFFFFFFFFFFFFFFF   # NeighborSampler's
+            N.check(lib.hgnn_sample_hop_static(*hop["args"], hop["fanout"], hop_seed,
+                                               *hop["outs"], s), "hgnn_sample_hop_static")
+            if "relabel" in hop:
+                N.check(lib.hgnn_relabel_static(*hop["relabel"], s), "hgnn_relabel_static")
+        self.blocks._stage_derived(lib, s)
+        self.loss.prepare(pu, pp, pn)
+
+    def edge_count(self) -> torch.Tensor:
+        """The staged batch's sampled message edges (every hop and relation), on the device."""
+        return self.d_E.sum(dtype=torch.int64)
+
+
+def _offsets(sizes):
+    out, o = [], 0
+    for n in sizes:
+        out.append(o)
+        o += n
+    return out
