@@ -186,6 +186,20 @@ int hgnn_split_weight_grads(int32_t n_rel, const float* dw, const float* db, con
                             int32_t k_root, const float* scale, int32_t h, float* const* dwl,
                             float* const* dwr, float* const* dbl, hgnn_stream_t stream);
 
+/* Both for n_groups (<= 4) destination updates of one layer in one launch: group g's relations
+ * are the flattened entries [base_g, base_g + n_rel[g]) of wl / k / wr / bl / scale (and of
+ * dwl / dwr / dbl), base_g = n_rel[0] + ... + n_rel[g - 1]; w_out[g] / b_out[g] (b_out or its
+ * entries nullable) and dw[g] / db[g] per group, h shared.  Results exactly those of the
+ * single-update calls. */
+int hgnn_fuse_weights_multi(int32_t n_groups, const int32_t* n_rel, const float* const* wl,
+                            const int32_t* k, const float* const* wr, const int32_t* k_root,
+                            const float* const* bl, const float* scale, int32_t h,
+                            float* const* w_out, float* const* b_out, hgnn_stream_t stream);
+int hgnn_split_weight_grads_multi(int32_t n_groups, const int32_t* n_rel, const float* const* dw,
+                                  const float* const* db, const int32_t* k, const int32_t* k_root,
+                                  const float* scale, int32_t h, float* const* dwl,
+                                  float* const* dwr, float* const* dbl, hgnn_stream_t stream);
+
 /* hgnn_linear_fwd_add that also writes the ReLU mask of `out` as bits (relu != 0, h % 32 == 0):
  * bit c % 32 of mask[row * (h / 32) + c / 32] = out[row][c] > 0, 16-B aligned.  The backward
  * (hgnn_linear_bwd_mask) reads h/8 bytes per row instead of out's 4h: autograd's saved ReLU

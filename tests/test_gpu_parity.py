@@ -321,6 +321,36 @@ def test_linear_bwd_dx_accumulate_bitwise(ks, h, masked):
     assert torch.equal(dw0, dw1) and torch.equal(db0, db1)
 
 
+def test_fuse_weights_multi_equals_per_update_calls():
+    """hgnn_fuse_weights_multi / hgnn_split_weight_grads_multi (one launch each way for a
+    layer's updates, round 6) against the per-update calls: three updates of different shapes
+    (root + bias, no root, no bias, a shared parameter), outputs and every gradient bitwise."""
+    gen = torch.Generator().manual_seed(11)
+    h = 48
+    p = lambda *shape: torch.randn(*shape, generator=gen).to(DEV).requires_grad_()  # noqa: E731
+    shared = p(h, 64)
+    groups = [([p(h, 64), p(h, 32)], [p(h, 64), shared], [p(h), p(h)], [1.0, 0.75]),
+              ([p(h, 16)], [None], [p(h)], [0.5]),
+              ([p(h, 64), shared, p(h, 8)], [p(h, 32), p(h, 32), None], [None, None, None],
+               [1.75, 0.7, 0.3])]
+    got = ops.fuse_weights_multi(groups)
+    ref = [ops.fuse_weights(*g) for g in groups]
+    params = list({id(t): t for g in groups for part in g[:3] for t in part
+                   if t is not None}.values())
+    loss, loss_ref = 0, 0
+    for (W, b), (Wr, br) in zip(got, ref):
+        assert torch.equal(W, Wr) and ((b is None and br is None) or torch.equal(b, br))
+        gW = torch.randn(W.shape, generator=gen).to(DEV)
+        loss = loss + (W * gW).sum()
+        loss_ref = loss_ref + (Wr * gW).sum()
+        if b is not None:
+            gb = torch.randn(h, generator=gen).to(DEV)
+            loss = loss + (b * gb).sum()
+            loss_ref = loss_ref + (br * gb).sum()
+    for a, r in zip(torch.autograd.grad(loss, params), torch.autograd.grad(loss_ref, params)):
+        assert torch.equal(a, r)
+
+
 @pytest.mark.parametrize("case", ["rgcn", "author", "no_root", "no_bias", "single"])
 def test_fuse_weights_bitwise_equals_torch_expression(case):
     """hgnn_fuse_weights / hgnn_split_weight_grads against the torch expression they replace

@@ -56,6 +56,10 @@ _SIGS = {
     "hgnn_fuse_weights": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _p, _c_i32, _p, _p, _p]),
     "hgnn_split_weight_grads": (_c_i32, [_c_i32, _p, _p, _p, _c_i32, _p, _c_i32, _p, _p, _p,
                                          _p]),
+    "hgnn_fuse_weights_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, _c_i32, _p, _p,
+                                         _p]),
+    "hgnn_split_weight_grads_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _c_i32, _p, _p,
+                                               _p, _p]),
     "hgnn_linear_bwd_ws_bytes": (_c_sz, [_c_i64, _c_i32, _c_i32]),
     "hgnn_linear_bwd": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p, _p, _p,
                                  _c_sz, _p]),

@@ -9,6 +9,8 @@
 // so both are bitwise what the torch expression gives.
 #include "hgnn_common.h"
 
+#include <algorithm>
+
 namespace hgnn {
 
 constexpr int kMaxRel = HGNN_MAX_SEG - 1;
@@ -29,9 +31,8 @@ struct FuseArgs {
   int32_t h;
 };
 
-__global__ void k_fuse_weights(const FuseArgs a, float* w, float* b) {
+__device__ __forceinline__ void fuse_one(const FuseArgs& a, float* w, float* b, int64_t idx) {
 #pragma clang fp contract(off)   // s_r * W_r and the sum rounded separately, as torch does
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)a.h * a.k_tot;
   if (idx < n) {
     const int j = (int)(idx / a.k_tot), c = (int)(idx % a.k_tot);
@@ -66,9 +67,13 @@ __global__ void k_fuse_weights(const FuseArgs a, float* w, float* b) {
   }
 }
 
-__global__ void k_split_weight_grads(const FuseArgs a, const float* dw, const float* db) {
+__global__ void k_fuse_weights(const FuseArgs a, float* w, float* b) {
+  fuse_one(a, w, b, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+__device__ __forceinline__ void split_one(const FuseArgs& a, const float* dw, const float* db,
+                                          int64_t idx) {
 #pragma clang fp contract(off)
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = (int64_t)a.h * a.k_tot;
   if (idx < n) {
     const int j = (int)(idx / a.k_tot), c = (int)(idx % a.k_tot);
@@ -89,6 +94,31 @@ __global__ void k_split_weight_grads(const FuseArgs a, const float* dw, const fl
     for (int r = 0; r < a.n_rel; ++r)
       if (a.dbl[r]) a.dbl[r][j] = (g * a.scale[r]);
   }
+}
+
+__global__ void k_split_weight_grads(const FuseArgs a, const float* dw, const float* db) {
+  split_one(a, dw, db, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Several destination updates' fused weights (or their adjoints) in one launch: blockIdx.y is
+// the update — a layer's updates are independent, so a layer costs one launch each way.
+constexpr int kMaxFuseGroups = 4;
+struct FuseMulti {
+  FuseArgs g[kMaxFuseGroups];
+  float* w[kMaxFuseGroups];
+  float* b[kMaxFuseGroups];
+  const float* dw[kMaxFuseGroups];
+  const float* db[kMaxFuseGroups];
+};
+
+__global__ void k_fuse_weights_multi(const FuseMulti m) {
+  const int g = blockIdx.y;
+  fuse_one(m.g[g], m.w[g], m.b[g], (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+__global__ void k_split_weight_grads_multi(const FuseMulti m) {
+  const int g = blockIdx.y;
+  split_one(m.g[g], m.dw[g], m.db[g], (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 static int fill(FuseArgs& a, int32_t n_rel, const int32_t* k, int32_t k_root, const float* scale,
@@ -159,6 +189,69 @@ int hgnn_split_weight_grads(int32_t n_rel, const float* dw, const float* db, con
   hipLaunchKernelGGL(k_split_weight_grads, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                      as_stream(stream), a, dw, db);
   return check_launch("k_split_weight_grads");
+}
+
+// The multi-update forms: group g owns the flattened per-relation entries [base_g, base_g +
+// n_rel[g]) of wl / k / wr / bl / scale (and dwl / dwr / dbl).
+int hgnn_fuse_weights_multi(int32_t n_groups, const int32_t* n_rel, const float* const* wl,
+                            const int32_t* k, const float* const* wr, const int32_t* k_root,
+                            const float* const* bl, const float* scale, int32_t h,
+                            float* const* w_out, float* const* b_out, hgnn_stream_t stream) {
+  if (n_groups < 1 || n_groups > kMaxFuseGroups || !n_rel || !wl || !k || !k_root || !w_out)
+    return fail(HGNN_E_ARG, "fuse_weights_multi: n_groups=%d (1..%d)", n_groups, kMaxFuseGroups);
+  FuseMulti m{};
+  int64_t total = 1;
+  for (int g = 0, base = 0; g < n_groups; base += n_rel[g], ++g) {
+    FuseArgs& a = m.g[g];
+    if (int rc = fill(a, n_rel[g], k + base, k_root[g], scale + base, h)) return rc;
+    bool any_root = false, any_b = false;
+    for (int r = 0; r < n_rel[g]; ++r) {
+      if (!wl[base + r]) return fail(HGNN_E_ARG, "fuse_weights_multi: group %d wl[%d] null", g, r);
+      a.wl[r] = wl[base + r];
+      a.wr[r] = wr ? wr[base + r] : nullptr;
+      a.bl[r] = bl ? bl[base + r] : nullptr;
+      any_root |= a.wr[r] != nullptr;
+      any_b |= a.bl[r] != nullptr;
+    }
+    m.w[g] = w_out[g];
+    m.b[g] = b_out ? b_out[g] : nullptr;
+    if (!m.w[g] || any_root != (k_root[g] > 0) || (m.b[g] && !any_b))
+      return fail(HGNN_E_ARG, "fuse_weights_multi: group %d: outputs / root blocks / biases", g);
+    total = std::max<int64_t>(total, (int64_t)h * a.k_tot + (m.b[g] ? h : 0));
+  }
+  hipLaunchKernelGGL(k_fuse_weights_multi, dim3((unsigned)cdiv(total, 256), (unsigned)n_groups),
+                     dim3(256), 0, as_stream(stream), m);
+  return check_launch("k_fuse_weights_multi");
+}
+
+int hgnn_split_weight_grads_multi(int32_t n_groups, const int32_t* n_rel, const float* const* dw,
+                                  const float* const* db, const int32_t* k, const int32_t* k_root,
+                                  const float* scale, int32_t h, float* const* dwl,
+                                  float* const* dwr, float* const* dbl, hgnn_stream_t stream) {
+  if (n_groups < 1 || n_groups > kMaxFuseGroups || !n_rel || !dw || !k || !k_root)
+    return fail(HGNN_E_ARG, "split_weight_grads_multi: n_groups=%d (1..%d)", n_groups,
+                kMaxFuseGroups);
+  FuseMulti m{};
+  int64_t total = 1;
+  for (int g = 0, base = 0; g < n_groups; base += n_rel[g], ++g) {
+    FuseArgs& a = m.g[g];
+    if (int rc = fill(a, n_rel[g], k + base, k_root[g], scale + base, h)) return rc;
+    if (!dw[g]) return fail(HGNN_E_ARG, "split_weight_grads_multi: dw[%d] is null", g);
+    for (int r = 0; r < n_rel[g]; ++r) {
+      a.dwl[r] = dwl ? dwl[base + r] : nullptr;
+      a.dwr[r] = dwr ? dwr[base + r] : nullptr;
+      a.dbl[r] = dbl ? dbl[base + r] : nullptr;
+      if (a.dwr[r] && k_root[g] == 0)
+        return fail(HGNN_E_ARG, "split_weight_grads_multi: group %d dwr[%d] without a root", g, r);
+    }
+    m.dw[g] = dw[g];
+    m.db[g] = db ? db[g] : nullptr;
+    total = std::max<int64_t>(total, (int64_t)h * a.k_tot + (m.db[g] ? h : 0));
+  }
+  hipLaunchKernelGGL(k_split_weight_grads_multi,
+                     dim3((unsigned)cdiv(total, 256), (unsigned)n_groups), dim3(256), 0,
+                     as_stream(stream), m);
+  return check_launch("k_split_weight_grads_multi");
 }
 
 }  // extern "C"

@@ -38,7 +38,7 @@ import torch
 from . import _native as N
 from . import ops
 from .graph import NO_SPLIT, GroupedEdges, Plan, RelationCSR
-from .nn import HeteroSAGE, _fused_weights
+from .nn import HeteroSAGE, _fused_weights_layer
 from .sampler import EdgeType, MiniBatch, NeighborSampler
 
 SLACK = 1024
@@ -319,7 +319,7 @@ class StaticBlocks:
             hop = L - 1 - li
             convs, csrs = model.layers[li], self.csrs[hop]
             outer = li == 0
-            out, groups, weights = {}, [], []
+            out, groups, msgs_g = {}, [], []
             for dst in sorted(self.cap[hop]):
                 msgs = [("__".join(et), et, w) for et, w in model.relations
                         if et[2] == dst and et in csrs]
@@ -333,11 +333,11 @@ class StaticBlocks:
                 else:
                     groups.append(ops.DstGroup(dst, rels, True, True, (),
                                                n_root=self.cap[hop][dst]))
-                weights.append(_fused_weights(convs, msgs, h_in if outer else h))
+                msgs_g.append(msgs)
             src = h_in if outer else h
             if groups:
                 out.update(ops.hetero_layer(ops.LayerSpec(tuple(sorted(src)), tuple(groups)), src,
-                                            weights))
+                                            _fused_weights_layer(convs, msgs_g, src)))
             h = out
         return {t: h[t][:n] for t, n in self.n_seeds.items()}
 
@@ -379,6 +379,7 @@ class CapturedStep:
         if partial_seeds is None:
             partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
         self.blocks = StaticBlocks(smp, n_seeds, x_dict, slack, partial_seeds=partial_seeds)
+        self._unit = ops.unit_grad(smp.device)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
@@ -393,7 +394,7 @@ class CapturedStep:
     def _body(self, with_opt: bool = True):
         out = self.blocks.forward(self.model, self.x_dict)
         loss = self.loss_fn(out)
-        loss.backward()
+        loss.backward(self._unit)          # a marked 1: no fill, no scale-by-1 launches
         if self.capture_between:
             self.between()
         if self.opt is not None and with_opt:

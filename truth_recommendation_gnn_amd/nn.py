@@ -118,13 +118,31 @@ def _fused_weights(convs: Dict[str, SAGEConv], msgs, x_dict) -> Tuple[torch.Tens
     return ops.fuse_weights(wl, wr, bl, scales)
 
 
+def _fused_weights_layer(convs: Dict[str, SAGEConv], msgs_per_group, x_dict
+                         ) -> List[Tuple[torch.Tensor, Optional[torch.Tensor]]]:
+    """``_fused_weights`` of every destination update of a layer, in one launch each way
+    (``ops.fuse_weights_multi``)."""
+    groups = []
+    for msgs in msgs_per_group:
+        wl, wr, bl, scales = [], [], [], []
+        for name, et, wt in msgs:
+            conv = convs[name]
+            conv.materialize(x_dict[et[0]].shape[1], x_dict[et[2]].shape[1])
+            wl.append(conv.lin_l.weight)
+            wr.append(conv.lin_r.weight if conv.lin_r is not None else None)
+            bl.append(conv.lin_l.bias)
+            scales.append(wt)
+        groups.append((wl, wr, bl, scales))
+    return ops.fuse_weights_multi(groups)
+
+
 class _LayoutModel(torch.nn.Module):
     """A hetero SAGE layer described by a layout, run as one fused ``hetero_layer``."""
     layout: Layout
 
     def _run_layer(self, convs, x_dict, edge_index_dict, relu: bool = True):
         types = tuple(sorted(x_dict))
-        groups, weights = [], []
+        groups = []
         for dst, msgs in self.layout.items():
             rels = []
             for name, et, _ in msgs:
@@ -133,7 +151,7 @@ class _LayoutModel(torch.nn.Module):
                                                  x_dict[dst].shape[0])))
             root = any(convs[name].lin_r is not None for name, _, _ in msgs)
             groups.append(ops.DstGroup(dst, tuple(rels), root, relu))
-            weights.append(_fused_weights(convs, msgs, x_dict))
+        weights = _fused_weights_layer(convs, list(self.layout.values()), x_dict)
         return ops.hetero_layer(ops.LayerSpec(types, tuple(groups)), dict(x_dict), weights)
 
 
@@ -210,7 +228,7 @@ class HeteroSAGE(torch.nn.Module):
         dsts = sorted({et[2] for et, _ in self.relations})
         for convs in self.layers:
             types = tuple(sorted(h))
-            groups, weights = [], []
+            groups, msgs_g = [], []
             for dst in dsts:
                 msgs = [("__".join(et), et, w) for et, w in self.relations if et[2] == dst]
                 rels = tuple((et[0], relation_csr(edge_index_dict[et], h[et[0]].shape[0],
@@ -218,7 +236,8 @@ class HeteroSAGE(torch.nn.Module):
                 pre = tuple(ops.use_pre_projection(h[et[0]], h[dst], self.hidden_dim, True)
                             for _, et, _ in msgs)
                 groups.append(ops.DstGroup(dst, rels, True, True, pre))
-                weights.append(_fused_weights(convs, msgs, h))
+                msgs_g.append(msgs)
+            weights = _fused_weights_layer(convs, msgs_g, h)
             out = ops.hetero_layer(ops.LayerSpec(types, tuple(groups)), h, weights)
             for t in h:
                 out.setdefault(t, h[t])

@@ -458,6 +458,132 @@ def fuse_weights(wl: Sequence[torch.Tensor], wr: Sequence[Optional[torch.Tensor]
     return out if isinstance(out, tuple) else (out, None)
 
 
+class _FuseWeightsMulti(torch.autograd.Function):
+    """``_FuseWeights`` for every destination update of a layer in one launch each way
+    (``hgnn_fuse_weights_multi`` / ``hgnn_split_weight_grads_multi``): a layer's updates cost
+    one fuse and one split launch instead of one each per update."""
+
+    @staticmethod
+    def forward(ctx, metas, *ts):
+        h, dev = int(ts[0].shape[0]), ts[0].device
+        outs, w_out, b_out, groups, i = [], [], [], [], 0
+        for meta in metas:
+            ks, k_root, scales, has_r, has_b = meta
+            R = len(ks)
+            n = R + sum(has_r) + sum(has_b)
+            g = ts[i:i + n]
+            i += n
+            wl, it = list(g[:R]), iter(g[R:])
+            wr = [next(it) if hr else None for hr in has_r]
+            bl = [next(it) if hb else None for hb in has_b]
+            groups.append((wl, wr, bl))
+            W = torch.empty(h, sum(ks) + k_root, dtype=torch.float32, device=dev)
+            b = torch.empty(h, dtype=torch.float32, device=dev) if any(has_b) else None
+            w_out.append(W)
+            b_out.append(b)
+            outs.append(W)
+            if b is not None:
+                outs.append(b)
+        plan = _fuse_multi_plan(metas, groups)
+        N.check(N.lib().hgnn_fuse_weights_multi(
+            len(metas), plan.a_nrel, plan.a_wl, plan.a_ks, plan.a_wr, plan.a_kroot, plan.a_bl,
+            plan.a_sc, h, N.ptr_array(w_out), N.ptr_array(b_out), N.stream_ptr(dev)),
+            "hgnn_fuse_weights_multi")
+        ctx.metas, ctx.h, ctx.dev, ctx.plan = metas, h, dev, plan
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        need = ctx.needs_input_grad[1:]
+        dws, dbs, dwl, dwr, dbl, ret = [], [], [], [], [], []
+        gi = ni = 0
+        for meta in ctx.metas:
+            ks, k_root, scales, has_r, has_b = meta
+            dW = grads[gi]
+            gi += 1
+            db = None
+            if any(has_b):
+                db = grads[gi]
+                gi += 1
+            if dW is None:
+                dW = torch.zeros(ctx.h, sum(ks) + k_root, dtype=torch.float32, device=ctx.dev)
+            if db is None and any(has_b):
+                db = torch.zeros(ctx.h, dtype=torch.float32, device=ctx.dev)
+            dws.append(dW.contiguous())
+            dbs.append(None if db is None else db.contiguous())
+            new = lambda shape, j: (torch.empty(shape, dtype=torch.float32, device=ctx.dev)
+                                    if need[j] else None)
+            gl = [new((ctx.h, k), ni + r) for r, k in enumerate(ks)]
+            j = ni + len(ks)
+            gr, gb = [], []
+            for hr in has_r:
+                gr.append(new((ctx.h, k_root), j) if hr else None)
+                j += hr
+            for hb in has_b:
+                gb.append(new((ctx.h,), j) if hb else None)
+                j += hb
+            ni = j
+            dwl += gl
+            dwr += gr
+            dbl += gb
+            ret += gl + [t for t, hr in zip(gr, has_r) if hr] + [t for t, hb in zip(gb, has_b)
+                                                                if hb]
+        p = ctx.plan
+        N.check(N.lib().hgnn_split_weight_grads_multi(
+            len(ctx.metas), p.a_nrel, N.ptr_array(dws), N.ptr_array(dbs), p.a_ks, p.a_kroot,
+            p.a_sc, ctx.h, N.ptr_array(dwl), N.ptr_array(dwr), N.ptr_array(dbl),
+            N.stream_ptr(ctx.dev)), "hgnn_split_weight_grads_multi")
+        return (None, *ret)
+
+
+class _FuseMultiPlan:
+    """The host arrays of one multi-update fuse (built once per set of parameter buffers)."""
+    __slots__ = ("a_nrel", "a_wl", "a_wr", "a_bl", "a_ks", "a_sc", "a_kroot")
+
+    def __init__(self, metas, groups):
+        wl = [t for g in groups for t in g[0]]
+        wr = [t for g in groups for t in g[1]]
+        bl = [t for g in groups for t in g[2]]
+        self.a_nrel = N.int_array([len(m[0]) for m in metas])
+        self.a_wl, self.a_wr, self.a_bl = N.ptr_array(wl), N.ptr_array(wr), N.ptr_array(bl)
+        self.a_ks = N.int_array([k for m in metas for k in m[0]])
+        self.a_sc = N.float_array([x for m in metas for x in m[2]])
+        self.a_kroot = N.int_array([m[1] for m in metas])
+
+
+_FUSE_MULTI_PLANS: Dict[tuple, _FuseMultiPlan] = {}
+
+
+def _fuse_multi_plan(metas, groups) -> _FuseMultiPlan:
+    key = (metas, tuple(0 if t is None else t.data_ptr()
+                        for g in groups for part in g for t in part))
+    plan = _FUSE_MULTI_PLANS.get(key)
+    if plan is None:
+        if len(_FUSE_MULTI_PLANS) >= 1024:
+            _FUSE_MULTI_PLANS.clear()
+        plan = _FUSE_MULTI_PLANS[key] = _FuseMultiPlan(metas, groups)
+    return plan
+
+
+def fuse_weights_multi(groups) -> List[Tuple[torch.Tensor, Optional[torch.Tensor]]]:
+    """``fuse_weights`` for several destination updates (``groups``: (wl, wr, bl, scales) each,
+    one hidden width) in one launch each way; one update, or more than 4, falls back to the
+    per-update calls."""
+    if len(groups) == 1 or len(groups) > 4:
+        return [fuse_weights(*g) for g in groups]
+    metas, flat = [], []
+    for wl, wr, bl, scales in groups:
+        ks = tuple(int(t.shape[1]) for t in wl)
+        roots = [t for t in wr if t is not None]
+        metas.append((ks, int(roots[0].shape[1]) if roots else 0,
+                      tuple(float(x) for x in scales), tuple(t is not None for t in wr),
+                      tuple(t is not None for t in bl)))
+        flat += [*wl, *roots, *[t for t in bl if t is not None]]
+    flat = [t.contiguous() for t in flat]     # (parameters are; the plan keys on addresses)
+    outs = iter(_FuseWeightsMulti.apply(tuple(metas), *flat))
+    return [(next(outs), next(outs) if any(m[4]) else None) for m in metas]
+
+
 # ----------------------------------------------------------------------------- layer spec
 @dataclasses.dataclass(frozen=True)
 class DstGroup:
@@ -985,7 +1111,8 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
     dU = torch.empty_like(U)
     part = torch.empty(int(lib.hgnn_edge_score_parts(nu)), dtype=torch.float32, device=dev)
     loss = torch.empty((), dtype=torch.float32, device=dev)
-    err = torch.zeros(2, dtype=torch.int32, device=dev)
+    # err[0]: zeroed and counted by the scoring pass, err[1] by the int64 negatives sort
+    err = torch.empty(2, dtype=torch.int32, device=dev)
     c = cscale.to(torch.float32).reshape(()).contiguous()
     inv_e = 1.0 / n_total if n_total > 0 else 0.0
     uop = _user_of_pos(csr)
@@ -1086,12 +1213,27 @@ class _EdgeBCELoss(torch.autograd.Function):
         else:
             dU, dP = ctx.grads
             ctx.grads = None         # handed on: autograd may accumulate into them from here
-        g = go.to(torch.float32).reshape(()).contiguous()
-        lib, s = N.lib(), N.stream_ptr(dU.device)
-        for t in (dU, dP):   # in place; a no-op launch for loss.backward()'s gradient of 1
-            N.check(lib.hgnn_scale_unless_one(N.ptr(t), t.numel(), N.ptr(g), s),
-                    "hgnn_scale_unless_one")
+        if not getattr(go, UNIT_GRAD, False):
+            g = go.to(torch.float32).reshape(()).contiguous()
+            lib, s = N.lib(), N.stream_ptr(dU.device)
+            for t in (dU, dP):   # in place; a no-op launch for loss.backward()'s gradient of 1
+                N.check(lib.hgnn_scale_unless_one(N.ptr(t), t.numel(), N.ptr(g), s),
+                        "hgnn_scale_unless_one")
         return dU, dP, None, None, None, None, None, None, None
+
+
+# A tensor carrying this attribute (set True) is a gradient of exactly 1 that nobody writes:
+# ``loss.backward(unit)`` with it skips the loss's scaling launches (minibatch.CapturedStep).
+UNIT_GRAD = "_hgnn_unit_grad"
+
+
+def unit_grad(device) -> torch.Tensor:
+    """A scalar 1.0 marked ``UNIT_GRAD``, for ``loss.backward(unit)``: the fused loss then hands
+    on its gradients unscaled, with no launch (the implicit ``loss.backward()`` makes a fill
+    and, per gradient, a scale-by-1 launch — three graph nodes of a captured step)."""
+    t = torch.ones((), dtype=torch.float32, device=device)
+    setattr(t, UNIT_GRAD, True)
+    return t
 
 
 def edge_bce_loss(user_emb: torch.Tensor, post_emb: torch.Tensor, pos_edges: torch.Tensor,

@@ -28,7 +28,7 @@ import torch
 from . import _native as N
 from . import ops
 from .graph import RelationCSR, relation_csr
-from .nn import HeteroSAGE, _fused_weights
+from .nn import HeteroSAGE, _fused_weights_layer
 
 EdgeType = Tuple[str, str, str]
 
@@ -267,7 +267,7 @@ def forward_blocks(model: HeteroSAGE, batch: MiniBatch,
     for convs, blk in zip(model.layers, batch.blocks):
         # one fused hetero layer per block (ops.hetero_layer: per destination type the K1 means of
         # its relations and one K3 over [aggr..., root prefix], one autograd node for the layer)
-        out, groups, weights = {}, [], []
+        out, groups, msgs_g = {}, [], []
         for dst, n_dst in blk.n_dst.items():
             msgs = [("__".join(et), et, w) for et, w in model.relations
                     if et[2] == dst and et in blk.csr]
@@ -276,9 +276,9 @@ def forward_blocks(model: HeteroSAGE, batch: MiniBatch,
                 continue
             rels = tuple((et[0], blk.csr[et]) for _, et, _ in msgs)
             groups.append(ops.DstGroup(dst, rels, True, True, (), n_root=n_dst))
-            weights.append(_fused_weights(convs, msgs, h))
+            msgs_g.append(msgs)
         if groups:
             out.update(ops.hetero_layer(ops.LayerSpec(tuple(sorted(h)), tuple(groups)), h,
-                                        weights))
+                                        _fused_weights_layer(convs, msgs_g, h)))
         h = out
     return h
