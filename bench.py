@@ -1048,6 +1048,11 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     # host is free during the step: 1.04 ms with it, 1.29-1.32 without — on by default.
     prefetch = args.prefetch or (use_graph and not args.no_prefetch)
     side = torch.cuda.Stream(dev) if prefetch else None
+    if side is not None:
+        # the setup above (the graph, the epoch's edge order) is queued on this stream: the side
+        # stream must not read it before it is written (rounds 4-5 sampled the capture's batch
+        # 0 from a half-written permutation)
+        side.wait_stream(torch.cuda.current_stream(dev))
 
     ph = _Phases() if os.environ.get("HGNN_CFG5_PHASES") else None
 
@@ -1056,9 +1061,11 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         (returns lb None), or — eager, before capture, ``--eager-sampler`` — a LinkBatch from
         link_batch + NeighborSampler.sample, staged by CapturedStep.prepare when ``prep``."""
         gb = (b % max(per_epoch, 1)) * world + rank            # this rank's slice of the order
-        ids = order[gb * nb:(gb + 1) * nb].long()
 
         def make():
+            # the edge ids made on the stream that samples them (rounds 4-5 cast them on the
+            # main stream, behind the running replay, and the side stream read them unwritten)
+            ids = order[gb * nb:(gb + 1) * nb].long()
             if ph:
                 ph.mark(b, "smp0")
             if static is not None and not eager:
@@ -1111,6 +1118,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
     loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
     loss_of.prepare, loss_of.commit = link_loss.prepare, link_loss.commit
+    loss_of.use_padded_rows = link_loss.use_padded_rows   # the captured step's padded tables
     loss_of.partial_seeds = True                 # both forms read the seed rows by local id
 
     # over RCCL the gradient all-reduce is recorded inside the step's graph (one replay per
@@ -1130,17 +1138,26 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         captured = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_of, opt,
                                           between=sync if (world > 1 or capture_ar) else None,
                                           capture_between=capture_ar)
-        lb0 = sample(0, prep=False)[0]
+        lb0, ev0 = sample(0, prep=False)
+        if ev0 is not None:
+            # batch 0 came from the side stream: the capture's warm-up steps read it here
+            # (rounds 4-5 did not wait, and their warm-up trained on a half-written batch 0)
+            torch.cuda.current_stream(dev).wait_event(ev0)
+            lb0.mb.record_stream(torch.cuda.current_stream(dev))
         link_loss.load(lb0.pu, lb0.pp, lb0.pn)
         captured.capture(lb0.mb, warmup=2)
+        if _SERIAL:
+            torch.cuda.synchronize()
+            state["after_capture"] = [float(p.double().sum()) for p in model.parameters()][:4]
         if not args.eager_sampler:
             # every later batch: sampled straight into the staging buffers, no host sync
             static = minibatch.LinkSampler(captured, pos_ei, cfg.num_posts, link_loss)
+        torch.cuda.synchronize()   # setup done: its buffers are written before the side stream runs
 
     def eager(lb):
         link_loss.make_csr()
         out = sampler.forward_blocks(model, lb.mb, g.x_dict)
-        loss = loss_of({t: v if t not in n_seeds else _pad_rows(v, n_seeds[t])
+        loss = loss_of({t: v if t not in n_seeds else _pad_rows(v, link_loss.rows[t])
                         for t, v in out.items()})
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -1161,6 +1178,10 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
             edges_dev.add_(static.edge_count())  # before the commit the next prepare waits on
         else:
             state["edges"] += sum(c.num_edges for blk in lb.mb.blocks for c in blk.csr.values())
+        if _SERIAL and "stage0" not in state and captured is not None:
+            torch.cuda.synchronize()
+            state["stage0"] = [int(captured.blocks.arena._bytes["stage"].sum()),
+                               int(link_loss.arena._bytes["stage"].sum())]
         if graph and captured is not None:
             if ph:
                 ph.mark(state["b"] - 1, "rep0")
@@ -1175,8 +1196,13 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                     t.record_stream(main)
             link_loss.commit()
             loss = eager(lb)
+        if _SERIAL:
+            torch.cuda.synchronize()
+            state.setdefault("losses", []).append(float(loss))
         if side is not None:
             nxt[0] = sample(state["b"], eager=not staged)   # under this step's GPU work
+            if _SERIAL:
+                torch.cuda.synchronize()
         return loss
 
     # the steps (commit + replay) on a high-priority stream, the side stream's sampling at the
@@ -1258,7 +1284,13 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         "kernels": _kernel_rows(kern, args.timer_steps, cfg.name, world),
         "loss": float(loss.detach()), "setup_s": round(setup_s, 1),
         **({"phases": phases} if phases else {}),
+        **({"losses": state.get("losses", [])[:40],
+            "after_capture": state.get("after_capture"),
+            "stage0": state.get("stage0")} if _SERIAL else {}),
     }
+
+
+_SERIAL = os.environ.get("HGNN_CFG5_SERIAL") == "1"   # (diagnosis: no overlap of the streams)
 
 
 class _Phases:

@@ -450,3 +450,43 @@ def test_link_sampler_stages_what_the_eager_sampler_stages():
     lb.mb = s.sample(lb.seeds, seed=5)
     ref = _ref_link_loss(sampler.forward_blocks(model, lb.mb, g.x_dict), lb)
     assert abs(got - float(ref)) <= 2e-6 * abs(float(ref)), (got, float(ref))
+
+
+@pytest.mark.parametrize("E,nu,np_", [(48, 48, 96), (1024, 1024, 2048), (1024, 2048, 3072),
+                                      (3000, 2500, 6100)])
+def test_link_group_equals_torch_grouping(E, nu, np_):
+    """hgnn_link_group (LinkLoss.prepare's one call) against the torch grouping it replaced:
+    pairs by user (stable), their posts / negatives / users in that order, the same pairs by
+    post (stable transpose: users and CSR positions), the negatives by post (users in order) —
+    at the bench's batch size too (B = 1024 pairs over 1024 users / 2048 posts)."""
+    from truth_recommendation_gnn_amd import _native as N
+    gen = torch.Generator(device=DEV).manual_seed(E)
+    pu = torch.randint(0, nu, (E,), device=DEV, generator=gen, dtype=torch.int32)
+    pp = torch.randint(0, np_, (E,), device=DEV, generator=gen, dtype=torch.int32)
+    pn = torch.randint(0, np_, (E,), device=DEV, generator=gen, dtype=torch.int32)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    out = {k: torch.full((n,), -7, **i32) for k, n in (
+        ("rowptr", nu + 1), ("col", E), ("neg", E), ("uop", E), ("p_rowptr", np_ + 1),
+        ("p_users", E), ("p_perm", E), ("n_rowptr", np_ + 1), ("n_users", E))}
+    ws = torch.empty(int(N.lib().hgnn_link_group_ws_bytes(E)), dtype=torch.uint8, device=DEV)
+    N.check(N.lib().hgnn_link_group(
+        N.ptr(pu), N.ptr(pp), N.ptr(pn), E, nu, np_,
+        *[N.ptr(out[k]) for k in ("rowptr", "col", "neg", "uop", "p_rowptr", "p_users",
+                                  "p_perm", "n_rowptr", "n_users")],
+        N.ptr(ws), ws.numel(), N.stream_ptr(DEV)), "hgnn_link_group")
+    order = torch.argsort(pu.long(), stable=True)
+    rowptr = torch.zeros(nu + 1, dtype=torch.long, device=DEV)
+    rowptr[1:] = torch.cumsum(torch.bincount(pu.long(), minlength=nu), 0)
+    col, neg, uop = pp[order], pn[order], pu[order]
+    assert torch.equal(out["rowptr"].long(), rowptr)
+    assert torch.equal(out["col"], col) and torch.equal(out["neg"], neg)
+    assert torch.equal(out["uop"], uop)
+    po = torch.argsort(col.long(), stable=True)            # positions by post, stable
+    prow = torch.zeros(np_ + 1, dtype=torch.long, device=DEV)
+    prow[1:] = torch.cumsum(torch.bincount(col.long(), minlength=np_), 0)
+    assert torch.equal(out["p_rowptr"].long(), prow)
+    assert torch.equal(out["p_perm"].long(), po) and torch.equal(out["p_users"], uop[po])
+    no = torch.argsort(neg.long(), stable=True)
+    nrow = torch.zeros(np_ + 1, dtype=torch.long, device=DEV)
+    nrow[1:] = torch.cumsum(torch.bincount(neg.long(), minlength=np_), 0)
+    assert torch.equal(out["n_rowptr"].long(), nrow) and torch.equal(out["n_users"], uop[no])

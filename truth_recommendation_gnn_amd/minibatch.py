@@ -300,10 +300,13 @@ class StaticBlocks:
         self.csrs = out
 
     # -- the model on the static blocks --------------------------------------------------------
-    def forward(self, model: HeteroSAGE, x_dict: Mapping[str, torch.Tensor]
-                ) -> Dict[str, torch.Tensor]:
+    def forward(self, model: HeteroSAGE, x_dict: Mapping[str, torch.Tensor],
+                padded: bool = False) -> Dict[str, torch.Tensor]:
         """``model`` on the static blocks; the seeds' rows per type (seed order), as
-        ``sampler.forward_blocks`` returns them for the loaded batch."""
+        ``sampler.forward_blocks`` returns them for the loaded batch — or, ``padded``, the whole
+        level-0 tables (``cap[0]`` rows: the seeds, then padded rows) for a loss that reads rows
+        by id and gives the others a zero gradient (no slice, so no zero-fill + copy of its
+        backward)."""
         if len(model.layers) != self.L:
             raise ValueError(f"{len(model.layers)}-layer model on {self.L} static levels")
         L = self.L
@@ -339,6 +342,8 @@ class StaticBlocks:
                 out.update(ops.hetero_layer(ops.LayerSpec(tuple(sorted(src)), tuple(groups)), src,
                                             _fused_weights_layer(convs, msgs_g, src)))
             h = out
+        if padded:
+            return {t: h[t] for t in self.n_seeds}
         return {t: h[t][:n] for t, n in self.n_seeds.items()}
 
 
@@ -380,6 +385,11 @@ class CapturedStep:
             partial_seeds = bool(getattr(loss_fn, "partial_seeds", False))
         self.blocks = StaticBlocks(smp, n_seeds, x_dict, slack, partial_seeds=partial_seeds)
         self._unit = ops.unit_grad(smp.device)
+        # a loss that takes the padded level-0 tables (LinkLoss) is sized for them here
+        pad = getattr(loss_fn, "use_padded_rows", None)
+        self.padded = pad is not None
+        if self.padded:
+            pad({t: self.blocks.cap[0][t] for t in self.blocks.n_seeds})
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.graph_opt: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
@@ -392,7 +402,7 @@ class CapturedStep:
             mk()
 
     def _body(self, with_opt: bool = True):
-        out = self.blocks.forward(self.model, self.x_dict)
+        out = self.blocks.forward(self.model, self.x_dict, padded=self.padded)
         loss = self.loss_fn(out)
         loss.backward(self._unit)          # a marked 1: no fill, no scale-by-1 launches
         if self.capture_between:
@@ -542,13 +552,25 @@ class LinkLoss:
         self.E, self.n_users, self.n_posts = int(n_edges), int(n_users), int(n_posts)
         self.n_total = int(n_total) if n_total else self.E
         self.device = torch.device(device)
-        i32, E = torch.int32, self.E
-        self.arena = _Arena({"rowptr": (self.n_users + 1, i32), "col": (E, i32),
-                             "neg": (E, i32), "uop": (E, i32),
-                             "p_rowptr": (self.n_posts + 1, i32), "p_users": (E, i32),
-                             "p_perm": (E, i32), "n_rowptr": (self.n_posts + 1, i32),
-                             "n_users": (E, i32)}, self.device)
         self.cscale = torch.ones((), dtype=torch.float32, device=self.device)
+        self._alloc(self.n_users, self.n_posts)
+
+    def use_padded_rows(self, rows: Mapping[str, int]) -> None:
+        """Take the embeddings as tables of ``rows`` (>= the id capacities) rows — a captured
+        step's padded level-0 tables: the rows past the ids are empty groups whose gradient the
+        loss writes as 0.  Called by ``CapturedStep`` before anything is loaded."""
+        if rows["user"] < self.n_users or rows["post"] < self.n_posts:
+            raise ValueError(f"padded rows {dict(rows)} below the id capacities")
+        self._alloc(int(rows["user"]), int(rows["post"]))
+
+    def _alloc(self, rows_u: int, rows_p: int) -> None:
+        i32, E = torch.int32, self.E
+        self.rows = {"user": rows_u, "post": rows_p}
+        self.arena = _Arena({"rowptr": (rows_u + 1, i32), "col": (E, i32),
+                             "neg": (E, i32), "uop": (E, i32),
+                             "p_rowptr": (rows_p + 1, i32), "p_users": (E, i32),
+                             "p_perm": (E, i32), "n_rowptr": (rows_p + 1, i32),
+                             "n_users": (E, i32)}, self.device)
         self.csr: Optional[_LossCSR] = None
         self.presorted = None
         st = self.arena.stage
@@ -571,7 +593,7 @@ class LinkLoss:
         st = self.arena.stage
         self.arena.wait_committed()
         N.check(N.lib().hgnn_link_group(
-            N.ptr(pu), N.ptr(pp), N.ptr(pn), self.E, self.n_users, self.n_posts,
+            N.ptr(pu), N.ptr(pp), N.ptr(pn), self.E, self.rows["user"], self.rows["post"],
             *self._stage_ptrs, self._ws.data_ptr(), self._ws.numel(),
             N.stream_ptr(self.device)), "hgnn_link_group")
 
@@ -584,14 +606,16 @@ class LinkLoss:
 
     def make_csr(self) -> None:
         lv = self.arena.live
-        self.csr = _LossCSR(lv, self.n_users, self.n_posts)
-        self.presorted = ops.PresortedNegatives(self.csr, lv["neg"], "user", self.n_posts,
+        nu, np_ = self.rows["user"], self.rows["post"]
+        self.csr = _LossCSR(lv, nu, np_)
+        self.presorted = ops.PresortedNegatives(self.csr, lv["neg"], "user", np_,
                                                 lv["n_rowptr"], lv["n_users"])
 
     def __call__(self, out: Mapping[str, torch.Tensor]) -> torch.Tensor:
         U, P = out["user"], out["post"]
-        if int(U.shape[0]) != self.n_users or int(P.shape[0]) != self.n_posts:
-            raise ValueError(f"link loss over {self.n_users} users / {self.n_posts} posts, got "
+        nu, np_ = self.rows["user"], self.rows["post"]
+        if int(U.shape[0]) != nu or int(P.shape[0]) != np_:
+            raise ValueError(f"link loss over {nu} user rows / {np_} post rows, got "
                              f"{tuple(U.shape)} / {tuple(P.shape)}")
         if self.csr is None:
             self.make_csr()
