@@ -1235,3 +1235,36 @@ def test_k3_split_matches_f32_kernels_closely():
     for a, c in zip(res[False], res[True]):
         scale = float(a.abs().max())
         assert float((a - c).abs().max()) <= 2e-5 * scale, (float((a - c).abs().max()), scale)
+
+
+@pytest.mark.parametrize("d", [128, 64, 16])
+def test_gather_multi_equals_single_calls(d):
+    """hgnn_gather_reduce_multi (a sampled layer's K1s, or one round of its K2s, as one launch;
+    round 6) against one hgnn_gather_reduce per job: the mean gathers into fresh outputs and the
+    weighted K2s accumulating into existing ones, bitwise; empty rows and an empty relation
+    included."""
+    from truth_recommendation_gnn_amd import graph as G
+    gen = torch.Generator().manual_seed(d)
+    jobs = []
+    for n_dst, n_src, max_deg in [(300, 50, 6), (100, 700, 12), (0, 10, 0), (257, 257, 3)]:
+        deg = torch.randint(0, max_deg + 1, (n_dst,), generator=gen)
+        rowptr = torch.zeros(n_dst + 1, dtype=torch.int32)
+        rowptr[1:] = torch.cumsum(deg, 0)
+        col = torch.randint(0, n_src, (int(rowptr[-1]),), generator=gen, dtype=torch.int32)
+        csr = G.RelationCSR.from_csr(rowptr.to(DEV), col.to(DEV), n_src, n_dst,
+                                     may_have_heavy_rows=False)
+        x = torch.randn(n_src, d, generator=gen).to(DEV)
+        jobs.append((x, csr))
+    got = ops.gather_mean_many(jobs)
+    for (x, csr), o in zip(jobs, got):
+        assert torch.equal(o, ops.gather_mean(x, csr))
+    # K2 round: accumulate into per-job outputs with the CSC weights
+    outs = [torch.randn(csr.n_src, d, generator=gen).to(DEV) for _, csr in jobs]
+    dAs = [torch.randn(csr.n_dst, d, generator=gen).to(DEV) for _, csr in jobs]
+    ref = [o.clone() for o in outs]
+    for dA, (_, csr), r in zip(dAs, jobs, ref):
+        ops.scatter_mean_bwd(dA, csr, out=r)
+    ops._gather_multi([(dA, csr.bwd, o) for dA, (_, csr), o in zip(dAs, jobs, outs)],
+                      mean=False, accumulate=True, edge_ws=[c.bwd_weights for _, c in jobs])
+    for o, r in zip(outs, ref):
+        assert torch.equal(o, r)

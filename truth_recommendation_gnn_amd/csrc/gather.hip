@@ -131,11 +131,10 @@ __device__ __forceinline__ void slot_combine(typename Vec<W>::T (&acc)[VPL]) {
     for (int q = 0; q < VPL; ++q) V::add(acc[q], V::shfl_xor(acc[q], m));
 }
 
-template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC = false>
-__global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
+// one item (a light row, or a chunk of a heavy row) per wave
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC>
+__device__ __forceinline__ void gather_item(const GatherArgs& a, const int64_t item) {
   using V = Vec<W>;
-  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (item >= a.n_items) return;
   const int lane = threadIdx.x & 63;
   const int sl = lane % LPR;
   const bool writer = lane < LPR;
@@ -199,6 +198,34 @@ __global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
       else V::store(dst + c, r);
     }
   }
+}
+
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W, bool SC = false>
+__global__ void __launch_bounds__(256) k_gather(const GatherArgs a) {
+  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= a.n_items) return;
+  gather_item<LPR, VPL, W, UNROLL, HAS_W, SC>(a, item);
+}
+
+// Several gathers of one row width in one launch (hgnn_gather_reduce_multi): job j owns the
+// waves [base[j], base[j + 1]); light rows only (no heavy-row plan), distinct outputs.
+constexpr int kGatherMultiMax = 8;
+struct GatherMulti {
+  GatherArgs j[kGatherMultiMax];
+  int64_t base[kGatherMultiMax + 1];
+  int32_t n;
+};
+
+template <int LPR, int VPL, int W, int UNROLL, bool HAS_W>
+__global__ void __launch_bounds__(256) k_gather_multi(const GatherMulti m) {
+  // the wave index made scalar: the job search and the job's arguments are then scalar loads
+  // (a per-lane index fetched every argument with vector loads, one more dependent round trip
+  // per wave — slower than the separate launches)
+  const int64_t item = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (item >= m.base[m.n]) return;
+  int j = 0;
+  while (j + 1 < m.n && item >= m.base[j + 1]) ++j;
+  gather_item<LPR, VPL, W, UNROLL, HAS_W, false>(m.j[j], item - m.base[j]);
 }
 
 // Heavy rows: out[row] (+)= s * sum_k slab[first + k].  One block per heavy row: S slices of
@@ -351,6 +378,50 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
   a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
   nt_policy(a, n_x);
   return run_gather(a, as_stream(stream));
+}
+
+int hgnn_gather_reduce_multi(int32_t n_jobs, const float* const* x, const int64_t* n_x, int32_t d,
+                             const int32_t* const* rowptr, const int32_t* const* col,
+                             const int64_t* n_rows, const float* const* edge_w, int32_t flags,
+                             float* const* out, hgnn_stream_t stream_) {
+  if (n_jobs < 1 || n_jobs > kGatherMultiMax || d <= 0 || d % 4 || d > 512)
+    return fail(HGNN_E_ARG, "gather_reduce_multi: n_jobs=%d (1..%d) d=%d (4..512, % 4)", n_jobs,
+                kGatherMultiMax, d);
+  GatherMulti m{};
+  m.n = n_jobs;
+  bool has_w = false;
+  for (int j = 0; j < n_jobs; ++j) {
+    GatherArgs& a = m.j[j];
+    if (n_rows[j] < 0 || (n_rows[j] > 0 && (!rowptr[j] || !out[j])))
+      return fail(HGNN_E_ARG, "gather_reduce_multi: job %d: null rowptr/out", j);
+    for (int i = 0; i < j; ++i)
+      if (n_rows[j] > 0 && out[i] == out[j])
+        return fail(HGNN_E_ARG, "gather_reduce_multi: jobs %d and %d share an output", i, j);
+    a.x = x[j]; a.rowptr = rowptr[j]; a.col = col[j]; a.out = out[j];
+    a.edge_w = edge_w ? edge_w[j] : nullptr;
+    has_w |= a.edge_w != nullptr;
+    a.n_rows = n_rows[j]; a.n_items = n_rows[j]; a.d = d; a.chunk = INT32_MAX;
+    a.mean = (flags & HGNN_MEAN) ? 1 : 0;
+    a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+    nt_policy(a, n_x[j]);
+    m.base[j + 1] = m.base[j] + n_rows[j];
+  }
+  if (m.base[n_jobs] == 0) return HGNN_OK;
+  const dim3 grid((unsigned)cdiv(m.base[n_jobs], 4)), block(256);
+  hipStream_t stream = as_stream(stream_);
+  // the row widths dispatch_gather takes at d % 4 == 0 (d = 64: its mean / weighted depths)
+  const int nv = d / 4;
+#define HGNN_GM(LPR, VPL, U, UW)                                                                 \
+  if (has_w) hipLaunchKernelGGL((k_gather_multi<LPR, VPL, 4, UW, true>), grid, block, 0, stream, m); \
+  else hipLaunchKernelGGL((k_gather_multi<LPR, VPL, 4, U, false>), grid, block, 0, stream, m);
+  if (nv <= 4) { HGNN_GM(4, 1, 4, 4) }
+  else if (nv <= 8) { HGNN_GM(8, 1, 4, 4) }
+  else if (nv <= 16) { HGNN_GM(16, 1, 8, 6) }
+  else if (nv <= 32) { HGNN_GM(32, 1, 4, 4) }
+  else if (nv <= 64) { HGNN_GM(64, 1, 4, 4) }
+  else { HGNN_GM(64, 2, 2, 2) }
+#undef HGNN_GM
+  return check_launch("k_gather_multi");
 }
 
 int hgnn_gather_reduce_scaled(const float* x, int64_t n_x, int32_t d, const int32_t* rowptr,

@@ -167,6 +167,50 @@ def gather_mean(x_src: torch.Tensor, csr: RelationCSR,
     return out
 
 
+def _multi_ok(jobs) -> bool:
+    """Whether gathers (x, grouped, out) can share one ``hgnn_gather_reduce_multi`` launch:
+    2..8 of them, no heavy-row plan, one fp32 row width (a multiple of 4, <= 512), distinct
+    outputs, and no per-kernel timer running (its events time each relation's launch)."""
+    if _timer is not None or not 2 <= len(jobs) <= 8:
+        return False
+    d = int(jobs[0][2].shape[1])
+    outs = {o.data_ptr() for _, _, o in jobs}
+    return (len(outs) == len(jobs) and d % 4 == 0 and d <= 512 and
+            all(g.plan.n_heavy == 0 and int(o.shape[1]) == d and x.dtype == torch.float32
+                for x, g, o in jobs))
+
+
+def _gather_multi(jobs, mean: bool, accumulate: bool, edge_ws=None) -> None:
+    """``_gather`` of every (x, grouped, out) job in one launch (see ``_multi_ok``)."""
+    dev = jobs[0][2].device
+    flags = (N.HGNN_MEAN if mean else 0) | (N.HGNN_ACCUMULATE if accumulate else 0)
+    N.check(N.lib().hgnn_gather_reduce_multi(
+        len(jobs), N.ptr_array([x for x, _, _ in jobs]),
+        N.i64_array([int(x.shape[0]) for x, _, _ in jobs]), int(jobs[0][2].shape[1]),
+        N.ptr_array([g.rowptr for _, g, _ in jobs]), N.ptr_array([g.col for _, g, _ in jobs]),
+        N.i64_array([g.n_rows for _, g, _ in jobs]),
+        N.ptr_array(edge_ws) if edge_ws is not None else None, flags,
+        N.ptr_array([o for _, _, o in jobs]), N.stream_ptr(dev)), "hgnn_gather_reduce_multi")
+
+
+def gather_mean_many(pairs: Sequence[Tuple[torch.Tensor, RelationCSR]]) -> List[torch.Tensor]:
+    """``gather_mean(x, csr)`` of every pair — one launch for all of them when they qualify
+    (sampled blocks: short rows, one pass each; ``_multi_ok``), else one call each."""
+    jobs = []
+    for x, csr in pairs:
+        x = _check_f32(x, "gather_mean")
+        if x.shape[0] != csr.n_src:
+            raise ValueError(f"x_src has {x.shape[0]} rows, relation expects {csr.n_src}")
+        if csr.num_edges and gather_blocks(x, csr.num_edges) > 1:
+            return [gather_mean(x, c) for x, c in pairs]
+        jobs.append((x, csr.fwd, torch.empty(csr.n_dst, int(x.shape[1]), dtype=torch.float32,
+                                             device=x.device)))
+    if not _multi_ok(jobs):
+        return [gather_mean(x, c) for x, c in pairs]
+    _gather_multi(jobs, mean=True, accumulate=False)
+    return [o for _, _, o in jobs]
+
+
 def _gather(x, grouped, col_w, csr_mean, out, accumulate, edge_w=None, kind=None):
     p = grouped.plan
     dev = out.device
@@ -705,10 +749,23 @@ class _HeteroLayer(torch.autograd.Function):
         outs, aggrs_by_g, masks = [None] * ng, [None] * ng, [None] * ng
         dev = flat[0].device
         lanes = _Lanes(dev, ng)
+        many = None
+        if lanes.side is None and not any(any(g.pre) for g in spec.groups):
+            # every relation's K1 of the layer in one launch (sampled blocks; gather_mean_many
+            # falls back to one launch each where they do not qualify)
+            many = iter(gather_mean_many([(xs[src], csr) for g in spec.groups
+                                          for src, csr in g.rels]))
         for gi, g in enumerate(spec.groups):   # destination types are independent chains
             w, b = wb[2 * gi], wb[2 * gi + 1]
             with lanes.ctx(gi):
-                if any(g.pre):
+                if many is not None:
+                    aggrs = [next(many) for _ in g.rels]
+                    segs = aggrs + ([_root(g, xs)] if g.root else [])
+                    mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev,
+                                       sum(int(t.shape[1]) for t in segs))
+                    y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
+                                   g.relu, mask_out=mk)
+                elif any(g.pre):
                     # pre-projected relations: P = x_src W_r^T, gathered (means summed into
                     # one [N_dst, h] input) and added in the destination update's epilogue
                     cols = _group_columns(g, xs)
@@ -815,12 +872,40 @@ class _HeteroLayer(torch.autograd.Function):
             if gx[t] is None:
                 gx[t] = torch.zeros_like(xs[t])
         lanes = _Lanes(saved[0].device, len(pending))
+        if lanes.side is None and len(pending) > 1 and _k2_rounds(pending, gx):
+            return (None, *[gx[t] for t in spec.types], *gwb)
         for li, (t, items) in enumerate(pending.items()):
             with lanes.ctx(li):
                 for dA, csr in items:
                     scatter_mean_bwd(dA, csr, out=gx[t])
         lanes.join()
         return (None, *[gx[t] for t in spec.types], *gwb)
+
+
+def _k2_rounds(pending, gx) -> bool:
+    """The K2s of a layer's backward as rounds of one launch each: round r takes the r-th
+    relation of every target type (distinct outputs, so no two jobs of a launch add into the
+    same rows; each target's relations keep their order).  False (nothing launched) where the
+    relations do not qualify (source-blocked or heavy-row gathers, ``_multi_ok``)."""
+    jobs_by_round: List[list] = []
+    for t, items in pending.items():
+        for r, (dA, csr) in enumerate(items):
+            if csr.num_edges and gather_blocks(dA, csr.num_edges) > 1:
+                return False
+            if len(jobs_by_round) <= r:
+                jobs_by_round.append([])
+            jobs_by_round[r].append((dA.contiguous(), csr, gx[t]))
+    for jobs in jobs_by_round:
+        if len(jobs) > 1 and not _multi_ok([(dA, csr.bwd, o) for dA, csr, o in jobs]):
+            return False
+    for jobs in jobs_by_round:
+        if len(jobs) == 1:
+            dA, csr, o = jobs[0]
+            scatter_mean_bwd(dA, csr, out=o)
+        else:
+            _gather_multi([(dA, csr.bwd, o) for dA, csr, o in jobs], mean=False,
+                          accumulate=True, edge_ws=[csr.bwd_weights for _, csr, _ in jobs])
+    return True
 
 
 def _group_columns(g: DstGroup, xs) -> List[Tuple[int, int]]:
