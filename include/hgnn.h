@@ -128,12 +128,15 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
 /* n_jobs (<= 8) gathers of one row width in one launch, as hgnn_gather_reduce each (job j: x[j]
  * of n_x[j] rows, rowptr[j] / col[j] over n_rows[j] rows, edge_w[j] nullable, the shared flags)
  * into DISTINCT outputs out[j]; rows are never split (no heavy-row plan: short rows, e.g. sampled
- * blocks), d % 4 == 0 and d <= 512.  The per-relation K1s of a sampled layer (and each round of
- * its K2s) as one graph node.  Results exactly those of the single calls. */
+ * blocks), d % 4 == 0 and d <= 512.  With HGNN_ACCUMULATE, acc_limit[j] > 0 (acc_limit nullable)
+ * limits the accumulation to rows below it and writes the other rows fresh (a K2 into a gradient
+ * whose prefix holds the root term: no zero-fill of the rest).  The per-relation K1s of a sampled
+ * layer (and each round of its K2s) as one graph node.  Results exactly those of the single calls
+ * (on a zeroed remainder). */
 int hgnn_gather_reduce_multi(int32_t n_jobs, const float* const* x, const int64_t* n_x, int32_t d,
                              const int32_t* const* rowptr, const int32_t* const* col,
                              const int64_t* n_rows, const float* const* edge_w, int32_t flags,
-                             float* const* out, hgnn_stream_t stream);
+                             const int64_t* acc_limit, float* const* out, hgnn_stream_t stream);
 
 /* hgnn_gather_reduce with a per-row output scale: out[i,:] (+)= row_w[i] * sum_p w_p x[col[p],:]
  * (row_w replaces HGNN_MEAN's 1/segment length; not both).  With row_w = 1/deg of the whole

@@ -39,7 +39,7 @@ _SIGS = {
     "hgnn_gather_reduce": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_i64, _p, _p, _c_i32, _p, _p,
                                     _c_i64, _c_i64, _c_i32, _p, _p, _p]),
     "hgnn_gather_reduce_multi": (_c_i32, [_c_i32, _p, _p, _c_i32, _p, _p, _p, _p, _c_i32, _p,
-                                          _p]),
+                                          _p, _p]),
     "hgnn_gather_reduce_scaled": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_i64, _p, _p, _p,
                                            _c_i32, _p, _p, _c_i64, _c_i64, _c_i32, _p, _p, _p]),
     "hgnn_gather_mean_fwd": (_c_i32, [_p, _c_i64, _c_i32, _p, _p, _c_i64, _p, _p, _c_i64,

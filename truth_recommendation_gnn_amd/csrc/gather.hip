@@ -38,6 +38,8 @@ struct GatherArgs {
   int32_t chunk;
   int32_t mean;
   int32_t accumulate;
+  int64_t acc_limit;           // > 0: only rows below it accumulate, the others are written
+                               // fresh (a K2 whose output holds a root-gradient prefix)
   // score mode (hgnn_score_gather): w_p = f(<x[col[p]], rowvec[row]>) recomputed per edge
   const float* rowvec;
   const float* cscale;
@@ -192,7 +194,7 @@ __device__ __forceinline__ void gather_item(const GatherArgs& a, const int64_t i
       typename V::T r = acc[q];
       if (!partial) {
         V::scale(r, s);
-        if (a.accumulate) V::add(r, V::load(dst + c));
+        if (a.accumulate && (a.acc_limit == 0 || row < a.acc_limit)) V::add(r, V::load(dst + c));
       }
       if (a.nt_store) V::store_nt(dst + c, r);
       else V::store(dst + c, r);
@@ -383,7 +385,8 @@ int hgnn_gather_reduce(const float* x, int64_t n_x, int32_t d, const int32_t* ro
 int hgnn_gather_reduce_multi(int32_t n_jobs, const float* const* x, const int64_t* n_x, int32_t d,
                              const int32_t* const* rowptr, const int32_t* const* col,
                              const int64_t* n_rows, const float* const* edge_w, int32_t flags,
-                             float* const* out, hgnn_stream_t stream_) {
+                             const int64_t* acc_limit, float* const* out,
+                             hgnn_stream_t stream_) {
   if (n_jobs < 1 || n_jobs > kGatherMultiMax || d <= 0 || d % 4 || d > 512)
     return fail(HGNN_E_ARG, "gather_reduce_multi: n_jobs=%d (1..%d) d=%d (4..512, % 4)", n_jobs,
                 kGatherMultiMax, d);
@@ -403,6 +406,8 @@ int hgnn_gather_reduce_multi(int32_t n_jobs, const float* const* x, const int64_
     a.n_rows = n_rows[j]; a.n_items = n_rows[j]; a.d = d; a.chunk = INT32_MAX;
     a.mean = (flags & HGNN_MEAN) ? 1 : 0;
     a.accumulate = (flags & HGNN_ACCUMULATE) ? 1 : 0;
+    a.acc_limit = acc_limit ? acc_limit[j] : 0;
+    if (a.acc_limit < 0) return fail(HGNN_E_ARG, "gather_reduce_multi: acc_limit[%d] < 0", j);
     nt_policy(a, n_x[j]);
     m.base[j + 1] = m.base[j] + n_rows[j];
   }

@@ -180,8 +180,9 @@ def _multi_ok(jobs) -> bool:
                 for x, g, o in jobs))
 
 
-def _gather_multi(jobs, mean: bool, accumulate: bool, edge_ws=None) -> None:
-    """``_gather`` of every (x, grouped, out) job in one launch (see ``_multi_ok``)."""
+def _gather_multi(jobs, mean: bool, accumulate: bool, edge_ws=None, acc_limit=None) -> None:
+    """``_gather`` of every (x, grouped, out) job in one launch (see ``_multi_ok``);
+    ``acc_limit[j]`` > 0: job j accumulates only into its rows below it."""
     dev = jobs[0][2].device
     flags = (N.HGNN_MEAN if mean else 0) | (N.HGNN_ACCUMULATE if accumulate else 0)
     N.check(N.lib().hgnn_gather_reduce_multi(
@@ -190,6 +191,7 @@ def _gather_multi(jobs, mean: bool, accumulate: bool, edge_ws=None) -> None:
         N.ptr_array([g.rowptr for _, g, _ in jobs]), N.ptr_array([g.col for _, g, _ in jobs]),
         N.i64_array([g.n_rows for _, g, _ in jobs]),
         N.ptr_array(edge_ws) if edge_ws is not None else None, flags,
+        N.i64_array(acc_limit) if acc_limit is not None else None,
         N.ptr_array([o for _, _, o in jobs]), N.stream_ptr(dev)), "hgnn_gather_reduce_multi")
 
 
@@ -658,14 +660,19 @@ def _root(g: DstGroup, xs) -> torch.Tensor:
     return x if g.n_root is None else x[:g.n_root]
 
 
-def _root_grad_buffer(g: DstGroup, xs, gx) -> torch.Tensor:
+def _root_grad_buffer(g: DstGroup, xs, gx, prefix=None) -> torch.Tensor:
     """Allocates gx[dst] and returns the view the root segment's dgrad writes (a block's prefix;
-    the rows after it are zero until the K2s add into them)."""
+    the rows after it are zero until the K2s add into them — or, with ``prefix`` (a dict), left
+    unwritten and recorded there: the first K2 round writes them fresh, ``_k2_rounds``)."""
     x = xs[_root_type(g)]
     if g.n_root is None or g.root_src is not None:
         gx[_root_type(g)] = torch.empty_like(x)
         return gx[_root_type(g)]
-    gx[g.dst] = torch.zeros_like(x)
+    if prefix is not None:
+        gx[g.dst] = torch.empty_like(x)
+        prefix[g.dst] = int(g.n_root)
+    else:
+        gx[g.dst] = torch.zeros_like(x)
     return gx[g.dst][:g.n_root]
 
 
@@ -828,6 +835,13 @@ class _HeteroLayer(torch.autograd.Function):
         jobs = []
         ai = 0
         pre_jobs = []
+        # sampled blocks on one lane: a destination type that K2s will write (its relations'
+        # sources) gets its block gradient unzeroed, the first K2 round writing past the prefix
+        one_lane = (_Lanes(saved[0].device, 2).side is None
+                    and not any(any(g.pre) for g in spec.groups))
+        k2_targets = {src for g in spec.groups for src, csr in g.rels
+                      if need_x[src] and csr.num_edges > 0}
+        prefix: Dict[str, int] = {}
         for gi, g in enumerate(spec.groups):
             aggrs = aggrs_all[ai:ai + _n_main_rels(g)]
             ai += _n_main_rels(g)
@@ -851,7 +865,9 @@ class _HeteroLayer(torch.autograd.Function):
             segs = list(aggrs)
             if g.root:
                 segs.append(_root(g, xs))
-                dxs.append(_root_grad_buffer(g, xs, gx) if need_x[_root_type(g)] else None)
+                fresh = one_lane and _root_type(g) in k2_targets
+                dxs.append(_root_grad_buffer(g, xs, gx, prefix if fresh else None)
+                           if need_x[_root_type(g)] else None)
             jobs.append((gi, g, segs, w, dout.contiguous(), dxs, need_w, need_b))
         lanes = _Lanes(saved[0].device, len(jobs))
         for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
@@ -872,8 +888,10 @@ class _HeteroLayer(torch.autograd.Function):
             if gx[t] is None:
                 gx[t] = torch.zeros_like(xs[t])
         lanes = _Lanes(saved[0].device, len(pending))
-        if lanes.side is None and len(pending) > 1 and _k2_rounds(pending, gx):
+        if lanes.side is None and len(pending) > 1 and _k2_rounds(pending, gx, prefix):
             return (None, *[gx[t] for t in spec.types], *gwb)
+        for t, n in prefix.items():          # (no rounds after all: zero what K2s add into)
+            gx[t][n:].zero_()
         for li, (t, items) in enumerate(pending.items()):
             with lanes.ctx(li):
                 for dA, csr in items:
@@ -882,11 +900,14 @@ class _HeteroLayer(torch.autograd.Function):
         return (None, *[gx[t] for t in spec.types], *gwb)
 
 
-def _k2_rounds(pending, gx) -> bool:
+def _k2_rounds(pending, gx, prefix=None) -> bool:
     """The K2s of a layer's backward as rounds of one launch each: round r takes the r-th
     relation of every target type (distinct outputs, so no two jobs of a launch add into the
-    same rows; each target's relations keep their order).  False (nothing launched) where the
-    relations do not qualify (source-blocked or heavy-row gathers, ``_multi_ok``)."""
+    same rows; each target's relations keep their order).  ``prefix[t]``: gx[t] holds only its
+    first rows (the root term); round 0 adds into those and writes the rest fresh.  False
+    (nothing launched) where the relations do not qualify (source-blocked or heavy-row gathers,
+    ``_multi_ok``)."""
+    prefix = prefix or {}
     jobs_by_round: List[list] = []
     for t, items in pending.items():
         for r, (dA, csr) in enumerate(items):
@@ -898,13 +919,20 @@ def _k2_rounds(pending, gx) -> bool:
     for jobs in jobs_by_round:
         if len(jobs) > 1 and not _multi_ok([(dA, csr.bwd, o) for dA, csr, o in jobs]):
             return False
-    for jobs in jobs_by_round:
+    if any(len(j) == 1 for j in jobs_by_round[:1]) and prefix:
+        return False                         # round 0 must be a multi launch to honour prefix
+    targets = list(pending)
+    for r, jobs in enumerate(jobs_by_round):
         if len(jobs) == 1:
             dA, csr, o = jobs[0]
             scatter_mean_bwd(dA, csr, out=o)
         else:
+            lim = None
+            if r == 0 and prefix:
+                lim = [prefix.get(t, 0) for t in targets if pending[t]]
             _gather_multi([(dA, csr.bwd, o) for dA, csr, o in jobs], mean=False,
-                          accumulate=True, edge_ws=[csr.bwd_weights for _, csr, _ in jobs])
+                          accumulate=True, edge_ws=[csr.bwd_weights for _, csr, _ in jobs],
+                          acc_limit=lim)
     return True
 
 
