@@ -104,6 +104,12 @@ def parse(argv=None):
                    help="cfg5 mini-batch: no side-stream sampling of the next batch")
     p.add_argument("--prefetch", action="store_true",
                    help="cfg5 mini-batch: sample the next batch on a side stream under this one")
+    p.add_argument("--single-buffer", action="store_true",
+                   help="cfg5 mini-batch: one recorded step, each batch staged and copied into "
+                        "its buffers, instead of two steps over their own buffers in turn")
+    p.add_argument("--side-cus", type=int, default=0,
+                   help="cfg5 mini-batch: run the side stream's sampling on this many CUs only "
+                        "(a CU-masked stream; 0: all)")
     p.add_argument("--default-priority", action="store_true",
                    help="cfg5 mini-batch: replay on a default-priority stream (by default the "
                         "steps run on a high-priority one, above the side stream's sampling)")
@@ -1047,7 +1053,9 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     # without — that step is bound by host issue, so it is off there.  Replaying the graph the
     # host is free during the step: 1.04 ms with it, 1.29-1.32 without — on by default.
     prefetch = args.prefetch or (use_graph and not args.no_prefetch)
-    side = torch.cuda.Stream(dev) if prefetch else None
+    side = None
+    if prefetch:
+        side = _cu_masked_stream(dev, args.side_cus) if args.side_cus else torch.cuda.Stream(dev)
     if side is not None:
         # the setup above (the graph, the epoch's edge order) is queued on this stream: the side
         # stream must not read it before it is written (rounds 4-5 sampled the capture's batch
@@ -1070,7 +1078,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                 ph.mark(b, "smp0")
             if static is not None and not eager:
                 with _Phases.host(ph, "sample"):
-                    static.prepare(ids, gb, gen_neg)
+                    statics[b % len(statics)].prepare(ids, gb, gen_neg)
                 if ph:
                     ph.mark(b, "smp1")
                     ph.mark(b, "prep1")
@@ -1106,20 +1114,24 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     n_seeds = {"user": nb, "post": 2 * nb}
     link_loss = minibatch.LinkLoss(nb, n_seeds["user"], n_seeds["post"], dev, n_total=nb * world)
 
-    def loss_of(out):
-        if args.torch_loss:
-            u, p = out["user"], out["post"]
-            pu, pp, pn = link_loss.uop.long(), link_loss.col.long(), link_loss.neg.long()
-            pos = (u[pu] * p[pp]).sum(1)
-            neg = (u[pu] * p[pn]).sum(1)
-            return (torch.nn.functional.softplus(-pos).sum()
-                    + torch.nn.functional.softplus(neg).sum()) / (nb * world)
-        return link_loss(out)
+    def loss_for(ll):
+        def loss_of(out):
+            if args.torch_loss:
+                u, p = out["user"], out["post"]
+                pu, pp, pn = ll.uop.long(), ll.col.long(), ll.neg.long()
+                pos = (u[pu] * p[pp]).sum(1)
+                neg = (u[pu] * p[pn]).sum(1)
+                return (torch.nn.functional.softplus(-pos).sum()
+                        + torch.nn.functional.softplus(neg).sum()) / (nb * world)
+            return ll(out)
 
-    loss_of.make_csr = link_loss.make_csr        # fresh loss structures per recorded pass
-    loss_of.prepare, loss_of.commit = link_loss.prepare, link_loss.commit
-    loss_of.use_padded_rows = link_loss.use_padded_rows   # the captured step's padded tables
-    loss_of.partial_seeds = True                 # both forms read the seed rows by local id
+        loss_of.make_csr = ll.make_csr           # fresh loss structures per recorded pass
+        loss_of.prepare, loss_of.commit, loss_of.link_loss = ll.prepare, ll.commit, ll
+        loss_of.use_padded_rows = ll.use_padded_rows   # the captured step's padded tables
+        loss_of.partial_seeds = True             # both forms read the seed rows by local id
+        return loss_of
+
+    loss_of = loss_for(link_loss)
 
     # over RCCL the gradient all-reduce is recorded inside the step's graph (one replay per
     # step; with --dist at world 1 it is still issued, as a rehearsal of the captured
@@ -1132,6 +1144,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         parallel.sync_grads(model, env, force=capture_ar)   # no-op at world size 1 otherwise
 
     captured = static = None
+    caps, statics = [], []        # the captured step(s) and their LinkSamplers, used in turn
     edges_dev = torch.zeros((), dtype=torch.int64, device=dev)   # the LinkSampler's counts
     if use_graph:
         # the capture's two warm-up passes are training steps on batch 0 (then recorded once)
@@ -1149,9 +1162,29 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         if _SERIAL:
             torch.cuda.synchronize()
             state["after_capture"] = [float(p.double().sum()) for p in model.parameters()][:4]
+        caps = [captured]
+        lls = [link_loss]
+        if not args.eager_sampler and not args.single_buffer and captured.graph_opt is None:
+            # a second recorded step over its own buffers: batches alternate between the two,
+            # each sampled straight into the live buffers of the one not replaying — no staging
+            # copy on the main stream (no warm-up: the first capture's steps are the training's)
+            ll2 = minibatch.LinkLoss(nb, n_seeds["user"], n_seeds["post"], dev,
+                                     n_total=nb * world)
+            cap2 = minibatch.CapturedStep(model, g.x_dict, s, n_seeds, loss_for(ll2), opt,
+                                          between=sync if (world > 1 or capture_ar) else None,
+                                          capture_between=capture_ar)
+            ll2.load(lb0.pu, lb0.pp, lb0.pn)
+            cap2.capture(lb0.mb, warmup=0)
+            caps.append(cap2)
+            lls.append(ll2)
+            for c, ll in zip(caps, lls):
+                c.blocks.use_direct()
+                ll.use_direct()
         if not args.eager_sampler:
             # every later batch: sampled straight into the staging buffers, no host sync
-            static = minibatch.LinkSampler(captured, pos_ei, cfg.num_posts, link_loss)
+            statics = [minibatch.LinkSampler(c, pos_ei, cfg.num_posts, ll)
+                       for c, ll in zip(caps, lls)]
+            static = statics[0]
         torch.cuda.synchronize()   # setup done: its buffers are written before the side stream runs
 
     def eager(lb):
@@ -1170,12 +1203,13 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
         if nxt[0] is not None and (nxt[0][0] is None) != staged:
             nxt[0] = None                        # a prefetched batch of the other kind
         lb, ev = nxt[0] if nxt[0] is not None else sample(state["b"], eager=not staged)
+        k = state["b"] % len(caps) if staged else 0
         state["b"] += 1
         main = torch.cuda.current_stream(dev)
         if ev is not None:
             main.wait_event(ev)
         if staged:
-            edges_dev.add_(static.edge_count())  # before the commit the next prepare waits on
+            edges_dev.add_(statics[k].edge_count())   # before the replay the next prepare waits on
         else:
             state["edges"] += sum(c.num_edges for blk in lb.mb.blocks for c in blk.csr.values())
         if _SERIAL and "stage0" not in state and captured is not None:
@@ -1186,7 +1220,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
             if ph:
                 ph.mark(state["b"] - 1, "rep0")
             with _Phases.host(ph, "step"):
-                loss = captured.step()           # commit the staged batch, replay
+                loss = caps[k].step()            # commit the staged batch (if staged), replay
             if ph:
                 ph.mark(state["b"] - 1, "rep1")
         else:
@@ -1265,6 +1299,7 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                    "graph_replays_per_step": (None if captured is None else
                                               1 if captured.graph_opt is None else 2),
                    "graph_nodes": None if captured is None else captured.graph_nodes(),
+                   "recorded_steps": len(caps) or None,
                    "parallelism": f"data-parallel x{world}" if world > 1 else "single",
                    "execution": ((("one HIP graph replay per step (forward + loss + backward + "
                                    "RCCL gradient all-reduce + Adam) over static-capacity blocks "
@@ -1277,7 +1312,10 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
                                  if captured is not None else "eager")
                    + (", next batch sampled on a side stream" if side is not None else "")
                    + (" by the sync-free LinkSampler straight into the staging buffers"
-                      if static is not None else "")},
+                      if static is not None else "")
+                   + ("; two recorded steps replayed in turn, each batch sampled into the live "
+                      "buffers of the one not replaying (no staging copy)" if len(caps) > 1
+                      else "")},
         "roofline": _roofline(kern, cfg, world, pooled=True),
         "projection": _projection(kern, cfg.name),
         "cpu_baseline": cpu,
@@ -1291,6 +1329,25 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
 
 
 _SERIAL = os.environ.get("HGNN_CFG5_SERIAL") == "1"   # (diagnosis: no overlap of the streams)
+
+
+def _cu_masked_stream(dev, n_cus: int):
+    """A stream whose kernels run on the first ``n_cus`` compute units only
+    (``hipExtStreamCreateWithCUMask``), wrapped for torch: the side stream's sampling then leaves
+    the other CUs to the replay."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n_total = torch.cuda.get_device_properties(dev).multi_processor_count
+    words = (n_total + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in range(min(n_cus, n_total)):
+        mask[c // 32] |= 1 << (c % 32)
+    stream = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(stream), words, mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(stream.value, device=dev)
 
 
 class _Phases:

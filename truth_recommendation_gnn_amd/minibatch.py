@@ -88,6 +88,10 @@ class _Arena:
         self.stage = self._views("stage")
         self._committed: Optional[torch.cuda.Event] = None
         self._dirty = False
+        # direct: writers fill the LIVE buffers themselves (two captured steps replayed in turn,
+        # each batch prepared into the one not replaying); commit() copies nothing, and the
+        # event a writer waits for is the last replay that read them (consumed())
+        self.direct = False
 
     def _views(self, which):
         buf = self._bytes[which]
@@ -99,9 +103,21 @@ class _Arena:
             torch.cuda.current_stream(self._bytes["stage"].device).wait_event(self._committed)
         self._dirty = True
 
+    def target(self):
+        """The buffers a writer fills: the stage, or the live ones in direct mode."""
+        return self.live if self.direct else self.stage
+
+    def consumed(self) -> None:
+        """Direct mode: the live buffers were just read (a replay was queued on the current
+        stream); the next writer waits for this point."""
+        ev = torch.cuda.Event()
+        ev.record()
+        self._committed = ev
+
     def commit(self) -> None:
-        """No-op when nothing was prepared since the last commit."""
-        if not self._dirty:
+        """No-op when nothing was prepared since the last commit (and in direct mode)."""
+        if not self._dirty or self.direct:
+            self._dirty = False
             return
         self._dirty = False
         self._bytes["live"].copy_(self._bytes["stage"])
@@ -157,11 +173,17 @@ class StaticBlocks:
         self.csrs: Optional[List[Dict[EdgeType, RelationCSR]]] = None
         self._static_calls()
 
+    def use_direct(self) -> None:
+        """Prepare straight into the live buffers (``_Arena.direct``): for two captured steps
+        replayed in turn, each batch staged into the one that is not replaying."""
+        self.arena.direct = True
+        self._static_calls()
+
     def _static_calls(self) -> None:
-        """The staging calls' arguments that do not change per batch (the stage buffers, the
+        """The staging calls' arguments that do not change per batch (the target buffers, the
         capacities), built once: a batch then fills five small arrays (its CSR and id
         pointers, row and entry counts) — prepare's host cost is three ctypes calls."""
-        L, st, dev = self.L, self.arena.stage, self.smp.device
+        L, st, dev = self.L, self.arena.target(), self.smp.device
         lib = N.lib()
         # pad items: every (hop, relation) in the static layout's order, then the root id lists
         self._items = [(h, et) for h in range(L) for et in self.ecap[h]]
@@ -483,6 +505,10 @@ class CapturedStep:
         if self.graph_opt is not None:
             self.between()
             self.graph_opt.replay()
+        lf = getattr(self.loss_fn, "link_loss", self.loss_fn)    # (a wrapper's LinkLoss)
+        for ar in (self.blocks.arena, getattr(lf, "arena", None)):
+            if isinstance(ar, _Arena) and ar.direct:
+                ar.consumed()
         return self.loss
 
 
@@ -563,6 +589,14 @@ class LinkLoss:
             raise ValueError(f"padded rows {dict(rows)} below the id capacities")
         self._alloc(int(rows["user"]), int(rows["post"]))
 
+    def use_direct(self) -> None:
+        """Prepare straight into the live buffers (see ``StaticBlocks.use_direct``)."""
+        self.arena.direct = True
+        st = self.arena.target()
+        self._stage_ptrs = tuple(st[k].data_ptr() for k in (
+            "rowptr", "col", "neg", "uop", "p_rowptr", "p_users", "p_perm", "n_rowptr",
+            "n_users"))
+
     def _alloc(self, rows_u: int, rows_p: int) -> None:
         i32, E = torch.int32, self.E
         self.rows = {"user": rows_u, "post": rows_p}
@@ -590,7 +624,6 @@ class LinkLoss:
         if int(pu.numel()) != self.E:
             raise ValueError(f"{int(pu.numel())} positives for a {self.E}-edge link loss")
         pu, pp, pn = (t.to(torch.int32).contiguous() for t in (pu, pp, pn))
-        st = self.arena.stage
         self.arena.wait_committed()
         N.check(N.lib().hgnn_link_group(
             N.ptr(pu), N.ptr(pp), N.ptr(pn), self.E, self.rows["user"], self.rows["post"],
@@ -693,7 +726,7 @@ class LinkSampler:
         self.counts = [torch.zeros(max(len(blocks.cap[h]), 2), dtype=i32, device=dev)
                        for h in range(L)]
         self.d_E = torch.zeros(L, 8, dtype=i32, device=dev)
-        st = blocks.arena.stage
+        st = blocks.arena.target()      # (the live buffers when the blocks are in direct mode)
         # level h's node buffers (h >= 1): the outermost block's destinations are the staged
         # root ids; deeper inner levels a scratch buffer each
         nodes = [dict(self.seeds)]
