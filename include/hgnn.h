@@ -292,7 +292,8 @@ int hgnn_score_gather2(const float* x, int64_t n_x, const float* rowvec, int32_t
  * hpos[post-grouped
  * pos] (weight of U[u] in dP[p], needs to_post_pos) and neg_w (weight in dP[n]) — not needed when
  * dP is formed by hgnn_score_gather, which recomputes both;
- * part needs hgnn_edge_score_parts(n_users) floats (16-B aligned); *err counts out-of-range negatives. */
+ * part needs hgnn_edge_score_parts(n_users) floats (16-B aligned); *err counts out-of-range negatives
+ * (err nullable: not counted — a caller whose negatives are valid by construction). */
 int64_t hgnn_edge_score_parts(int64_t n_users);
 int hgnn_edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_users,
                         int64_t n_posts, const int32_t* rowptr_u, const int32_t* col_u,

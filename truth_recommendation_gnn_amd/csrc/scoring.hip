@@ -102,7 +102,9 @@ __global__ void __launch_bounds__(256) k_edge_score(const ScoreArgs a) {
         pid = a.col[base + lane];
         const int64_t nn = seed_p ? (int64_t)uniform_draw(seed, base + lane, (uint32_t)a.n_posts)
                            : a.neg32 ? (int64_t)a.neg32[base + lane] : a.neg[base + lane];
-        if (nn < 0 || nn >= a.n_posts) atomicAdd(a.err, 1);
+        if (nn < 0 || nn >= a.n_posts) {
+          if (a.err) atomicAdd(a.err, 1);
+        }
         else nid = (int)nn;
       }
       float my_hp = 0.f, my_hn = 0.f;
@@ -277,11 +279,11 @@ static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_u
   hipStream_t stream = as_stream(stream_);
   if (d < 1 || n_users < 0 || n_posts < 0 || n_edges < 0)
     return fail(HGNN_E_ARG, "edge_score: bad sizes");
-  if (!cscale || !loss || !err ||
+  if (!cscale || !loss ||
       (n_users > 0 && (!U || !rowptr_u || !dU || !part)) || (!neg_key != !neg_user))
     return fail(HGNN_E_ARG, "edge_score: null pointer");
   if (hpos && !to_post_pos) return fail(HGNN_E_ARG, "edge_score: hpos needs to_post_pos");
-  (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);
+  if (err) (void)hipMemsetAsync(err, 0, sizeof(int32_t), stream);   // (null: not counted)
   ScoreArgs a{};
   a.U = U; a.P = P; a.rowptr = rowptr_u; a.col = col_u; a.neg = neg_u_order; a.neg32 = neg32;
   a.neg_seed = neg_seed;

@@ -38,7 +38,7 @@ import torch
 from . import _native as N
 from . import ops
 from .graph import NO_SPLIT, GroupedEdges, Plan, RelationCSR
-from .nn import HeteroSAGE, _fused_weights_layer
+from .nn import HeteroSAGE, _fused_weights_layers
 from .sampler import EdgeType, MiniBatch, NeighborSampler
 
 SLACK = 1024
@@ -340,11 +340,23 @@ class StaticBlocks:
         for t in self.cap[L - 1]:
             h_in[f"{t}@root"] = self.root_rows(t)
         h: Dict[str, torch.Tensor] = {}
+        # every layer's fused weights in one launch (and their split in one): the weights do
+        # not depend on the activations, only each layer's input widths
+        layer_msgs = []
+        for li in range(L):
+            csrs = self.csrs[L - 1 - li]
+            msgs_g = [m for m in ([("__".join(et), et, w) for et, w in model.relations
+                                   if et[2] == dst and et in csrs]
+                                  for dst in sorted(self.cap[L - 1 - li])) if m]
+            dims = ({t: int(x.shape[1]) for t, x in x_dict.items()} if li == 0 else
+                    {t: int(model.hidden_dim) for t in self.smp.num_nodes})
+            layer_msgs.append((model.layers[li], msgs_g, dims))
+        weights_all = _fused_weights_layers(layer_msgs)
         for li in range(L):
             hop = L - 1 - li
             convs, csrs = model.layers[li], self.csrs[hop]
             outer = li == 0
-            out, groups, msgs_g = {}, [], []
+            out, groups = {}, []
             for dst in sorted(self.cap[hop]):
                 msgs = [("__".join(et), et, w) for et, w in model.relations
                         if et[2] == dst and et in csrs]
@@ -358,11 +370,10 @@ class StaticBlocks:
                 else:
                     groups.append(ops.DstGroup(dst, rels, True, True, (),
                                                n_root=self.cap[hop][dst]))
-                msgs_g.append(msgs)
             src = h_in if outer else h
             if groups:
                 out.update(ops.hetero_layer(ops.LayerSpec(tuple(sorted(src)), tuple(groups)), src,
-                                            _fused_weights_layer(convs, msgs_g, src)))
+                                            weights_all[li]))
             h = out
         if padded:
             return {t: h[t] for t in self.n_seeds}

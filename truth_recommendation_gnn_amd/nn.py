@@ -14,7 +14,7 @@ per destination type); nothing runs on the CPU.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Sequence, Tuple, Union
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple, Union
 
 import torch
 from torch.nn.parameter import UninitializedParameter
@@ -118,22 +118,38 @@ def _fused_weights(convs: Dict[str, SAGEConv], msgs, x_dict) -> Tuple[torch.Tens
     return ops.fuse_weights(wl, wr, bl, scales)
 
 
+def _weight_group(convs: Dict[str, SAGEConv], msgs, dims: Mapping[str, int]):
+    wl, wr, bl, scales = [], [], [], []
+    for name, et, wt in msgs:
+        conv = convs[name]
+        conv.materialize(dims[et[0]], dims[et[2]])
+        wl.append(conv.lin_l.weight)
+        wr.append(conv.lin_r.weight if conv.lin_r is not None else None)
+        bl.append(conv.lin_l.bias)
+        scales.append(wt)
+    return wl, wr, bl, scales
+
+
 def _fused_weights_layer(convs: Dict[str, SAGEConv], msgs_per_group, x_dict
                          ) -> List[Tuple[torch.Tensor, Optional[torch.Tensor]]]:
     """``_fused_weights`` of every destination update of a layer, in one launch each way
     (``ops.fuse_weights_multi``)."""
-    groups = []
-    for msgs in msgs_per_group:
-        wl, wr, bl, scales = [], [], [], []
-        for name, et, wt in msgs:
-            conv = convs[name]
-            conv.materialize(x_dict[et[0]].shape[1], x_dict[et[2]].shape[1])
-            wl.append(conv.lin_l.weight)
-            wr.append(conv.lin_r.weight if conv.lin_r is not None else None)
-            bl.append(conv.lin_l.bias)
-            scales.append(wt)
-        groups.append((wl, wr, bl, scales))
-    return ops.fuse_weights_multi(groups)
+    dims = {t: int(x.shape[1]) for t, x in x_dict.items()}
+    return ops.fuse_weights_multi([_weight_group(convs, m, dims) for m in msgs_per_group])
+
+
+def _fused_weights_layers(layers) -> List[List[Tuple[torch.Tensor, Optional[torch.Tensor]]]]:
+    """``_fused_weights_layer`` of several layers — ``layers``: (convs, msgs per group, input
+    width per type) each — in one launch each way when they hold at most 4 updates in all (a
+    2-layer sampled step: its fuse and its split are one graph node each)."""
+    groups = [[_weight_group(convs, m, dims) for m in msgs_g] for convs, msgs_g, dims in layers]
+    flat = [g for gs in groups for g in gs]
+    if len(flat) > 4:
+        return [ops.fuse_weights_multi(gs) for gs in groups]
+    out, it = [], iter(ops.fuse_weights_multi(flat))
+    for gs in groups:
+        out.append([next(it) for _ in gs])
+    return out
 
 
 class _LayoutModel(torch.nn.Module):

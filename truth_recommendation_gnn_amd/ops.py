@@ -1278,17 +1278,18 @@ def _edge_bce(U, P, csr: RelationCSR, neg_u_order, cscale, check: bool, n_total:
             N.check(lib.hgnn_edge_score_fwd_draw(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
                 N.ptr(draw.seed), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
-                N.ptr(err), s), "hgnn_edge_score_fwd_draw")
+                N.ptr(err if check else None), s), "hgnn_edge_score_fwd_draw")
         elif neg32:
             N.check(lib.hgnn_edge_score_fwd_i32(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
                 N.ptr(neg), n_total, N.ptr(c), N.ptr(dU), N.ptr(part), N.ptr(loss),
-                N.ptr(err), s), "hgnn_edge_score_fwd_i32")
+                N.ptr(err if check else None), s), "hgnn_edge_score_fwd_i32")
         else:
             N.check(lib.hgnn_edge_score_fwd(
                 N.ptr(U), N.ptr(P), d, nu, np_, N.ptr(ub.rowptr), N.ptr(ub.col),
                 N.ptr(neg), None, n_total, N.ptr(c), N.ptr(dU), None, None, None, None,
-                N.ptr(part), N.ptr(loss), N.ptr(err), s), "hgnn_edge_score_fwd")
+                N.ptr(part), N.ptr(loss), N.ptr(err if check else None), s),
+                "hgnn_edge_score_fwd")
     lanes.join()
     if check and int(err[0]):
         raise ValueError("edge_bce_loss: negative post id out of range")
