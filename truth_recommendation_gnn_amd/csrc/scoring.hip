@@ -247,6 +247,60 @@ __global__ void k_loss_final(const double* red, const float* cscale, float inv_e
   *loss = (float)((double)*cscale * (double)inv_e * p + (double)inv_e * q);
 }
 
+// k_loss_partial + k_loss_final in one block (few partials: a sampled batch's loss), bitwise the
+// same sums: wave w takes virtual blocks 4w .. 4w + 3; lane l stands for the partial kernel's
+// threads l, l + 64, l + 128, l + 192 (the same strided double sums), the shared-memory tree's
+// first two levels are in-lane adds and the other six shuffles in the same order; the 64 block
+// sums are then added in order as k_loss_final does.
+__global__ void __launch_bounds__(1024) k_loss_one(const float* part, int64_t n_part,
+                                                   const float* cscale, float inv_e,
+                                                   float* loss) {
+  __shared__ double red[2 * kRedBlocks];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t per = cdiv(n_part, kRedBlocks);
+  for (int vb = 4 * wv; vb < 4 * wv + 4; ++vb) {
+    const int64_t b0 = vb * per, b1 = min<int64_t>(b0 + per, n_part);
+    double p[4], q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      p[k] = 0.0;
+      q[k] = 0.0;
+      for (int64_t i = b0 + lane + 64 * k; i < b1; i += 256) {
+        p[k] += part[2 * i];
+        q[k] += part[2 * i + 1];
+      }
+    }
+    // s = 128: t += t + 128 (slots 0, 1 take 2, 3); s = 64: slot 0 takes slot 1
+    p[0] += p[2]; q[0] += q[2];
+    p[1] += p[3]; q[1] += q[3];
+    p[0] += p[1]; q[0] += q[1];
+    double pp = p[0], qq = q[0];
+    for (int s = 32; s > 0; s >>= 1) {   // t += t + s for t < s (lanes >= s carry don't-cares)
+      const double po = __shfl_down(pp, s, 64), qo = __shfl_down(qq, s, 64);
+      if (lane < s) {
+        pp += po;
+        qq += qo;
+      }
+    }
+    if (lane == 0) {
+      red[2 * vb] = pp;
+      red[2 * vb + 1] = qq;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ps = 0.0, qs = 0.0;
+    for (int i = 0; i < kRedBlocks; ++i) {
+      ps += red[2 * i];
+      qs += red[2 * i + 1];
+    }
+    *loss = (float)((double)*cscale * (double)inv_e * ps + (double)inv_e * qs);
+  }
+}
+
+// few enough partials for one block to sum them faster than two launches
+constexpr int64_t kLossOneMax = 65536;
+
 template <int LPR, int VPL, int W>
 static int launch_score(const ScoreArgs& a, int64_t nblocks, hipStream_t stream) {
   if (a.nt_neg)   // the cache policy as its own instantiation: the default one is unchanged
@@ -306,6 +360,11 @@ static int edge_score_fwd(const float* U, const float* P, int32_t d, int64_t n_u
   }
   // the reduction scratch lives after the block partials: part holds 2*nb floats + 2*64 doubles
   double* red = reinterpret_cast<double*>(part + align_up((size_t)(2 * nb), 4));
+  if (nb <= kLossOneMax) {
+    hipLaunchKernelGGL(k_loss_one, dim3(1), dim3(1024), 0, stream, part, nb, cscale, a.inv_e,
+                       loss);
+    return check_launch("k_loss_one");
+  }
   hipLaunchKernelGGL(k_loss_partial, dim3(kRedBlocks), dim3(256), 0, stream, part, nb, red);
   if (int rc2 = check_launch("k_loss_partial")) return rc2;
   hipLaunchKernelGGL(k_loss_final, dim3(1), dim3(64), 0, stream, red, cscale, a.inv_e, loss);
