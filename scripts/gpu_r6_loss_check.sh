@@ -11,5 +11,3 @@ run() {
 run
 run --single-buffer
 run --no-prefetch
-run
-run --single-buffer

@@ -326,6 +326,7 @@ def test_captured_link_step_with_rccl_allreduce_in_the_graph():
         port = sk.getsockname()[1]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1)
+    step = None
     try:
         env = parallel.DistEnv.from_torch()
         g, s, batch, make_model, _, _, n_seeds = _link_setup()
@@ -363,6 +364,12 @@ def test_captured_link_step_with_rccl_allreduce_in_the_graph():
             _close(p.detach(), r.detach(), n)
         assert all(np.isfinite(losses))
     finally:
+        # the recorded graphs hold the communicator's collective: release them (and let the
+        # GPU drain) before the process group goes (its teardown aborted with them alive)
+        del step
+        import gc
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()
 
 

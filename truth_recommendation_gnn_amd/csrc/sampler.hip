@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(256) k_sample_fill(const int32_t* rowptr, cons
                                                      int32_t* out_col) {
   const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= n) return;
-  sample_fill(rowptr, col, n_rows, dst_ids[w], fanout, seed, out_col + out_rowptr[w]);
+  sample_fill<64>(rowptr, col, n_rows, dst_ids[w], fanout, seed, out_col + out_rowptr[w]);
 }
 
 // ---- one hop over every relation into the frontier: one launch per phase ------------------------
@@ -80,13 +80,16 @@ __global__ void k_hop_rowptr(const HopTab t, const int32_t* pre, int32_t* totals
   if (j == t.off[r + 1] - t.off[r]) totals[r] = v;
 }
 
+// G lanes per destination (16 when the fanout fits: 4 destinations per wave)
+template <int G>
 __global__ void __launch_bounds__(256) k_hop_fill(const HopTab t) {
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t w = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / G) +
+                    (threadIdx.x & 63) / G;
   if (w >= t.off[t.n_rel]) return;
   const int r = hop_rel(t, w);
   const int64_t j = w - t.off[r];
-  sample_fill(t.rowptr[r], t.col[r], t.n_rows[r], t.dst[r][j], t.fanout, t.seed,
-              t.out_col[r] + t.out_rowptr[r][j]);
+  sample_fill<G>(t.rowptr[r], t.col[r], t.n_rows[r], t.dst[r][j], t.fanout, t.seed,
+                 t.out_col[r] + t.out_rowptr[r][j]);
 }
 
 // ---- relabel: a hash set over the ids this call sees, O(n_prefix + n_items) work --------------
@@ -328,7 +331,12 @@ int hgnn_sample_hop_fill(int32_t n_rel, const int32_t* const* rowptrs, const int
   t.seed = seed;
   const int64_t n = t.off[n_rel];
   if (n == 0) return HGNN_OK;
-  hipLaunchKernelGGL(k_hop_fill, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, as_stream(stream_), t);
+  if (fanout > 0 && fanout <= 16)
+    hipLaunchKernelGGL(k_hop_fill<16>, dim3((unsigned)cdiv(n, 16)), dim3(256), 0,
+                       as_stream(stream_), t);
+  else
+    hipLaunchKernelGGL(k_hop_fill<64>, dim3((unsigned)cdiv(n, 4)), dim3(256), 0,
+                       as_stream(stream_), t);
   return check_launch("k_hop_fill");
 }
 

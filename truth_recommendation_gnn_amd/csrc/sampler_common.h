@@ -30,28 +30,34 @@ __device__ __forceinline__ int32_t sample_count(const int32_t* rowptr, int64_t n
   return (fanout < 0 || deg <= fanout) ? deg : fanout;
 }
 
-// One wave: the sample of destination d into out[0 .. count).
+// G lanes (64: a wave; 16: a quarter wave, fanout <= 16) sample destination d into out[0 ..
+// count).  Floyd: for jj = deg-k .. deg-1 draw t in [0, jj]; take t unless already taken, then jj;
+// the chosen positions are held one per lane of the group, "already taken?" is one ballot masked
+// to the group.  The draws and choices do not depend on G (a quarter wave samples what a wave
+// does); fanout is one per launch, so every group still sampling runs the same iterations.
+template <int G>
 __device__ __forceinline__ void sample_fill(const int32_t* rowptr, const int32_t* col,
                                             int64_t n_rows, int32_t d, int32_t fanout,
                                             uint64_t seed, int32_t* out) {
   const int lane = threadIdx.x & 63;
+  const int gl = lane % G;
   if (d < 0 || d >= n_rows) return;   // counted 0
   const int32_t beg = rowptr[d], deg = rowptr[d + 1] - beg;
   if (fanout < 0 || deg <= fanout) {   // keep every neighbour, in CSR order
-    for (int32_t j = lane; j < deg; j += 64) out[j] = col[beg + j];
+    for (int32_t j = gl; j < deg; j += G) out[j] = col[beg + j];
     return;
   }
-  // Floyd: for jj = deg-k .. deg-1 draw t in [0, jj]; take t unless already taken, then jj
   int32_t chosen = -1;
   for (int r = 0; r < fanout; ++r) {
     const int32_t jj = deg - fanout + r;
     const int32_t t = (int32_t)draw(seed, d, r, (uint32_t)jj + 1u);
-    const bool taken = __ballot(lane < r && chosen == t) != 0ull;
-    if (lane == r) chosen = taken ? jj : t;
+    const uint64_t bal = __ballot(gl < r && chosen == t);
+    const bool taken = G == 64 ? bal != 0ull
+                               : ((bal >> ((lane / G) * G)) & ((1ull << G) - 1ull)) != 0ull;
+    if (gl == r) chosen = taken ? jj : t;
   }
-  if (lane < fanout) out[lane] = col[beg + chosen];
+  if (gl < fanout) out[gl] = col[beg + chosen];
 }
-
 
 // slot of `key` in an open-addressing table (key[] -1 = empty, capacity mask + 1, a power of two,
 // at least twice the keys inserted); *found = the key was already there (inserted by another

@@ -162,14 +162,16 @@ __global__ void __launch_bounds__(256) k_shop_rowptr(const SHop t, const int32_t
   }
 }
 
+template <int G>   // lanes per destination, as k_hop_fill
 __global__ void __launch_bounds__(256) k_shop_fill(const SHop t) {
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t w = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / G) +
+                    (threadIdx.x & 63) / G;
   if (w >= t.off[t.n_rel]) return;
   const int r = shop_rel(t, w);
   const int64_t j = w - t.off[r];
   if (j >= *t.d_ndst[r]) return;
-  sample_fill(t.rowptr[r], t.col[r], t.n_rows[r], t.dst[r][j], t.fanout, t.seed,
-              t.fill[r] + t.out_rowptr[r][j]);
+  sample_fill<G>(t.rowptr[r], t.col[r], t.n_rows[r], t.dst[r][j], t.fanout, t.seed,
+                 t.fill[r] + t.out_rowptr[r][j]);
 }
 
 // ---------------------------------------------------------------------------- relabel
@@ -339,7 +341,10 @@ int hgnn_sample_hop_static(int32_t n_rel, const int32_t* const* rowptrs,
   const unsigned gx = (unsigned)std::min<int64_t>(cdiv(span, 256), 256);
   hipLaunchKernelGGL(k_shop_rowptr, dim3(gx, (unsigned)n_rel), dim3(256), 0, stream, t, pre);
   if (int rc = check_launch("k_shop_rowptr")) return rc;
-  hipLaunchKernelGGL(k_shop_fill, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, stream, t);
+  if (fanout <= 16)
+    hipLaunchKernelGGL(k_shop_fill<16>, dim3((unsigned)cdiv(n, 16)), dim3(256), 0, stream, t);
+  else
+    hipLaunchKernelGGL(k_shop_fill<64>, dim3((unsigned)cdiv(n, 4)), dim3(256), 0, stream, t);
   return check_launch("k_shop_fill");
 }
 
