@@ -251,6 +251,29 @@ int hgnn_linear_bwd_ex(int32_t n_seg, const float* const* xs, const int32_t* ks,
                        const float* out, const uint32_t* mask, float* const* dxs,
                        uint32_t dx_accumulate, float* dw, float* db, float* dz_out, void* ws,
                        size_t ws_bytes, hgnn_stream_t stream);
+/* Several K3 calls at once — job j is hgnn_linear_fwd_mask(n_seg[j], the next n_seg[j] entries
+ * of xs / ks, n_rows[j], w[j], h, bias[j], NULL, relu[j], out[j], mask[j]) — in one launch per
+ * column block where two jobs both take the K = 384 / 512 split path with the same K (a sampled
+ * layer's two destination types: ops._HeteroLayer), job by job otherwise.  bias / relu / mask
+ * may be NULL (none for every job).  A pair only runs side by side when neither job writes what
+ * the other reads (byte ranges checked; else job by job).  Replaces the per-destination-type
+ * lin_l / lin_r calls of HeteroConv (reference train_gnn.py:147-200), like hgnn_linear_fwd. */
+int hgnn_linear_fwd_multi(int32_t n_jobs, const int32_t* n_seg, const float* const* xs,
+                          const int32_t* ks, const int64_t* n_rows, const float* const* w,
+                          int32_t h, const float* const* bias, const int32_t* relu,
+                          float* const* out, uint32_t* const* mask, hgnn_stream_t stream);
+/* Backward of hgnn_linear_fwd_multi: job j is hgnn_linear_bwd_ex(n_seg[j], xs / ks / dxs from
+ * the job's entries, n_rows[j], w[j], h, dout[j], out[j], mask[j], dx_accumulate[j], dw[j], db[j],
+ * NULL, its workspace).  ws: hgnn_linear_bwd_multi_ws_bytes (the jobs' hgnn_linear_bwd_ws_bytes
+ * one after the other).  out / mask / dx_accumulate / dw / db may be NULL (none for every job). */
+size_t hgnn_linear_bwd_multi_ws_bytes(int32_t n_jobs, const int64_t* n_rows,
+                                      const int32_t* k_total, int32_t h);
+int hgnn_linear_bwd_multi(int32_t n_jobs, const int32_t* n_seg, const float* const* xs,
+                          const int32_t* ks, const int64_t* n_rows, const float* const* w,
+                          int32_t h, const float* const* dout, const float* const* out,
+                          const uint32_t* const* mask, float* const* dxs,
+                          const uint32_t* dx_accumulate, float* const* dw, float* const* db,
+                          void* ws, size_t ws_bytes, hgnn_stream_t stream);
 int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,

@@ -1268,3 +1268,56 @@ def test_gather_multi_equals_single_calls(d):
                       mean=False, accumulate=True, edge_ws=[c.bwd_weights for _, c in jobs])
     for o, r in zip(outs, ref):
         assert torch.equal(o, r)
+
+
+@pytest.mark.parametrize("case", ["pair", "pair_root", "k_differs", "small"])
+def test_linear_multi_equals_per_job_calls(case):
+    """hgnn_linear_fwd_multi / hgnn_linear_bwd_multi (a sampled layer's two destination types'
+    K3 as one launch per column block, round 6) against one hgnn_linear_fwd_mask /
+    hgnn_linear_bwd_ex call per job.  The forward's rows, the ReLU bits and dX do not depend on
+    the grid: bitwise.  dW / db are the same partial sums over a different block split (the pair
+    shares one chip's worth of blocks): within 2e-6 of the largest entry.  'k_differs' (K = 384
+    beside K = 512) and 'small' (blocks under the split path's 8192 rows) run job by job:
+    bitwise throughout."""
+    gen = torch.Generator().manual_seed(7)
+    h = 128
+    shapes = {"pair": [(9000, [128, 128, 128]), (12345, [128, 128, 128])],
+              "pair_root": [(8192, [128, 128, 128]), (20000, [128, 128, 128])],
+              "k_differs": [(9000, [128, 128, 128]), (10000, [128, 128, 128, 128])],
+              "small": [(3000, [128, 128, 128]), (2500, [128, 128, 128])]}[case]
+    jobs_f, ref_f = [], []
+    for n, ks in shapes:
+        segs = [torch.randn(n, k, generator=gen).to(DEV) for k in ks]
+        w = (torch.randn(h, sum(ks), generator=gen) * 0.05).to(DEV)
+        b = torch.randn(h, generator=gen).to(DEV)
+        mk = ops.relu_mask_for(n, h, True, torch.device(DEV), sum(ks))
+        jobs_f.append((segs, w, b, True, mk))
+        mk_ref = None if mk is None else torch.empty_like(mk)
+        ref_f.append((ops.linear_fwd(segs, w, b, True, mask_out=mk_ref), mk_ref))
+    outs = ops.linear_fwd_many(jobs_f)
+    for o, (r, mr), (_, _, _, _, mk) in zip(outs, ref_f, jobs_f):
+        assert torch.equal(o, r)
+        if mk is not None:
+            assert torch.equal(mk, mr)
+    # backward: dX of the first two segments; the root segment's dX only in 'pair_acc_root'
+    jobs_b, ref_b = [], []
+    for (segs, w, b, _, mk), o in zip(jobs_f, outs):
+        dout = torch.randn(o.shape, generator=gen).to(DEV)
+        root = case == "pair_root"
+        dxs = [torch.empty_like(s_) for s_ in segs[:2]] + \
+            [torch.empty_like(s_) if root else None for s_ in segs[2:]]
+        dxs_ref = [None if d is None else torch.empty_like(d) for d in dxs]
+        jobs_b.append((segs, w, dout, o, dxs, True, True, mk))
+        ref_b.append((ops.linear_bwd(segs, w, dout, o, dxs_ref, True, True, mask=mk), dxs_ref))
+    got = ops.linear_bwd_many(jobs_b)
+    for (dw, db), ((rdw, rdb), dxs_ref), job in zip(got, ref_b, jobs_b):
+        for d, r in zip(job[4], dxs_ref):
+            if d is not None:
+                assert torch.equal(d, r)
+        exact = case in ("k_differs", "small")
+        for a, r in ((dw, rdw), (db, rdb)):
+            if exact:
+                assert torch.equal(a, r)
+            else:
+                tol = 2e-6 * float(r.abs().max())
+                assert float((a - r).abs().max()) <= tol, (float((a - r).abs().max()), tol)

@@ -257,7 +257,7 @@ def test_captured_link_step_matches_reference_loss():
     ll.load(lb0.pu, lb0.pp, lb0.pn)
     step.capture(lb0.mb)
     nodes = step.graph_nodes()                    # the recorded step, by node kind
-    assert nodes["kernel"] >= 20 and nodes["total"] == sum(
+    assert nodes["kernel"] >= 15 and nodes["total"] == sum(
         nodes[k] for k in ("kernel", "memcpy", "memset", "other"))
     for b in (1, 2, 6):
         lb = batch(b)

@@ -326,15 +326,15 @@ __global__ void __launch_bounds__(256) k_linear_wgrad(const LinArgs a) {
 
 // dw[j][k] = sum_b slab[b][j][k] (k < K), db[j] = sum_b slab[b][j][K]; fixed b order.
 // ldd: dw's row stride (kext - 1, or the whole dW's K for a column block of it)
-__global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
-                                                       int32_t kext, float* dw, float* db,
-                                                       int32_t ldd) {
+__device__ __forceinline__ void wgrad_reduce_body(const float* slab, int64_t nb, int32_t h,
+                                                  int32_t kext, float* dw, float* db, int32_t ldd,
+                                                  int64_t bid) {
   // 64 outputs per block (lanes), 16 waves each sum a contiguous range of slabs with 4
   // independent accumulators, then wave 0 adds the 16 partials in order: a fixed summation
   // order for a given nb (deterministic), and enough loads in flight to stream the slabs
   __shared__ float part[16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t e = bid * 64 + lane;
   const int64_t total = (int64_t)h * kext;
   const int64_t per = cdiv(nb, 16);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
@@ -359,6 +359,30 @@ __global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_
     if (k < kext - 1) { if (dw) dw[(int64_t)j * ldd + k] = v; }
     else if (db) db[j] = v;
   }
+}
+
+__global__ void __launch_bounds__(1024) k_wgrad_reduce(const float* slab, int64_t nb, int32_t h,
+                                                       int32_t kext, float* dw, float* db,
+                                                       int32_t ldd) {
+  wgrad_reduce_body(slab, nb, h, kext, dw, db, ldd, blockIdx.x);
+}
+
+// Two jobs' slabs (the split kernels' two-job backward) in one launch: blocks [0, nblk0) reduce
+// job 0, the rest job 1 — each output the same sum in the same order as a launch of its own.
+struct ReducePair {
+  const float* slab[2];
+  int64_t nb[2];
+  float* dw[2];
+  float* db[2];
+  int64_t nblk0;
+  int32_t h, kext, ldd;
+};
+__global__ void __launch_bounds__(1024) k_wgrad_reduce2(const ReducePair p) {
+  if ((int64_t)blockIdx.x < p.nblk0)
+    wgrad_reduce_body(p.slab[0], p.nb[0], p.h, p.kext, p.dw[0], p.db[0], p.ldd, blockIdx.x);
+  else
+    wgrad_reduce_body(p.slab[1], p.nb[1], p.h, p.kext, p.dw[1], p.db[1], p.ldd,
+                      (int64_t)blockIdx.x - p.nblk0);
 }
 
 // ================================================================ fused backward (LDS path)
@@ -1354,6 +1378,119 @@ static int xs_bwd_wide(const LinArgs& a, float* dw, float* db, void* ws, size_t 
   return check_launch("k_wgrad_reduce");
 }
 
+// ---- two jobs per launch (the two destination types of a sampled layer) ----
+// Both jobs on the K = 384 / 512 split path with the same K: each column block is one launch for
+// both (k_lin_fwd_xs2 / k_lin_bwd_xs2) and the backward's two slabs one reduce (k_wgrad_reduce2),
+// 5 launches where job by job takes 10.  HGNN_K3_PAIR=0: job by job.
+static bool pair_enabled() {
+  static const bool v = !getenv("HGNN_K3_PAIR") || atoi(getenv("HGNN_K3_PAIR")) != 0;
+  return v;
+}
+
+// byte range [p, p + bytes) against [q, q + qbytes)
+static bool ranges_overlap(const void* p, size_t bytes, const void* q, size_t qbytes) {
+  if (!p || !q) return false;
+  const uintptr_t p0 = reinterpret_cast<uintptr_t>(p), q0 = reinterpret_cast<uintptr_t>(q);
+  return p0 < q0 + qbytes && q0 < p0 + bytes;
+}
+
+// what job `a` reads, against a range job `b` writes (the jobs run side by side in a pair)
+static bool reads_overlap(const LinArgs& a, const void* p, size_t bytes) {
+  const size_t rows = (size_t)a.n * 4;
+  for (int s = 0; s < a.n_seg; ++s)
+    if (ranges_overlap(a.seg[s].x, rows * a.seg[s].k, p, bytes) ||
+        ranges_overlap(a.seg[s].dx, rows * a.seg[s].k, p, bytes))
+      return true;
+  return ranges_overlap(a.add, rows * a.h, p, bytes) || ranges_overlap(a.dout, rows * a.h, p, bytes) ||
+         ranges_overlap(a.out_act, rows * a.h, p, bytes) ||
+         ranges_overlap(a.mask_in, rows * 4, p, bytes) ||
+         ranges_overlap(a.out, rows * a.h, p, bytes);
+}
+
+static bool writes_hit(const LinArgs& w, const LinArgs& r) {
+  const size_t rows = (size_t)w.n * 4;
+  if (reads_overlap(r, w.out, rows * w.h) || reads_overlap(r, w.mask_out, rows * 4)) return true;
+  for (int s = 0; s < w.n_seg; ++s)
+    if (reads_overlap(r, w.seg[s].dx, rows * w.seg[s].k)) return true;
+  return false;
+}
+
+static int xs_fwd_wide2(const LinArgs (&a)[2], hipStream_t stream) {
+  LinArgs A[2], B[2];
+  ChunkTab TA[2], TB[2];
+  for (int j = 0; j < 2; ++j) {
+    A[j] = a[j];
+    A[j].k_total = 256;
+    A[j].bias = nullptr;
+    A[j].relu = 0;
+    A[j].mask_out = nullptr;
+    TA[j] = chunk_table_range(a[j], 0, 256);
+    B[j] = a[j];
+    B[j].k_total = a[j].k_total - 256;
+    B[j].w = a[j].w + 256;
+    B[j].add = a[j].out;
+    TB[j] = chunk_table_range(a[j], 256, B[j].k_total);
+  }
+  if (int rc = xs_linear_fwd2(A, TA, stream)) return rc;
+  return xs_linear_fwd2(B, TB, stream);
+}
+
+// the backward's column blocks of both jobs; false (nothing launched) when their variants differ
+static bool xs_bwd_parts(const LinArgs (&a)[2], float* const (&slab)[2], LinArgs (&P)[2][2],
+                         ChunkTab (&T)[2][2], bool (&pdx)[2]) {
+  for (int part = 0; part < 2; ++part) {
+    int cls[2];
+    bool d[2];
+    for (int j = 0; j < 2; ++j) {
+      const int c0 = part ? 256 : 0, kp = part ? a[j].k_total - 256 : 256;
+      LinArgs& p = P[part][j];
+      p = a[j];
+      p.k_total = kp;
+      p.w = a[j].w + c0;
+      p.dz_out = nullptr;
+      T[part][j] = chunk_table_range(a[j], c0, kp);
+      d[j] = false;
+      for (int c = 0; c < kp / 16; ++c) d[j] |= T[part][j].dx[c] != nullptr;
+      p.slab = slab[j];
+      p.slab_ld = a[j].k_total + 1;
+      p.slab_c0 = c0;
+      cls[j] = xs_bwd_class(p, T[part][j], d[j]);
+    }
+    if (cls[0] != cls[1]) return false;
+    pdx[part] = d[0];
+  }
+  return true;
+}
+
+static int xs_bwd_wide2(LinArgs (&P)[2][2], ChunkTab (&T)[2][2], const bool (&pdx)[2],
+                        float* const (&dw)[2], float* const (&db)[2], hipStream_t stream) {
+  const bool wg = P[0][0].slab != nullptr;
+  int G[2] = {0, 0};
+  for (int part = 0; part < 2; ++part) {
+    if (pdx[part] || wg) {
+      LinArgs pa[2] = {P[part][0], P[part][1]};
+      ChunkTab pt[2] = {T[part][0], T[part][1]};
+      if (int rc = xs_linear_bwd2(pa, pt, pdx[part], G, stream)) return rc;
+    }
+  }
+  if (!wg) return HGNN_OK;
+  const int K = P[0][0].slab_ld - 1, h = P[0][0].h;
+  ReducePair r;
+  const int64_t total = (int64_t)h * (K + 1);
+  for (int j = 0; j < 2; ++j) {
+    r.slab[j] = P[0][j].slab;
+    r.nb[j] = G[j];
+    r.dw[j] = dw[j];
+    r.db[j] = db[j];
+  }
+  r.nblk0 = cdiv(total, 64);
+  r.h = h;
+  r.kext = K + 1;
+  r.ldd = K;
+  hipLaunchKernelGGL(k_wgrad_reduce2, dim3((unsigned)(2 * r.nblk0)), dim3(1024), 0, stream, r);
+  return check_launch("k_wgrad_reduce2");
+}
+
 // every 8 consecutive 16-column chunks one 128-column segment (x_chunk<true>'s addressing)
 static bool chunks_in_segments_of_8(const ChunkTab& tab, int k_total) {
   for (int c = 0; c < k_total / 16; ++c) {
@@ -1388,11 +1525,156 @@ static int fill_args(LinArgs& a, int32_t n_seg, const float* const* xs, const in
   return HGNN_OK;
 }
 
+// a forward job's arguments as hgnn_linear_fwd_mask (add = NULL) fills them, and whether that call
+// would take the K = 384 / 512 split path; false on any argument the call itself would refuse
+static bool fwd_wide_job(LinArgs& a, int32_t n_seg, const float* const* xs, const int32_t* ks,
+                         int64_t n_rows, const float* w, int32_t h, const float* bias,
+                         int32_t relu, float* out, uint32_t* mask) {
+  a = LinArgs{};
+  bool vec;
+  if (fill_args(a, n_seg, xs, ks, nullptr, n_rows, w, h, &vec) != HGNN_OK) return false;
+  if (mask && (!relu || h % 16 != 0 || h > 128)) return false;
+  if (n_rows == 0 || !out) return false;
+  a.bias = bias;
+  a.out = out;
+  a.relu = relu;
+  a.mask_out = mask;
+  return xs_wide_ok(a, vec && reinterpret_cast<uintptr_t>(out) % 16 == 0 &&
+                           reinterpret_cast<uintptr_t>(bias) % 16 == 0) &&
+         !out_overlaps_inputs(a);
+}
+
+// the same for a backward job (hgnn_linear_bwd_ex with dz_out = NULL)
+static bool bwd_wide_job(LinArgs& a, int32_t n_seg, const float* const* xs, const int32_t* ks,
+                         int64_t n_rows, const float* w, int32_t h, const float* dout,
+                         const float* out, const uint32_t* mask, float* const* dxs,
+                         uint32_t dx_accumulate, bool wg, bool have_ws) {
+  a = LinArgs{};
+  bool vec;
+  if (fill_args(a, n_seg, xs, ks, dxs, n_rows, w, h, &vec) != HGNN_OK) return false;
+  if ((dx_accumulate >> n_seg) || !dout || n_rows == 0) return false;
+  if (mask && (!out || h % 16 != 0 || h > 128)) return false;
+  a.dx_acc = dx_accumulate;
+  a.dout = dout;
+  a.out_act = out;
+  a.mask_in = mask;
+  vec = vec && reinterpret_cast<uintptr_t>(dout) % 16 == 0 &&
+        (!out || reinterpret_cast<uintptr_t>(out) % 16 == 0);
+  for (int s = 0; s < n_seg; ++s)
+    vec = vec && (!a.seg[s].dx || reinterpret_cast<uintptr_t>(a.seg[s].dx) % 16 == 0);
+  return xs_wide_ok(a, vec) && (have_ws || !wg);
+}
+
 }  // namespace hgnn
 
 using namespace hgnn;
 
 extern "C" {
+
+int hgnn_linear_fwd_multi(int32_t n_jobs, const int32_t* n_seg, const float* const* xs,
+                          const int32_t* ks, const int64_t* n_rows, const float* const* w,
+                          int32_t h, const float* const* bias, const int32_t* relu,
+                          float* const* out, uint32_t* const* mask, hgnn_stream_t stream_) {
+  if (n_jobs < 0 || (n_jobs > 0 && (!n_seg || !xs || !ks || !n_rows || !w || !out)))
+    return fail(HGNN_E_ARG, "linear_fwd_multi: bad arguments");
+  for (int j = 0; j < n_jobs; ++j)
+    if (n_seg[j] < 1 || n_seg[j] > HGNN_MAX_SEG)
+      return fail(HGNN_E_ARG, "linear_fwd_multi: job %d has n_seg=%d", j, n_seg[j]);
+  if (n_jobs == 2 && pair_enabled()) {
+    LinArgs a[2];
+    bool ok = true;
+    for (int j = 0, o = 0; j < 2 && ok; o += n_seg[j], ++j)
+      ok = fwd_wide_job(a[j], n_seg[j], xs + o, ks + o, n_rows[j], w[j], h, bias ? bias[j] : nullptr,
+                        relu ? relu[j] : 0, out[j], mask ? mask[j] : nullptr);
+    if (ok && a[0].k_total == a[1].k_total && !writes_hit(a[0], a[1]) && !writes_hit(a[1], a[0]))
+      return xs_fwd_wide2(a, as_stream(stream_));
+  }
+  for (int j = 0, o = 0; j < n_jobs; o += n_seg[j], ++j)
+    if (int rc = hgnn_linear_fwd_mask(n_seg[j], xs + o, ks + o, n_rows[j], w[j], h,
+                                      bias ? bias[j] : nullptr, nullptr, relu ? relu[j] : 0,
+                                      out[j], mask ? mask[j] : nullptr, stream_))
+      return rc;
+  return HGNN_OK;
+}
+
+size_t hgnn_linear_bwd_multi_ws_bytes(int32_t n_jobs, const int64_t* n_rows,
+                                      const int32_t* k_total, int32_t h) {
+  size_t total = 0;
+  for (int j = 0; j < n_jobs; ++j) total += hgnn_linear_bwd_ws_bytes(n_rows[j], k_total[j], h);
+  return total;
+}
+
+int hgnn_linear_bwd_multi(int32_t n_jobs, const int32_t* n_seg, const float* const* xs,
+                          const int32_t* ks, const int64_t* n_rows, const float* const* w,
+                          int32_t h, const float* const* dout, const float* const* out,
+                          const uint32_t* const* mask, float* const* dxs,
+                          const uint32_t* dx_accumulate, float* const* dw, float* const* db,
+                          void* ws, size_t ws_bytes, hgnn_stream_t stream_) {
+  if (n_jobs < 0 || (n_jobs > 0 && (!n_seg || !xs || !ks || !n_rows || !w || !dout)))
+    return fail(HGNN_E_ARG, "linear_bwd_multi: bad arguments");
+  // job j's workspace: its hgnn_linear_bwd_ws_bytes, one after the other
+  char* wsp[2] = {nullptr, nullptr};
+  size_t wsb[2] = {0, 0};
+  size_t off = 0;
+  for (int j = 0, o = 0; j < n_jobs; o += n_seg[j], ++j) {
+    if (n_seg[j] < 1 || n_seg[j] > HGNN_MAX_SEG)
+      return fail(HGNN_E_ARG, "linear_bwd_multi: job %d has n_seg=%d", j, n_seg[j]);
+    int32_t k = 0;
+    for (int s = 0; s < n_seg[j]; ++s) k += ks[o + s];
+    const size_t b = hgnn_linear_bwd_ws_bytes(n_rows[j], k, h);
+    if (j < 2) { wsp[j] = ws ? static_cast<char*>(ws) + off : nullptr; wsb[j] = b; }
+    off += b;
+  }
+  const bool any_w = [&] {
+    for (int j = 0; j < n_jobs; ++j) if ((dw && dw[j]) || (db && db[j])) return true;
+    return false;
+  }();
+  if (any_w && (!ws || ws_bytes < off)) return fail(HGNN_E_WS, "linear_bwd_multi: workspace too small");
+  hipStream_t stream = as_stream(stream_);
+  if (n_jobs == 2 && pair_enabled()) {
+    LinArgs a[2];
+    bool ok = true;
+    for (int j = 0, o = 0; j < 2 && ok; o += n_seg[j], ++j) {
+      const bool wg = (dw && dw[j]) || (db && db[j]);
+      ok = bwd_wide_job(a[j], n_seg[j], xs + o, ks + o, n_rows[j], w[j], h, dout[j],
+                        out ? out[j] : nullptr, mask ? mask[j] : nullptr, dxs ? dxs + o : nullptr,
+                        dx_accumulate ? dx_accumulate[j] : 0u, wg, wsp[j] != nullptr);
+      if (ok && wg) {
+        const size_t need = (size_t)xs_bwd_grid(a[j].n) * h * (a[j].k_total + 1) * 4;
+        ok = wsb[j] >= need;
+      }
+    }
+    if (ok && a[0].k_total == a[1].k_total && !writes_hit(a[0], a[1]) && !writes_hit(a[1], a[0])) {
+      float* slab[2];
+      float* dwj[2];
+      float* dbj[2];
+      for (int j = 0; j < 2; ++j) {
+        dwj[j] = dw ? dw[j] : nullptr;
+        dbj[j] = db ? db[j] : nullptr;
+        slab[j] = (dwj[j] || dbj[j]) ? reinterpret_cast<float*>(wsp[j]) : nullptr;
+      }
+      LinArgs P[2][2];
+      ChunkTab T[2][2];
+      bool pdx[2];
+      if (xs_bwd_parts(a, slab, P, T, pdx)) return xs_bwd_wide2(P, T, pdx, dwj, dbj, stream);
+    }
+  }
+  off = 0;
+  for (int j = 0, o = 0; j < n_jobs; o += n_seg[j], ++j) {
+    int32_t k = 0;
+    for (int s = 0; s < n_seg[j]; ++s) k += ks[o + s];
+    const size_t b = hgnn_linear_bwd_ws_bytes(n_rows[j], k, h);
+    if (int rc = hgnn_linear_bwd_ex(n_seg[j], xs + o, ks + o, n_rows[j], w[j], h, dout[j],
+                                    out ? out[j] : nullptr, mask ? mask[j] : nullptr,
+                                    dxs ? dxs + o : nullptr, dx_accumulate ? dx_accumulate[j] : 0u,
+                                    dw ? dw[j] : nullptr, db ? db[j] : nullptr, nullptr,
+                                    ws ? static_cast<char*>(ws) + off : nullptr, ws ? b : 0,
+                                    stream_))
+      return rc;
+    off += b;
+  }
+  return HGNN_OK;
+}
 
 int hgnn_linear_fwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* bias, int32_t relu, float* out,

@@ -196,6 +196,15 @@ __device__ __forceinline__ void x6_mma(const bf16x8_t (&w)[3], const bf16x8_t& x
   hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], x1, hi, 0, 0, 0);
 }
 
+// Two jobs of one split-kernel launch (k_lin_fwd_xs2 / k_lin_bwd_xs2): blocks [0, g0) run job
+// 0, the rest job 1; the jobs share K and the kernel variant.
+struct XsPair {
+  LinArgs a[2];
+  ChunkTab tab[2];
+  int64_t n_tiles[2];
+  int64_t g0;
+};
+
 // The split-once kernels (linear_xs.hip): H = 128, K = 128 / 256, every segment 16-column
 // chunked and float4-aligned.  Host launchers; the caller validated the arguments.
 int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream);
@@ -203,5 +212,12 @@ int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream);
 // dgrad too (tab.dx).  Returns the block count through *grid.
 int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid, hipStream_t stream);
 int64_t xs_bwd_grid(int64_t n_rows);
+// The same for two jobs in one launch each (the same K; in the backward the same dgrad /
+// wgrad / accumulate variant); grid[j]: job j's block count (its slab rows).
+int xs_linear_fwd2(const LinArgs (&a)[2], const ChunkTab (&tab)[2], hipStream_t stream);
+int xs_linear_bwd2(const LinArgs (&a)[2], const ChunkTab (&tab)[2], bool dx, int (&grid)[2],
+                   hipStream_t stream);
+// the split kernels' backward variant of a job: bit 0 dgrad, bit 1 wgrad, bit 2 accumulate
+int xs_bwd_class(const LinArgs& a, const ChunkTab& tab, bool dx);
 
 }  // namespace hgnn

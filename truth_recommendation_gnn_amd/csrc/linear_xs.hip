@@ -150,9 +150,12 @@ __device__ __forceinline__ bf16x8_t tr8(const unsigned short* pl, int c0, int la
 // Measured and not kept: a prefetch two tiles deep; the split interleaved into
 // the sweep; the burst issued at a later sweep step; the split level by level for ILP; the bias as
 // the accumulator's initial value; the output tile staged in LDS and stored as whole rows.
+// (bid, G): the block's index and the block count of its job — blockIdx.x / gridDim.x in a
+// launch of its own, the job's range of a two-job launch (k_lin_fwd_xs2)
 template <int K, bool ADD>
-__global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
-                                                        int64_t n_tiles) {
+__device__ __forceinline__ void lin_fwd_xs_body(const LinArgs& a, const ChunkTab& tab,
+                                                int64_t n_tiles, uint32_t bid, uint32_t G_) {
+  const int64_t G = G_;
   constexpr int R = K == 256 ? 32 : 64, KS = K / 32, RT = R / 16, LDP = K + 16, PS = R * LDP;
   constexpr int NA = ADD ? RT : 0, NX = XStage<K, R>::NL;
   __shared__ __attribute__((aligned(16))) unsigned short pl[2][3 * PS];
@@ -160,7 +163,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int32_t last = (int32_t)(a.n - 1);
-  const int64_t G = gridDim.x;
   // W pieces of this wave's 16 output columns, for the whole launch
   bf16x8_t wa[KS][3];
 #pragma unroll
@@ -194,7 +196,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
       mk[bp][threadIdx.x] = 0u;
     }
   };
-  int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
+  int64_t t = bid;   // the job's grid never exceeds its n_tiles
   xs.issue(xr, t * R, last);
   xs.template put<LDP, PS>(xr, pl[0]);
   // Staggered halves (HGNN_XS_STAGGER): the two waves sharing a SIMD (w and w + 4) run the same
@@ -313,6 +315,23 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
   }
 }
 
+template <int K, bool ADD>
+__global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const ChunkTab tab,
+                                                        int64_t n_tiles) {
+  lin_fwd_xs_body<K, ADD>(a, tab, n_tiles, blockIdx.x, gridDim.x);
+}
+
+// Two jobs of the same shape class in one launch (two destination types' projections of a
+// layer): blocks [0, g0) run job 0, the rest job 1, each a persistent grid of its own.
+template <int K, bool ADD>
+__global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs2(const XsPair p) {
+  const int j = blockIdx.x < (uint32_t)p.g0 ? 0 : 1;
+  const uint32_t g0 = (uint32_t)p.g0;
+  const uint32_t bid = j ? blockIdx.x - g0 : blockIdx.x;
+  const uint32_t G = j ? gridDim.x - g0 : g0;
+  lin_fwd_xs_body<K, ADD>(p.a[j], p.tab[j], p.n_tiles[j], bid, G);
+}
+
 // ---------------------------------------------------------------- backward
 // Per 32-row tile: dz = dout masked by the ReLU bits (or by out > 0, or none), written to dz_out
 // when asked, summed for db, split into planes; X split into planes.  Then
@@ -323,8 +342,9 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_fwd_xs(const LinArgs a, const C
 //       [KW w, KW w + KW), KW = K / 8, every h; A = transposed dz fragments, B = transposed X.
 // The block's dW / db partials go to its slab [H][K + 1] (k_wgrad_reduce sums them in order).
 template <int K, bool DX, bool WG, bool ACC>
-__global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const ChunkTab tab,
-                                                        int64_t n_tiles) {
+__device__ __forceinline__ void lin_bwd_xs_body(const LinArgs& a, const ChunkTab& tab,
+                                                int64_t n_tiles, uint32_t bid, uint32_t G_) {
+  const int64_t G = G_;
   static_assert(!(DX && WG) || K == 128, "dgrad + wgrad in one pass: K = 128");
   constexpr int R = 32, LDZ = kH + 16, LDX = K + 16, ZS = R * LDZ, XS = R * LDX;
   constexpr int KT = K / 128;      // 16-column k tiles of dW per wave
@@ -334,7 +354,6 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int i = lane & 15, g = lane >> 4;
   const int32_t last32 = (int32_t)(a.n - 1);
-  const int64_t G = gridDim.x;
   const bool bits = a.mask_in != nullptr;
   const bool masked = !bits && a.out_act != nullptr;
   // dgrad: W^T pieces of dX columns 16 (w + 8 u) + i, h = 32 s + 8 g .. +7
@@ -419,7 +438,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     dxld[u] = DX ? tab.ld[c] : 0;
     acc_dx[u] = DX && ((tab.dx_acc >> c) & 1u);
   }
-  int64_t t = blockIdx.x;   // the grid never exceeds n_tiles
+  int64_t t = bid;   // the job's grid never exceeds its n_tiles
   issue(t);
   put(t, 0);
   // staggered halves as in the forward: waves 4-7 put the next tile first, then sweep
@@ -541,7 +560,7 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
     const int64_t KEXT = a.slab_ld > 0 ? a.slab_ld : K + 1;
     const int c0 = a.slab_ld > 0 ? a.slab_c0 : 0;
     const int64_t dbc = KEXT - 1;
-    float* slab = a.slab + (int64_t)blockIdx.x * kH * KEXT;
+    float* slab = a.slab + (int64_t)bid * kH * KEXT;
 #pragma unroll
     for (int h = 0; h < 8; ++h)
 #pragma unroll
@@ -572,10 +591,35 @@ __global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const C
   }
 }
 
+template <int K, bool DX, bool WG, bool ACC>
+__global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs(const LinArgs a, const ChunkTab tab,
+                                                        int64_t n_tiles) {
+  lin_bwd_xs_body<K, DX, WG, ACC>(a, tab, n_tiles, blockIdx.x, gridDim.x);
+}
+
+template <int K, bool DX, bool WG, bool ACC>
+__global__ void __launch_bounds__(kThr, 1) k_lin_bwd_xs2(const XsPair p) {
+  // one copy of the body: the job index is uniform (from blockIdx), so its arguments are scalar
+  // loads at a uniform offset (two inlined copies spilled the K = 256 wgrad variant)
+  const int j = blockIdx.x < (uint32_t)p.g0 ? 0 : 1;
+  const uint32_t g0 = (uint32_t)p.g0;
+  const uint32_t bid = j ? blockIdx.x - g0 : blockIdx.x;
+  const uint32_t G = j ? gridDim.x - g0 : g0;
+  lin_bwd_xs_body<K, DX, WG, ACC>(p.a[j], p.tab[j], p.n_tiles[j], bid, G);
+}
+
 }  // namespace
 
 int64_t xs_bwd_grid(int64_t n_rows) {
   return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_rows, 32), 256));
+}
+
+// the forward's grid: at least kFwdTilesPerBlock tiles per block (each block splits its W slice
+// once; at cfg5's ~48k-row blocks 8 tiles per block: 0.631 / 0.633 vs 0.635 / 0.637 ms per batch,
+// 16: 0.652; blocks of a million rows and more fill the 256 CUs either way)
+constexpr int64_t kFwdTilesPerBlock = 8;
+static int64_t xs_fwd_grid(int64_t n_tiles) {
+  return std::max<int64_t>(1, std::min<int64_t>(cdiv(n_tiles, kFwdTilesPerBlock), 256));
 }
 
 int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
@@ -583,7 +627,7 @@ int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
   const int K = a.k_total;
   const int64_t R = K == 256 ? 32 : 64;
   const int64_t n_tiles = cdiv(a.n, R);
-  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 256))), block(kThr);
+  const dim3 grid((unsigned)xs_fwd_grid(n_tiles)), block(kThr);
   if (K == 128) {
     if (a.add) hipLaunchKernelGGL((k_lin_fwd_xs<128, true>), grid, block, 0, stream, a, tab, n_tiles);
     else hipLaunchKernelGGL((k_lin_fwd_xs<128, false>), grid, block, 0, stream, a, tab, n_tiles);
@@ -592,6 +636,93 @@ int xs_linear_fwd(const LinArgs& a, const ChunkTab& tab, hipStream_t stream) {
     else hipLaunchKernelGGL((k_lin_fwd_xs<256, false>), grid, block, 0, stream, a, tab, n_tiles);
   }
   return check_launch("k_lin_fwd_xs");
+}
+
+// A two-job launch's grids: each job's own grid, scaled to one chip's worth (256 blocks, one per
+// CU) in tile proportion when they add up to more — the two jobs then run side by side instead of
+// the second waiting for the first's blocks.
+static void pair_grids(int64_t t0, int64_t t1, int64_t g0, int64_t g1, int64_t (&g)[2]) {
+  g[0] = g0;
+  g[1] = g1;
+  if (g0 + g1 > 256) {
+    g[0] = std::max<int64_t>(1, std::min<int64_t>(g0, (256 * t0 + (t0 + t1) / 2) / (t0 + t1)));
+    g[1] = std::max<int64_t>(1, std::min<int64_t>(g1, 256 - g[0]));
+  }
+}
+
+int xs_linear_fwd2(const LinArgs (&a)[2], const ChunkTab (&tab)[2], hipStream_t stream) {
+  if (a[0].n >= (int64_t(1) << 31) || a[1].n >= (int64_t(1) << 31))
+    return fail(HGNN_E_UNSUPPORTED, "k_lin_fwd_xs2: n >= 2^31 rows");
+  const int K = a[0].k_total;
+  const int64_t R = K == 256 ? 32 : 64;
+  XsPair p;
+  int64_t g[2], own[2];
+  for (int j = 0; j < 2; ++j) {
+    p.a[j] = a[j];
+    p.tab[j] = tab[j];
+    p.n_tiles[j] = cdiv(a[j].n, R);
+    own[j] = xs_fwd_grid(p.n_tiles[j]);
+  }
+  pair_grids(p.n_tiles[0], p.n_tiles[1], own[0], own[1], g);
+  p.g0 = g[0];
+  const dim3 grid((unsigned)(g[0] + g[1])), block(kThr);
+  const bool add = a[0].add != nullptr;
+  if (K == 128) {
+    if (add) hipLaunchKernelGGL((k_lin_fwd_xs2<128, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((k_lin_fwd_xs2<128, false>), grid, block, 0, stream, p);
+  } else {
+    if (add) hipLaunchKernelGGL((k_lin_fwd_xs2<256, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((k_lin_fwd_xs2<256, false>), grid, block, 0, stream, p);
+  }
+  return check_launch("k_lin_fwd_xs2");
+}
+
+int xs_bwd_class(const LinArgs& a, const ChunkTab& tab, bool dx) {
+  bool acc = false;
+  for (int c = 0; c < a.k_total / 16; ++c) acc |= tab.dx[c] && ((tab.dx_acc >> c) & 1u);
+  return (dx ? 1 : 0) | (a.slab ? 2 : 0) | (acc && dx ? 4 : 0);
+}
+
+int xs_linear_bwd2(const LinArgs (&a)[2], const ChunkTab (&tab)[2], bool dx, int (&grid_out)[2],
+                   hipStream_t stream) {
+  if (a[0].n >= (int64_t(1) << 31) || a[1].n >= (int64_t(1) << 31))
+    return fail(HGNN_E_UNSUPPORTED, "k_lin_bwd_xs2: n >= 2^31 rows");
+  const int K = a[0].k_total;
+  const int cls = xs_bwd_class(a[0], tab[0], dx);
+  if (cls != xs_bwd_class(a[1], tab[1], dx) || K != a[1].k_total)
+    return fail(HGNN_E_ARG, "k_lin_bwd_xs2: the two jobs differ in K or variant");
+  XsPair p;
+  int64_t g[2];
+  for (int j = 0; j < 2; ++j) {
+    p.a[j] = a[j];
+    p.tab[j] = tab[j];
+    p.n_tiles[j] = cdiv(a[j].n, 32);
+  }
+  pair_grids(p.n_tiles[0], p.n_tiles[1], xs_bwd_grid(a[0].n), xs_bwd_grid(a[1].n), g);
+  p.g0 = g[0];
+  grid_out[0] = (int)g[0];
+  grid_out[1] = (int)g[1];
+  const bool wg = (cls & 2) != 0, acc = (cls & 4) != 0;
+  const dim3 grid((unsigned)(g[0] + g[1])), block(kThr);
+#define HGNN_BXS2(KV, DXV, WGV, ACCV) \
+  hipLaunchKernelGGL((k_lin_bwd_xs2<KV, DXV, WGV, ACCV>), grid, block, 0, stream, p)
+  if (K == 128 && dx) {
+    if (wg) { if (acc) HGNN_BXS2(128, true, true, true); else HGNN_BXS2(128, true, true, false); }
+    else { if (acc) HGNN_BXS2(128, true, false, true); else HGNN_BXS2(128, true, false, false); }
+  } else if (K == 128) {
+    HGNN_BXS2(128, false, true, false);
+  } else {
+    if (dx) {
+      if (acc) HGNN_BXS2(256, true, false, true); else HGNN_BXS2(256, true, false, false);
+      if (int rc = check_launch("k_lin_bwd_xs2")) return rc;
+    }
+    if (wg) {
+      p.a[0].dz_out = p.a[1].dz_out = nullptr;   // the dgrad pass wrote it
+      HGNN_BXS2(256, false, true, false);
+    }
+  }
+#undef HGNN_BXS2
+  return check_launch("k_lin_bwd_xs2");
 }
 
 int xs_linear_bwd(const LinArgs& a, const ChunkTab& tab, bool dx, int* grid_out,

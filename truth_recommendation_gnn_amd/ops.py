@@ -397,6 +397,91 @@ def linear_bwd(segs, w, dout, out_act, dxs: Sequence[Optional[torch.Tensor]], ne
     return dw, db
 
 
+def linear_fwd_many(jobs) -> List[torch.Tensor]:
+    """:func:`linear_fwd` (no ``add``) of each ``(segs, w, b, relu, mask_out)`` job in one native
+    call (``hgnn_linear_fwd_multi``): a sampled layer's two destination types on the K = 384 /
+    512 split path share each column block's launch; anything else runs job by job there."""
+    if len(jobs) == 1 or len({int(j[1].shape[0]) for j in jobs}) > 1:   # (one output width)
+        return [linear_fwd(segs, w, b, relu, mask_out=mk) for segs, w, b, relu, mk in jobs]
+    outs, n_seg, xs, ks, rows, ws_, bs, relus, mks = [], [], [], [], [], [], [], [], []
+    nb = fl = 0
+    for segs, w, b, relu, mk in jobs:
+        n, h = int(segs[0].shape[0]), int(w.shape[0])
+        k = [int(s_.shape[1]) for s_ in segs]
+        if w.shape[1] != sum(k):
+            raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(k)}")
+        _check_rows(segs, n, "linear_fwd_many")
+        if b is not None and b.numel() != h:
+            raise ValueError(f"linear_fwd_many: bias has {b.numel()} entries, expected {h}")
+        out = torch.empty(n, h, dtype=torch.float32, device=w.device)
+        outs.append(out)
+        n_seg.append(len(segs)); xs.extend(segs); ks.extend(k); rows.append(n)
+        ws_.append(w); bs.append(b); relus.append(1 if relu else 0); mks.append(mk)
+        nb += 4 * n * (sum(k) + h) + (16 * n if mk is not None else 0)
+        fl += 2 * n * sum(k) * h
+    dev = jobs[0][1].device
+    h = int(jobs[0][1].shape[0])
+    with _timed(f"linear_fwd_multi[{'+'.join(str(r) for r in rows)}x{sum(ks) // len(jobs)}->{h}]",
+                nb, flops=fl):
+        N.check(N.lib().hgnn_linear_fwd_multi(
+            len(jobs), N.int_array(n_seg), N.ptr_array(xs), N.int_array(ks), N.i64_array(rows),
+            N.ptr_array(ws_), h, N.ptr_array(bs), N.int_array(relus), N.ptr_array(outs),
+            N.ptr_array(mks), N.stream_ptr(dev)), "hgnn_linear_fwd_multi")
+    return outs
+
+
+def linear_bwd_many(jobs):
+    """:func:`linear_bwd` (no ``dz_out``, no ``dx_add``) of each ``(segs, w, dout, out_act, dxs,
+    need_w, need_b, mask)`` job in one native call (``hgnn_linear_bwd_multi``); returns the
+    ``(dw, db)`` of each."""
+    if len(jobs) == 1 or len({int(j[1].shape[0]) for j in jobs}) > 1:
+        return [linear_bwd(segs, w, dout, out_act, dxs, need_w, need_b, mask=mk)
+                for segs, w, dout, out_act, dxs, need_w, need_b, mk in jobs]
+    n_seg, xs, ks, rows, kt, ws_, douts, outs, mks, dxs_all, dws, dbs = ([] for _ in range(12))
+    nb = fl = 0
+    h = int(jobs[0][1].shape[0])
+    for segs, w, dout, out_act, dxs, need_w, need_b, mk in jobs:
+        n = int(segs[0].shape[0])
+        k = [int(s_.shape[1]) for s_ in segs]
+        if w.shape[1] != sum(k):
+            raise ValueError(f"weight has {w.shape[1]} input columns, segments sum to {sum(k)}")
+        _check_rows(segs, n, "linear_bwd_many")
+        for what, t in (("dout", dout), ("out_act", out_act)):
+            if t is not None and tuple(t.shape) != (n, h):
+                raise ValueError(f"linear_bwd_many: {what} is {tuple(t.shape)}, expected {(n, h)}")
+        if len(dxs) != len(segs):
+            raise ValueError(f"linear_bwd_many: {len(dxs)} dx buffers for {len(segs)} segments")
+        for s_, dx in zip(segs, dxs):
+            if dx is not None and tuple(dx.shape) != tuple(s_.shape):
+                raise ValueError(f"linear_bwd_many: dx {tuple(dx.shape)} for a "
+                                 f"{tuple(s_.shape)} segment")
+        if mk is not None and tuple(mk.shape) != (n, 4):
+            raise ValueError(f"linear_bwd_many: ReLU bits are {tuple(mk.shape)}, expected {(n, 4)}")
+        n_seg.append(len(segs)); xs.extend(segs); ks.extend(k); rows.append(n); kt.append(sum(k))
+        ws_.append(w); douts.append(dout); outs.append(out_act)
+        mks.append(mk if out_act is not None else None); dxs_all.extend(dxs)
+        dws.append(torch.empty_like(w) if need_w else None)
+        dbs.append(torch.empty(h, dtype=torch.float32, device=w.device) if need_b else None)
+        k_dx = sum(kk for kk, dx in zip(k, dxs) if dx is not None)
+        bits = mk is not None and out_act is not None
+        nb += 4 * n * (h + (h if out_act is not None and not bits else 0) + sum(k) + k_dx) + \
+            (16 * n if bits else 0)
+        fl += 2 * n * h * k_dx + (2 * n * sum(k) * h if need_w else 0)
+    dev = jobs[0][1].device
+    ws = None
+    if any(d is not None for d in dws + dbs):
+        ws = N.workspace(N.lib().hgnn_linear_bwd_multi_ws_bytes(
+            len(jobs), N.i64_array(rows), N.int_array(kt), h), dev)
+    with _timed(f"linear_bwd_multi[{'+'.join(str(r) for r in rows)}x{sum(kt) // len(jobs)}->{h}]",
+                nb, flops=fl):
+        N.check(N.lib().hgnn_linear_bwd_multi(
+            len(jobs), N.int_array(n_seg), N.ptr_array(xs), N.int_array(ks), N.i64_array(rows),
+            N.ptr_array(ws_), h, N.ptr_array(douts), N.ptr_array(outs), N.ptr_array(mks),
+            N.ptr_array(dxs_all), None, N.ptr_array(dws), N.ptr_array(dbs), N.ptr(ws),
+            0 if ws is None else ws.numel(), N.stream_ptr(dev)), "hgnn_linear_bwd_multi")
+    return list(zip(dws, dbs))
+
+
 # ----------------------------------------------------------------------------- fused weights
 def split_weight_grads(dW: torch.Tensor, db: Optional[torch.Tensor], ks: Sequence[int],
                        k_root: int, scales: Sequence[float],
@@ -762,17 +847,24 @@ class _HeteroLayer(torch.autograd.Function):
             # falls back to one launch each where they do not qualify)
             many = iter(gather_mean_many([(xs[src], csr) for g in spec.groups
                                           for src, csr in g.rels]))
-        for gi, g in enumerate(spec.groups):   # destination types are independent chains
+        if many is not None:
+            # and every destination type's K3 in one native call (the split path's column blocks
+            # one launch for both types, hgnn_linear_fwd_multi)
+            jobs = []
+            for gi, g in enumerate(spec.groups):
+                w, b = wb[2 * gi], wb[2 * gi + 1]
+                aggrs = [next(many) for _ in g.rels]
+                segs = aggrs + ([_root(g, xs)] if g.root else [])
+                mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev,
+                                   sum(int(t.shape[1]) for t in segs))
+                jobs.append((segs, w.contiguous(), None if b is None else b.contiguous(), g.relu,
+                             mk))
+                aggrs_by_g[gi], masks[gi] = aggrs, mk
+            outs = linear_fwd_many(jobs)
+        for gi, g in enumerate(spec.groups if many is None else ()):   # independent chains
             w, b = wb[2 * gi], wb[2 * gi + 1]
             with lanes.ctx(gi):
-                if many is not None:
-                    aggrs = [next(many) for _ in g.rels]
-                    segs = aggrs + ([_root(g, xs)] if g.root else [])
-                    mk = relu_mask_for(segs[0].shape[0], int(w.shape[0]), g.relu, dev,
-                                       sum(int(t.shape[1]) for t in segs))
-                    y = linear_fwd(segs, w.contiguous(), None if b is None else b.contiguous(),
-                                   g.relu, mask_out=mk)
-                elif any(g.pre):
+                if any(g.pre):
                     # pre-projected relations: P = x_src W_r^T, gathered (means summed into
                     # one [N_dst, h] input) and added in the destination update's epilogue
                     cols = _group_columns(g, xs)
@@ -870,6 +962,14 @@ class _HeteroLayer(torch.autograd.Function):
                            if need_x[_root_type(g)] else None)
             jobs.append((gi, g, segs, w, dout.contiguous(), dxs, need_w, need_b))
         lanes = _Lanes(saved[0].device, len(jobs))
+        if one_lane and lanes.side is None:
+            # one native call for the destination types' K3 backward (hgnn_linear_bwd_multi)
+            res = linear_bwd_many([(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w,
+                                    need_b, ctx.masks[gi])
+                                   for gi, g, segs, w, dout, dxs, need_w, need_b in jobs])
+            for (gi, *_), (dw, db) in zip(jobs, res):
+                gwb[2 * gi], gwb[2 * gi + 1] = dw, db
+            jobs = []
         for li, (gi, g, segs, w, dout, dxs, need_w, need_b) in enumerate(jobs):
             with lanes.ctx(li):
                 dw, db = linear_bwd(segs, w, dout, outs[gi] if g.relu else None, dxs, need_w,
