@@ -1,5 +1,6 @@
 #!/bin/bash
-# cfg5: the K = 384 blocks below N rows on the general K3 kernels instead of the split pair (A/B).
+# cfg5: the K = 384 blocks below N rows on the general K3 kernels instead of the split pair (A/B;
+# the HGNN_XS_WIDE_MIN_ROWS switch it set was removed once the pair path made 0 the better value).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 for n in ${MINS:-0 8192 0 8192 65536}; do

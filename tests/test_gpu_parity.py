@@ -1270,21 +1270,22 @@ def test_gather_multi_equals_single_calls(d):
         assert torch.equal(o, r)
 
 
-@pytest.mark.parametrize("case", ["pair", "pair_root", "k_differs", "small"])
+@pytest.mark.parametrize("case", ["pair", "pair_root", "small", "k_differs", "w_differs"])
 def test_linear_multi_equals_per_job_calls(case):
     """hgnn_linear_fwd_multi / hgnn_linear_bwd_multi (a sampled layer's two destination types'
     K3 as one launch per column block, round 6) against one hgnn_linear_fwd_mask /
     hgnn_linear_bwd_ex call per job.  The forward's rows, the ReLU bits and dX do not depend on
     the grid: bitwise.  dW / db are the same partial sums over a different block split (the pair
     shares one chip's worth of blocks): within 2e-6 of the largest entry.  'k_differs' (K = 384
-    beside K = 512) and 'small' (blocks under the split path's 8192 rows) run job by job:
-    bitwise throughout."""
+    beside K = 512) and 'w_differs' (one job without weight gradients: a different kernel
+    variant) run job by job: bitwise throughout."""
     gen = torch.Generator().manual_seed(7)
     h = 128
     shapes = {"pair": [(9000, [128, 128, 128]), (12345, [128, 128, 128])],
               "pair_root": [(8192, [128, 128, 128]), (20000, [128, 128, 128])],
               "k_differs": [(9000, [128, 128, 128]), (10000, [128, 128, 128, 128])],
-              "small": [(3000, [128, 128, 128]), (2500, [128, 128, 128])]}[case]
+              "small": [(3000, [128, 128, 128]), (2500, [128, 128, 128])],
+              "w_differs": [(9000, [128, 128, 128]), (7000, [128, 128, 128])]}[case]
     jobs_f, ref_f = [], []
     for n, ks in shapes:
         segs = [torch.randn(n, k, generator=gen).to(DEV) for k in ks]
@@ -1301,22 +1302,25 @@ def test_linear_multi_equals_per_job_calls(case):
             assert torch.equal(mk, mr)
     # backward: dX of the first two segments; the root segment's dX only in 'pair_acc_root'
     jobs_b, ref_b = [], []
-    for (segs, w, b, _, mk), o in zip(jobs_f, outs):
+    for i, ((segs, w, b, _, mk), o) in enumerate(zip(jobs_f, outs)):
         dout = torch.randn(o.shape, generator=gen).to(DEV)
         root = case == "pair_root"
         dxs = [torch.empty_like(s_) for s_ in segs[:2]] + \
             [torch.empty_like(s_) if root else None for s_ in segs[2:]]
         dxs_ref = [None if d is None else torch.empty_like(d) for d in dxs]
-        jobs_b.append((segs, w, dout, o, dxs, True, True, mk))
-        ref_b.append((ops.linear_bwd(segs, w, dout, o, dxs_ref, True, True, mask=mk), dxs_ref))
+        need = not (case == "w_differs" and i == 1)
+        jobs_b.append((segs, w, dout, o, dxs, need, need, mk))
+        ref_b.append((ops.linear_bwd(segs, w, dout, o, dxs_ref, need, need, mask=mk), dxs_ref))
     got = ops.linear_bwd_many(jobs_b)
     for (dw, db), ((rdw, rdb), dxs_ref), job in zip(got, ref_b, jobs_b):
         for d, r in zip(job[4], dxs_ref):
             if d is not None:
                 assert torch.equal(d, r)
-        exact = case in ("k_differs", "small")
+        exact = case in ("k_differs", "w_differs")
         for a, r in ((dw, rdw), (db, rdb)):
-            if exact:
+            if r is None:
+                assert a is None
+            elif exact:
                 assert torch.equal(a, r)
             else:
                 tol = 2e-6 * float(r.abs().max())

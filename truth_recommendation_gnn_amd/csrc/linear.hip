@@ -1297,20 +1297,13 @@ static ChunkTab chunk_table(const LinArgs& a) { return chunk_table_range(a, 0, a
 // and applies the bias, activation and mask; the backward runs each block's dgrad / wgrad into
 // its columns of one shared [G][h][K + 1] slab, reduced once.  Replaces the f32-input general
 // kernels there (51 / 65 us per launch at cfg5's ~17k rows).
-// Blocks of fewer rows stay on the general kernels: at cfg5's inner blocks (2-3k rows) the
-// split pair's forward (2 launches) and backward (3 + reduce) cost the same time as the general
-// kernels' fewer launches (0.680 vs 0.677 ms per batch, A/B), so the replay is 4 nodes shorter;
-// the outer blocks (~48k rows) keep the split (all on the general kernels: 0.869 ms).
-// HGNN_XS_WIDE_MIN_ROWS overrides (A/B).
-static int64_t xs_wide_min_rows() {
-  static const int64_t v = getenv("HGNN_XS_WIDE_MIN_ROWS") ? atoll(getenv("HGNN_XS_WIDE_MIN_ROWS"))
-                                                           : 8192;
-  return v;
-}
-
+// Blocks of every size take it: at cfg5's inner blocks (2-3k rows) the general kernels measured
+// the same time one destination type at a time (0.680 vs 0.677 ms per batch, 4 launches fewer),
+// but with both types paired into one launch per column block (hgnn_linear_fwd_multi) the split
+// kernels are faster: 0.603 / 0.604 vs 0.622 / 0.621 ms per batch, 22 vs 24 launches
+// (profiles/r6_wide_min_ab.txt).
 static bool xs_wide_ok(const LinArgs& a, bool vec) {
-  if (!vec || a.h != 128 || a.k_total <= 256 || a.k_total > 512 || a.k_total % 128 != 0 ||
-      a.n < xs_wide_min_rows())
+  if (!vec || a.h != 128 || a.k_total <= 256 || a.k_total > 512 || a.k_total % 128 != 0)
     return false;
   for (int s = 0; s < a.n_seg; ++s)
     if (a.seg[s].k % 16) return false;
