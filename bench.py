@@ -52,7 +52,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from truth_recommendation_gnn_amd import HeteroSAGE, synth  # noqa: E402
-from truth_recommendation_gnn_amd import parallel  # noqa: E402
+from truth_recommendation_gnn_amd import optim, parallel  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
 FP32_MFMA_PEAK_TFS = 157.3  # same table: dense fp32 matrix (v_mfma_f32_16x16x4_f32), no xf32 on gfx950
@@ -113,6 +113,9 @@ def parse(argv=None):
     p.add_argument("--default-priority", action="store_true",
                    help="cfg5 mini-batch: replay on a default-priority stream (by default the "
                         "steps run on a high-priority one, above the side stream's sampling)")
+    p.add_argument("--native-adam", action="store_true",
+                   help="optim.Adam (one native launch over every parameter) instead of "
+                        "torch.optim.Adam(fused=True)")
     p.add_argument("--eager-sampler", action="store_true",
                    help="cfg5 mini-batch: sample with the eager NeighborSampler (host-sized "
                         "launches, read-backs) and stage its batches, instead of the sync-free "
@@ -645,9 +648,10 @@ def _run_full_batch(args, dev, world, rank, local, sharded, impl):
             h_u, h_p = shard.forward(model, x_user, x_post, wait=False, x_user_full=x_user_full)
             return shard.loss(h_u, h_p, negatives(), neg_order="user")
 
-    # the reference's optimizer (train_gnn.py:207, Adam lr 0.001); on the GPU torch's fused
-    # kernel: one launch for every parameter instead of a multi-tensor chain per Adam stage
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=not on_cpu)
+    # the reference's optimizer (train_gnn.py:207, Adam lr 0.001); on the GPU one native launch
+    # over every parameter with --native-adam (optim.Adam), else torch's fused kernel
+    opt = (optim.Adam(model.parameters(), lr=1e-3) if not on_cpu and args.native_adam
+           else torch.optim.Adam(model.parameters(), lr=1e-3, fused=not on_cpu))
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -1034,7 +1038,12 @@ def _run_minibatch(args, dev, world, rank, local, sharded, impl):
     # blocks (minibatch.py); the sampler stays eager (two syncs per hop).  N > 1: the forward +
     # loss + backward graph, the eager all-reduce of the gradients, then the Adam graph.
     use_graph = not args.no_graph
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
+    # the reference's Adam (train_gnn.py:207); --native-adam: one native launch over every
+    # parameter, its step count on the device (optim.Adam: one graph node; torch's capturable
+    # fused Adam: two)
+    opt = (torch.optim.Adam(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
+           if not args.native_adam or torch.device(dev).type != "cuda"
+           else optim.Adam(model.parameters(), lr=1e-3))
     gen = torch.Generator(device=dev).manual_seed(0)
     gen_neg = torch.Generator(device=dev).manual_seed(1)
     # link prediction as a link loader does it: one shuffle of the positive (engages) edges per

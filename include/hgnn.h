@@ -274,6 +274,15 @@ int hgnn_linear_bwd_multi(int32_t n_jobs, const int32_t* n_seg, const float* con
                           const uint32_t* const* mask, float* const* dxs,
                           const uint32_t* dx_accumulate, float* const* dw, float* const* db,
                           void* ws, size_t ws_bytes, hgnn_stream_t stream);
+/* Adam (torch.optim.Adam, the reference's optimizer: train_gnn.py:207) over n_tensors fp32
+ * parameters in one launch (per 32 tensors): p, m, v updated in place from g.  step: one device
+ * float, the steps done so far — the launch uses step + 1 and writes it back once every block has
+ * read it (capturable: no host value); done: one device uint32, zero between launches (the
+ * launch leaves it zero).  One update per (step, done) pair in flight. */
+int hgnn_adam_multi(int32_t n_tensors, float* const* params, const float* const* grads,
+                    float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                    float* step, uint32_t* done, double lr, double beta1, double beta2, double eps,
+                    double weight_decay, hgnn_stream_t stream);
 int hgnn_linear_bwd(int32_t n_seg, const float* const* xs, const int32_t* ks, int64_t n_rows,
                     const float* w, int32_t h, const float* dout, const float* out,
                     float* const* dxs, float* dw, float* db, void* ws, size_t ws_bytes,

@@ -1325,3 +1325,62 @@ def test_linear_multi_equals_per_job_calls(case):
             else:
                 tol = 2e-6 * float(r.abs().max())
                 assert float((a - r).abs().max()) <= tol, (float((a - r).abs().max()), tol)
+
+
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_adam_matches_torch(wd):
+    """optim.Adam (hgnn_adam_multi: every parameter in one launch, the step count on the device)
+    against torch.optim.Adam(fused=True) over 6 steps with the same gradients: 40 tensors (two
+    launches of 32), odd sizes, an empty one; then a recorded step replayed 3 times against 3
+    eager steps, bitwise, and the device step count."""
+    from truth_recommendation_gnn_amd import optim
+    gen = torch.Generator().manual_seed(11)
+    shapes = [(128, 384), (128,), (7,), (0,), (33, 5)] * 8
+    init = [torch.randn(s, generator=gen) for s in shapes]
+    ours = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    ref = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    opt = optim.Adam(ours, lr=1e-3, weight_decay=wd)
+    opt_ref = torch.optim.Adam(ref, lr=1e-3, weight_decay=wd, fused=True)
+    for _ in range(6):
+        grads = [torch.randn(s, generator=gen).to(DEV) for s in shapes]
+        for p, q, g in zip(ours, ref, grads):
+            p.grad = g.clone()
+            q.grad = g.clone()
+        opt.step()
+        opt_ref.step()
+    assert opt.steps_done() == 6
+    worst = 0.0
+    for p, q in zip(ours, ref):
+        if p.numel():
+            worst = max(worst, float((p - q).abs().max() / q.abs().max().clamp_min(1e-30)))
+    assert worst <= 1e-6, worst
+    # recorded: one eager step done above; capture one step and replay it 3 times
+    twin = [torch.nn.Parameter(p.detach().clone()) for p in ours]
+    opt_twin = optim.Adam(twin, lr=1e-3, weight_decay=wd)
+    for p, q in zip(ours, twin):
+        q.grad = p.grad.clone()
+    opt_twin.step()                                    # the twin's state: 1 step
+    for p, q in zip(ours, twin):                      # ours: 6 steps; restart both from equal
+        q.data.copy_(p.data)
+        opt_twin.state[q]["exp_avg"].copy_(opt.state[p]["exp_avg"])
+        opt_twin.state[q]["exp_avg_sq"].copy_(opt.state[p]["exp_avg_sq"])
+    opt_twin.param_groups[0]["_dev_state"][0].fill_(6.0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            opt_twin.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for _ in range(3):
+        grads = [torch.randn(sh, generator=gen).to(DEV) for sh in shapes]
+        for p, q, gr in zip(ours, twin, grads):
+            p.grad.copy_(gr)
+            q.grad.copy_(gr)
+        opt.step()
+        g.replay()
+    torch.cuda.synchronize()
+    assert opt.steps_done() == 9 and opt_twin.steps_done() == 9
+    for p, q in zip(ours, twin):
+        assert torch.equal(p, q)

@@ -55,6 +55,9 @@ _SIGS = {
                                       _p, _p, _p, _c_sz, _p]),
     "hgnn_linear_bwd_ex": (_c_i32, [_c_i32, _p, _p, _c_i64, _p, _c_i32, _p, _p, _p, _p,
                                     ctypes.c_uint32, _p, _p, _p, _p, _c_sz, _p]),
+    "hgnn_adam_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _p, _p, ctypes.c_double,
+                                 ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                 ctypes.c_double, _p]),
     "hgnn_linear_fwd_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _c_i32, _p, _p, _p, _p, _p]),
     "hgnn_linear_bwd_multi_ws_bytes": (_c_sz, [_c_i32, _p, _p, _c_i32]),
     "hgnn_linear_bwd_multi": (_c_i32, [_c_i32, _p, _p, _p, _p, _p, _c_i32, _p, _p, _p, _p, _p,
