@@ -5,8 +5,8 @@
 // (bench.py, minibatch.CapturedStep) replays it inside the recorded graph.  torch's capturable
 // fused Adam is two launches there — a multi-tensor add for the step tensors, then the update
 // over 48 blocks of 12288 threads (20 us for cfg5's 264k parameters, most of it launch-bound).
-// Here every block runs a slice of the concatenated parameters and the last block to finish
-// writes the new step, so the replay has one node and the chip's width.
+// Here every block runs 1024 elements of one tensor and the last block to finish writes the new
+// step, so the replay has one node and the chip's width.
 //
 // The arithmetic follows torch's fused kernel (ATen fused_adam_utils.cuh, the ORIGINAL mode):
 // the hyper-parameters are doubles, so beta1 * m, (1 - beta1) * g, the v update, lr / bc1 and
@@ -19,13 +19,15 @@
 namespace hgnn {
 
 constexpr int kAdamMaxTensors = 32;
+constexpr int kAdamPer = 4;   // elements per thread
 
 struct AdamArgs {
   float* p[kAdamMaxTensors];
   const float* g[kAdamMaxTensors];
   float* m[kAdamMaxTensors];
   float* v[kAdamMaxTensors];
-  int64_t off[kAdamMaxTensors + 1];   // prefix sums of the tensors' sizes
+  int64_t numel[kAdamMaxTensors];
+  int32_t blk[kAdamMaxTensors + 1];   // prefix sums of the tensors' block counts
   int32_t n;
   double lr, beta1, beta2, eps, weight_decay;
   float* step;        // [1] steps done so far (the launch uses step + 1)
@@ -38,34 +40,47 @@ __global__ void __launch_bounds__(256) k_adam_multi(const AdamArgs a) {
   const float bc1 = (float)(1.0 - pow(a.beta1, (double)t));
   const float bc2_sqrt = (float)sqrt(1.0 - pow(a.beta2, (double)t));
   const float step_size = (float)(a.lr / (double)bc1);
-  const int64_t total = a.off[a.n];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    int lo = 0, hi = a.n - 1;   // the tensor holding element e: off[lo] <= e < off[lo + 1]
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (a.off[mid] <= e) lo = mid;
-      else hi = mid - 1;
+  // the block's tensor: uniform (from blockIdx), so its pointers are scalar loads — a per-element
+  // search over a flat index made them per-lane and measured slower than torch's kernel
+  int lo = 0, hi = a.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.blk[mid] <= (int)blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  float* __restrict__ P = a.p[lo];
+  const float* __restrict__ Gr = a.g[lo];
+  float* __restrict__ M = a.m[lo];
+  float* __restrict__ V = a.v[lo];
+  const int64_t n = a.numel[lo];
+  const int64_t base = (int64_t)(blockIdx.x - a.blk[lo]) * (256 * kAdamPer);
+#pragma unroll
+  for (int k = 0; k < kAdamPer; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i < n) {
+      float p = P[i];
+      float g = Gr[i];
+      if (a.weight_decay != 0.0) g = (float)((double)g + (double)p * a.weight_decay);
+      float m = M[i], v = V[i];
+      m = (float)(a.beta1 * (double)m + (1.0 - a.beta1) * (double)g);
+      v = (float)(a.beta2 * (double)v + (1.0 - a.beta2) * (double)g * (double)g);
+      const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + a.eps);
+      p -= step_size * m / denom;
+      P[i] = p;
+      M[i] = m;
+      V[i] = v;
     }
-    const int64_t i = e - a.off[lo];
-    float p = a.p[lo][i];
-    float g = a.g[lo][i];
-    if (a.weight_decay != 0.0) g = (float)((double)g + (double)p * a.weight_decay);
-    float m = a.m[lo][i], v = a.v[lo][i];
-    m = (float)(a.beta1 * (double)m + (1.0 - a.beta1) * (double)g);
-    v = (float)(a.beta2 * (double)v + (1.0 - a.beta2) * (double)g * (double)g);
-    const float denom = (float)((double)(sqrtf(v) / bc2_sqrt) + a.eps);
-    p -= step_size * m / denom;
-    a.p[lo][i] = p;
-    a.m[lo][i] = m;
-    a.v[lo][i] = v;
   }
   if (!a.advance) return;
   // every block read the old step above; the last one to get here writes the new one
   __shared__ bool last;
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
+    // only the order "this block read the step, then counted itself" matters (no block reads
+    // another's data): a workgroup-scope fence waits for the block's own accesses, where a
+    // device-scope one would write the XCD's L2 back on every block
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     last = atomicAdd(a.done, 1u) == gridDim.x - 1;
   }
   __syncthreads();
@@ -93,7 +108,7 @@ int hgnn_adam_multi(int32_t n_tensors, float* const* params, const float* const*
   for (int c0 = 0; c0 < n_tensors; c0 += kAdamMaxTensors) {   // tensors in launches of 32
     AdamArgs a{};
     a.n = std::min(kAdamMaxTensors, n_tensors - c0);
-    a.off[0] = 0;
+    a.blk[0] = 0;
     for (int j = 0; j < a.n; ++j) {
       const int t = c0 + j;
       if (numel[t] < 0 || (numel[t] > 0 && (!params[t] || !grads[t] || !exp_avg[t] ||
@@ -103,14 +118,20 @@ int hgnn_adam_multi(int32_t n_tensors, float* const* params, const float* const*
       a.g[j] = grads[t];
       a.m[j] = exp_avg[t];
       a.v[j] = exp_avg_sq[t];
-      a.off[j + 1] = a.off[j] + numel[t];
+      a.numel[j] = numel[t];
+      const int64_t nb = cdiv(numel[t], 256 * kAdamPer);
+      if ((int64_t)a.blk[j] + nb > (int64_t(1) << 30))
+        return fail(HGNN_E_UNSUPPORTED, "adam_multi: too many elements in one launch");
+      a.blk[j + 1] = a.blk[j] + (int32_t)nb;
     }
     a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps; a.weight_decay = weight_decay;
     a.step = step;
     a.done = done;
     a.advance = c0 + kAdamMaxTensors >= n_tensors ? 1 : 0;
-    const int64_t total = a.off[a.n];
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(total, 256), 2048));
+    if (a.blk[a.n] == 0) {   // nothing to update: the step still advances (torch's does)
+      a.blk[a.n] = 1;
+    }
+    const unsigned grid = (unsigned)a.blk[a.n];
     hipLaunchKernelGGL(k_adam_multi, dim3(grid), dim3(256), 0, stream, a);
     if (int rc = check_launch("k_adam_multi")) return rc;
   }
